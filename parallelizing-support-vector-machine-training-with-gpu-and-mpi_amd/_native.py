@@ -1,0 +1,190 @@
+"""ctypes bindings to the native runtime (``lib/libsvm355_core.so`` and ``lib/libsvm355_hip.so``).
+
+The C ABI is declared in ``csrc/include/svm355.h`` and ``csrc/include/svm355_device.h``.  The
+libraries are built in-tree by :mod:`svm355.build`; the CPU core is rebuilt on demand when it is
+missing (g++ only, a few seconds), the device library must have been built beforehand (hipcc).
+Every failing native call raises :class:`NativeError` carrying ``svm_last_error()``; there is no
+silent fallback from the device library to anything else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_uint64, c_void_p
+from pathlib import Path
+
+LIB_DIR = Path(__file__).resolve().parent / "lib"
+
+_lock = threading.Lock()
+_core = None
+_hip = None
+
+STOP_NAMES = {
+    0: "running",
+    1: "converged",
+    2: "no_candidate",
+    3: "infeasible",
+    4: "nonpositive_eta",
+    5: "max_iter",
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class SvmParams(ctypes.Structure):
+    _fields_ = [
+        ("C", c_double),
+        ("gamma", c_double),
+        ("tau", c_double),
+        ("eps", c_double),
+        ("sv_tol", c_double),
+        ("max_iter", c_int64),
+        ("n_threads", c_int32),
+        ("verbose", c_int32),
+    ]
+
+
+class SvmResult(ctypes.Structure):
+    _fields_ = [
+        ("iterations", c_int64),
+        ("b", c_double),
+        ("b_high", c_double),
+        ("b_low", c_double),
+        ("stop_reason", c_int32),
+        ("reserved", c_int32),
+        ("n_sv", c_int64),
+        ("seconds", c_double),
+    ]
+
+
+class SvmdTiming(ctypes.Structure):
+    _fields_ = [
+        ("h2d_ms", c_double),
+        ("preprocess_ms", c_double),
+        ("gram_ms", c_double),
+        ("smo_ms", c_double),
+        ("total_ms", c_double),
+    ]
+
+
+_P = c_void_p  # raw pointers are passed as integers / c_void_p
+_CORE_SIGS = {
+    "svm_last_error": (c_char_p, []),
+    "svm_default_params": (None, [POINTER(SvmParams)]),
+    "svm_stop_message": (c_char_p, [c_int32]),
+    "svm_csv_load": (c_void_p, [c_char_p, c_int64, c_int32, c_int32]),
+    "svm_dataset_dims": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),
+    "svm_dataset_copy": (c_int32, [c_void_p, _P, _P, _P]),
+    "svm_dataset_free": (None, [c_void_p]),
+    "svm_csv_write": (c_int32, [c_char_p, _P, _P, c_int64, c_int64]),
+    "svm_synth_mnist": (c_int32, [c_uint64, c_int64, _P, _P, c_int32]),
+    "svm_minmax": (c_int32, [_P, c_int64, c_int64, _P, _P]),
+    "svm_scale": (c_int32, [_P, c_int64, c_int64, _P, _P]),
+    "svm_rbf": (c_double, [_P, _P, c_int64, c_double]),
+    "svm_rbf_matrix": (c_int32, [_P, c_int64, _P, c_int64, c_int64, c_double, _P, c_int32]),
+    "svm_smo_train": (c_int32, [_P, _P, c_int64, c_int64, _P, c_int32, POINTER(SvmParams),
+                                POINTER(SvmResult), _P, c_int64]),
+    "svm_smo_train_gram": (c_int32, [_P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
+                                     POINTER(SvmResult), _P, c_int64]),
+    "svm_decision": (c_int32, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_double, c_double, _P,
+                               c_int32]),
+    "svm_sv_indices": (c_int64, [_P, c_int64, c_double, _P]),
+    "svm_model_save": (c_int32, [c_char_p, _P, _P, _P, c_int64, c_double]),
+}
+
+_HIP_SIGS = {
+    "svmd_padded_dim": (c_int64, [c_int64]),
+    "svmd_device_count": (c_int32, [POINTER(c_int32)]),
+    "svmd_alloc": (c_void_p, [c_void_p, c_int64]),
+    "svmd_free": (None, [c_void_p, c_void_p]),
+    "svmd_memcpy_h2d": (c_int32, [c_void_p, _P, _P, c_int64]),
+    "svmd_memcpy_d2h": (c_int32, [c_void_p, _P, _P, c_int64]),
+    "svmd_create": (c_void_p, [c_int32]),
+    "svmd_destroy": (None, [c_void_p]),
+    "svmd_set_stream": (c_int32, [c_void_p, c_void_p]),
+    "svmd_synchronize": (c_int32, [c_void_p]),
+    "svmd_upload_rows": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, c_int64]),
+    "svmd_preprocess": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int32]),
+    "svmd_row_norms": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P]),
+    "svmd_rbf_gram": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
+                                c_double, _P, c_int64, c_int32]),
+    "svmd_smo": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
+                           POINTER(SvmResult), _P, c_int64]),
+    "svmd_train": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32,
+                             POINTER(SvmParams), POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming)]),
+    "svmd_decision": (c_int32, [c_void_p, _P, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
+                                c_double, c_double, _P]),
+    "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
+}
+
+
+def _bind(lib, sigs):
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def core():
+    """The CPU core library (built on demand)."""
+    global _core
+    if _core is not None:
+        return _core
+    with _lock:
+        if _core is None:
+            path = LIB_DIR / "libsvm355_core.so"
+            if not path.exists() or os.environ.get("SVM355_REBUILD"):
+                from . import build
+
+                build.build_core()
+            # RTLD_GLOBAL so the device library resolves the core's symbols from this copy.
+            _core = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), _CORE_SIGS)
+    return _core
+
+
+def hip():
+    """The HIP/gfx950 device library.  Raises if it is missing or cannot be loaded."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    core()
+    with _lock:
+        if _hip is None:
+            path = LIB_DIR / "libsvm355_hip.so"
+            if not path.exists():
+                raise NativeError(
+                    f"{path} is missing: build it with `python -m svm355.build` (hipcc, gfx950)")
+            try:
+                _hip = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), _HIP_SIGS)
+            except OSError as e:  # pragma: no cover - depends on the ROCm install
+                raise NativeError(f"cannot load {path}: {e}") from e
+    return _hip
+
+
+def last_error() -> str:
+    msg = core().svm_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = "native call") -> None:
+    if rc != 0:
+        raise NativeError(f"{what} failed (status {rc}): {last_error()}")
+
+
+def ptr(a) -> int:
+    """Raw address of a numpy array or torch tensor (contiguity is the caller's contract)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def params_struct(C=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, sv_tol=1e-8, max_iter=100000,
+                  n_threads=1, verbose=0) -> SvmParams:
+    return SvmParams(float(C), float(gamma), float(tau), float(eps), float(sv_tol), int(max_iter),
+                     int(n_threads), int(verbose))

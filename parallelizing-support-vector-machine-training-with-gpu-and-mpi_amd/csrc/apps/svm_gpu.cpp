@@ -1,0 +1,153 @@
+// svm_gpu — single-GPU SMO trainer/evaluator on MI355X (the reference's gpu_svm_main3.cu and
+// gpu_svm_main4.cu programs; the positional argument / --n-limit is gpu_svm4's train-size limit).
+//
+// Timing scopes follow gpu_svm_main3.cu:525-694:
+//   training   = H2D of X and y, min/max + scaling (+ row norms), RBF Gram on MFMA, SMO
+//   prediction = test CSV parse, H2D, scaling, decision over the SVs, accuracy, SV count
+// stdout lines match the reference order (accuracy printed before the SV count).
+#include <cstdio>
+
+#include "cli_common.h"
+#include "svm355_device.h"
+
+namespace {
+
+struct Dev {
+  void* ctx;
+  std::vector<void*> bufs;
+  void* alloc(long long bytes) {
+    void* p = svmd_alloc(ctx, bytes);
+    if (!p) {
+      fprintf(stderr, "%s\n", svm_last_error());
+      exit(1);
+    }
+    bufs.push_back(p);
+    return p;
+  }
+  ~Dev() {
+    for (void* p : bufs) svmd_free(ctx, p);
+    svmd_destroy(ctx);
+  }
+};
+
+#define CK(x)                                      \
+  do {                                             \
+    if ((x) != SVM_OK) {                           \
+      fprintf(stderr, "%s\n", svm_last_error());   \
+      return 1;                                    \
+    }                                              \
+  } while (0)
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  cli::Options o;
+  if (!cli::parse(argc, argv, o, 0)) return 2;
+  int32_t ndev = 0;
+  svmd_device_count(&ndev);
+  if (ndev < 1) {
+    fprintf(stderr, "svm_gpu: no HIP device visible\n");
+    return 1;
+  }
+  cli::Data tr;
+  if (!cli::load_split(o, true, tr)) return 1;
+  printf("n = %lld\n", tr.n);
+  printf("n_features = %lld\n", tr.d);
+  if (tr.n == 0) {
+    fprintf(stderr, "Error: No data read from file.\n");
+    return 1;
+  }
+  const long long n = tr.n, d = tr.d, ld = svmd_padded_dim(d);
+  Dev dev{svmd_create(0), {}};
+  if (!dev.ctx) {
+    fprintf(stderr, "%s\n", svm_last_error());
+    return 1;
+  }
+  // Input buffers are allocated (and the HIP runtime initialised) before the timer starts; the
+  // Gram matrix and solver workspace are allocated inside the timed region.
+  auto* Xd = static_cast<double*>(dev.alloc(n * ld * 8));
+  auto* yd = static_cast<int32_t*>(dev.alloc(n * 4));
+  auto* mn = static_cast<double*>(dev.alloc(d * 8));
+  auto* mx = static_cast<double*>(dev.alloc(d * 8));
+  auto* sqn = static_cast<double*>(dev.alloc(n * 8));
+  auto* alpha = static_cast<double*>(dev.alloc(n * 8));
+  CK(svmd_synchronize(dev.ctx));
+
+  const auto t0 = std::chrono::steady_clock::now();
+  CK(svmd_upload_rows(dev.ctx, tr.X.data(), n, d, Xd, ld));
+  CK(svmd_memcpy_h2d(dev.ctx, yd, tr.y.data(), n * 4));
+  CK(svmd_preprocess(dev.ctx, Xd, n, d, ld, mn, mx, sqn, 0));
+  svm_result r{};
+  svmd_timing tm{};
+  CK(svmd_train(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm));
+  CK(svmd_synchronize(dev.ctx));
+  const auto t1 = std::chrono::steady_clock::now();
+  if (r.stop_reason != SVM_STOP_CONVERGED) fprintf(stderr, "%s\n", svm_stop_message(r.stop_reason));
+  printf("number of iterations: %lld\n", (long long)r.iterations);
+  printf("b = %.15f\n", r.b);
+  printf("(b_high - b_low)/2*1e10 = %.15f\n", (r.b_high - r.b_low) / 2 * 1e10);
+
+  // ---- prediction scope
+  cli::Data te;
+  if (!cli::load_split(o, false, te)) return 1;
+  const long long m = te.n;
+  std::vector<double> ah(static_cast<size_t>(n));
+  CK(svmd_memcpy_d2h(dev.ctx, ah.data(), alpha, n * 8));
+  std::vector<int64_t> sv(static_cast<size_t>(n));
+  const int64_t nsv = svm_sv_indices(ah.data(), n, o.p.sv_tol, sv.data());
+  sv.resize(size_t(nsv));
+  long long correct = 0;
+  if (m > 0) {
+    auto* Xq = static_cast<double*>(dev.alloc(m * ld * 8));
+    auto* nq = static_cast<double*>(dev.alloc(m * 8));
+    auto* out = static_cast<double*>(dev.alloc(m * 8));
+    CK(svmd_upload_rows(dev.ctx, te.X.data(), m, d, Xq, ld));
+    CK(svmd_preprocess(dev.ctx, Xq, m, d, ld, mn, mx, nq, 1));
+    const long long ns = nsv > 0 ? nsv : 1;
+    auto* idx = static_cast<int64_t*>(dev.alloc(ns * 8));
+    auto* Xs = static_cast<double*>(dev.alloc(ns * ld * 8));
+    auto* nsq = static_cast<double*>(dev.alloc(ns * 8));
+    auto* coef = static_cast<double*>(dev.alloc(ns * 8));
+    std::vector<double> ch(size_t(ns), 0.0), nh(static_cast<size_t>(n));
+    CK(svmd_memcpy_d2h(dev.ctx, nh.data(), sqn, n * 8));
+    std::vector<double> nsh(size_t(ns), 0.0);
+    for (int64_t k = 0; k < nsv; ++k) {
+      ch[size_t(k)] = ah[size_t(sv[size_t(k)])] * tr.y[size_t(sv[size_t(k)])];
+      nsh[size_t(k)] = nh[size_t(sv[size_t(k)])];
+    }
+    if (nsv > 0) {
+      CK(svmd_memcpy_h2d(dev.ctx, idx, sv.data(), nsv * 8));
+      CK(svmd_gather_rows(dev.ctx, Xd, ld, idx, nsv, Xs));
+      CK(svmd_memcpy_h2d(dev.ctx, coef, ch.data(), nsv * 8));
+      CK(svmd_memcpy_h2d(dev.ctx, nsq, nsh.data(), nsv * 8));
+    }
+    CK(svmd_decision(dev.ctx, Xs, nsq, coef, nsv, ld, Xq, nq, m, ld, ld, o.p.gamma, r.b, out));
+    std::vector<double> dec(static_cast<size_t>(m));
+    CK(svmd_memcpy_d2h(dev.ctx, dec.data(), out, m * 8));
+    for (long long i = 0; i < m; ++i) correct += ((dec[size_t(i)] > 0 ? 1 : -1) == te.y[size_t(i)]);
+  }
+  printf("Test accuracy = %.15f (%lld/%lld)\n", m ? double(correct) / double(m) : 0.0, correct, m);
+  printf("Final SV count = %lld\n", (long long)nsv);
+  const auto t2 = std::chrono::steady_clock::now();
+  const double train_ms = cli::ms_between(t0, t1), pred_ms = cli::ms_between(t1, t2);
+  printf("The training time: %.3f milliseconds\n", train_ms);
+  printf("The prediction time: %.3f milliseconds\n", pred_ms);
+  printf("The elapsed time: %.3f milliseconds\n", train_ms + pred_ms);
+  if (!o.quiet)
+    fprintf(stderr, "[svm_gpu] gram %.3f ms, smo %.3f ms, iterations %lld\n", tm.gram_ms, tm.smo_ms,
+            (long long)r.iterations);
+  if (!o.model_dir.empty()) {
+    std::vector<int32_t> lab(static_cast<size_t>(nsv));
+    std::vector<double> as(static_cast<size_t>(nsv));
+    for (int64_t k = 0; k < nsv; ++k) {
+      lab[size_t(k)] = tr.y[size_t(sv[size_t(k)])];
+      as[size_t(k)] = ah[size_t(sv[size_t(k)])];
+    }
+    if (svm_model_save(o.model_dir.c_str(), sv.data(), lab.data(), as.data(), nsv, r.b) != SVM_OK)
+      fprintf(stderr, "%s\n", svm_last_error());
+  }
+  char extra[256];
+  snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f", tm.gram_ms, tm.smo_ms);
+  cli::write_json(o.json, "svm_gpu", o, n, d, r, correct, m, train_ms, pred_ms, train_ms + pred_ms, extra);
+  return 0;
+}

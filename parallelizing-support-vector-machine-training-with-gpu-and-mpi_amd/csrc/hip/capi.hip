@@ -1,0 +1,299 @@
+// C ABI of the device library: context management and the end-to-end device training path.
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+#include "svm355_device.h"
+
+using namespace svm355;
+
+namespace {
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+svm_params resolve(const svm_params* p) {
+  svm_params q;
+  if (p)
+    q = *p;
+  else
+    svm_default_params(&q);
+  return q;
+}
+
+}  // namespace
+
+extern "C" {
+
+SVM_API int64_t svmd_padded_dim(int64_t d) { return padded_dim(d); }
+
+SVM_API int svmd_device_count(int32_t* count) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  if (count) *count = c;
+  return SVM_OK;
+}
+
+SVM_API void* svmd_alloc(void* h, int64_t bytes) {
+  auto* ctx = static_cast<DeviceCtx*>(h);
+  if (!ctx || bytes < 0) return nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  const hipError_t e = hipMalloc(&p, size_t(bytes ? bytes : 1));
+  if (e != hipSuccess) {
+    set_error("svmd_alloc(%lld): %s", (long long)bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+SVM_API void svmd_free(void* h, void* ptr) {
+  auto* ctx = static_cast<DeviceCtx*>(h);
+  if (!ctx || !ptr) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(ptr);
+}
+
+SVM_API int svmd_memcpy_h2d(void* h, void* dst_d, const void* src_h, int64_t bytes) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (bytes > 0) SVMD_CHECK(hipMemcpyAsync(dst_d, src_h, size_t(bytes), hipMemcpyHostToDevice, ctx->stream));
+  SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+  return ctx->end();
+}
+
+SVM_API int svmd_memcpy_d2h(void* h, void* dst_h, const void* src_d, int64_t bytes) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (bytes > 0) SVMD_CHECK(hipMemcpyAsync(dst_h, src_d, size_t(bytes), hipMemcpyDeviceToHost, ctx->stream));
+  SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+  return ctx->end();
+}
+
+SVM_API void* svmd_create(int32_t device) {
+  if (hipSetDevice(device) != hipSuccess) {
+    set_error("svmd_create: hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  auto* ctx = new DeviceCtx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_out, hipEventDisableTiming) != hipSuccess) {
+    set_error("svmd_create: stream/event creation failed");
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+SVM_API void svmd_destroy(void* h) {
+  auto* ctx = static_cast<DeviceCtx*>(h);
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  ctx->release_graph();
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
+  if (ctx->ev_out) (void)hipEventDestroy(ctx->ev_out);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+SVM_API int svmd_set_stream(void* h, void* stream) {
+  SVMD_CTX(h);
+  ctx->ext = static_cast<hipStream_t>(stream);
+  ctx->has_ext = true;
+  return SVM_OK;
+}
+
+SVM_API int svmd_synchronize(void* h) {
+  SVMD_CTX(h);
+  SVMD_CHECK(hipSetDevice(ctx->device));
+  SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+  if (ctx->has_ext) SVMD_CHECK(hipStreamSynchronize(ctx->ext));
+  return SVM_OK;
+}
+
+SVM_API int svmd_upload_rows(void* h, const double* X_host, int64_t n, int64_t d, double* X_d, int64_t ld) {
+  SVMD_CTX(h);
+  if (ld < d || n < 0) {
+    set_error("svmd_upload_rows: ld < d");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (n > 0) {
+    if (ld == d) {
+      SVMD_CHECK(hipMemcpyAsync(X_d, X_host, size_t(n * d) * 8, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      SVMD_CHECK(hipMemsetAsync(X_d, 0, size_t(n * ld) * 8, ctx->stream));
+      SVMD_CHECK(hipMemcpy2DAsync(X_d, size_t(ld) * 8, X_host, size_t(d) * 8, size_t(d) * 8, size_t(n),
+                                  hipMemcpyHostToDevice, ctx->stream));
+    }
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));  // the host buffer may be released on return
+  }
+  return ctx->end();
+}
+
+SVM_API int svmd_preprocess(void* h, double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
+                            double* mx_d, double* sqn_d, int32_t use_given) {
+  SVMD_CTX(h);
+  if (n <= 0 || d <= 0 || ld < d || !mn_d || !mx_d) {
+    set_error("svmd_preprocess: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (!use_given) {
+    const size_t scratch = size_t(2) * size_t(d) * 2048;
+    rc = ctx->ensure_ws(scratch * 8);
+    if (rc) return rc;
+    rc = launch_minmax(ctx->stream, X_d, n, d, ld, mn_d, mx_d, static_cast<double*>(ctx->ws), scratch);
+    if (rc) return rc;
+  }
+  rc = launch_scale_norms(ctx->stream, X_d, n, d, ld, mn_d, mx_d, sqn_d);
+  if (rc) return rc;
+  return ctx->end();
+}
+
+SVM_API int svmd_row_norms(void* h, const double* X_d, int64_t n, int64_t d, int64_t ld, double* sqn_d) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = launch_scale_norms(ctx->stream, const_cast<double*>(X_d), n, d, ld, nullptr, nullptr, sqn_d);
+  if (rc) return rc;
+  return ctx->end();
+}
+
+SVM_API int svmd_rbf_gram(void* h, const double* A_d, const double* nA_d, int64_t m, int64_t lda,
+                          const double* B_d, const double* nB_d, int64_t n, int64_t ldb, int64_t kdim,
+                          double gamma, double* K_d, int64_t ldk, int32_t sym_diag) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = launch_rbf_gram(ctx->stream, A_d, nA_d, m, lda, B_d, nB_d, n, ldb, kdim, gamma, K_d, ldk, sym_diag != 0);
+  if (rc) return rc;
+  return ctx->end();
+}
+
+SVM_API int svmd_smo(void* h, const double* K_d, int64_t ldk, const int32_t* y_d, int64_t n,
+                     double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
+                     int64_t* trace_host, int64_t trace_cap) {
+  SVMD_CTX(h);
+  const svm_params q = resolve(p);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = run_smo(ctx, K_d, ldk, y_d, n, alpha_d, warm, q, r, trace_host, trace_cap);
+  if (rc) return rc;
+  if (r) {
+    std::vector<double> a(static_cast<size_t>(n));
+    SVMD_CHECK(hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost));
+    r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
+  }
+  return ctx->end();
+}
+
+SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
+                       const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p,
+                       svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing) {
+  SVMD_CTX(h);
+  const svm_params q = resolve(p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ctx->begin();
+  if (rc) return rc;
+  double* K = K_d;
+  bool owned = false;
+  if (!K) {
+    ldk = (n + 1) / 2 * 2;  // keep rows 16-byte aligned
+    const hipError_t e = hipMalloc(&K, size_t(n) * size_t(ldk) * 8);
+    if (e != hipSuccess) {
+      set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s",
+                double(n) * double(ldk) * 8e-9, hipGetErrorString(e));
+      return SVM_ERR_OOM;
+    }
+    owned = true;
+  }
+  rc = launch_rbf_gram(ctx->stream, X_d, sqn_d, n, ld, X_d, sqn_d, n, ld, kdim, q.gamma, K, ldk, true);
+  if (!rc && timing) {
+    const hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      set_error("svmd_train: gram failed: %s", hipGetErrorString(e));
+      rc = SVM_ERR_DEVICE;
+    }
+  }
+  const double t_gram = ms_since(t0);
+  if (!rc) rc = run_smo(ctx, K, ldk, y_d, n, alpha_d, warm, q, r, nullptr, 0);
+  if (!rc && r) {
+    std::vector<double> a(static_cast<size_t>(n));
+    const hipError_t e = hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      set_error("svmd_train: %s", hipGetErrorString(e));
+      rc = SVM_ERR_DEVICE;
+    } else {
+      r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
+    }
+  }
+  if (owned) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(K);
+  }
+  if (rc) return rc;
+  if (timing) {
+    timing->gram_ms = t_gram;
+    timing->total_ms = ms_since(t0);
+    timing->smo_ms = timing->total_ms - t_gram;
+  }
+  return ctx->end();
+}
+
+SVM_API int svmd_decision(void* h, const double* Xs_d, const double* ns_d, const double* coef_d, int64_t nsv,
+                          int64_t lds, const double* Xq_d, const double* nq_d, int64_t m, int64_t ldq,
+                          int64_t kdim, double gamma, double b, double* out_d) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (m <= 0) return ctx->end();
+  if (nsv <= 0) {
+    // No support vectors: decision is -b everywhere.
+    std::vector<double> v(size_t(m), -b);
+    SVMD_CHECK(hipMemcpyAsync(out_d, v.data(), size_t(m) * 8, hipMemcpyHostToDevice, ctx->stream));
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+    return ctx->end();
+  }
+  // Cross-kernel block K(Xq, Xs) in row chunks of <= 512 MB scratch, then a deterministic GEMV.
+  const int64_t ldk = (nsv + 1) / 2 * 2;
+  int64_t rows = std::max<int64_t>(128, (int64_t(512) << 20) / (ldk * 8) / 128 * 128);
+  rows = std::min<int64_t>(rows, (m + 127) / 128 * 128);
+  rc = ctx->ensure_ws(size_t(rows) * size_t(ldk) * 8);
+  if (rc) return rc;
+  double* Kq = static_cast<double*>(ctx->ws);
+  for (int64_t r0 = 0; r0 < m; r0 += rows) {
+    const int64_t mr = std::min(rows, m - r0);
+    rc = launch_rbf_gram(ctx->stream, Xq_d + r0 * ldq, nq_d + r0, mr, ldq, Xs_d, ns_d, nsv, lds, kdim, gamma, Kq,
+                         ldk, false);
+    if (rc) return rc;
+    rc = launch_gemv_rows(ctx->stream, Kq, ldk, mr, nsv, coef_d, b, out_d + r0);
+    if (rc) return rc;
+  }
+  return ctx->end();
+}
+
+SVM_API int svmd_gather_rows(void* h, const double* src_d, int64_t ld, const int64_t* idx_d, int64_t k,
+                             double* dst_d) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = launch_gather_rows(ctx->stream, src_d, ld, idx_d, k, dst_d);
+  if (rc) return rc;
+  return ctx->end();
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// Device context: stream, cross-stream ordering and a grow-only workspace.
+#pragma once
+#include <vector>
+
+#include "hip_util.h"
+
+namespace svm355 {
+
+struct DeviceCtx {
+  int device = 0;
+  hipStream_t stream = nullptr;  // private non-blocking stream (graph-capturable)
+  hipStream_t ext = nullptr;     // caller's stream (PyTorch current stream), may be null
+  bool has_ext = false;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  // Cached SMO iteration graph (smo.hip) and the argument key it was captured for.
+  hipGraphExec_t smo_exec = nullptr;
+  hipGraph_t smo_graph = nullptr;
+  std::vector<uint64_t> smo_key;
+
+  void release_graph() {
+    if (smo_exec) (void)hipGraphExecDestroy(smo_exec);
+    if (smo_graph) (void)hipGraphDestroy(smo_graph);
+    smo_exec = nullptr;
+    smo_graph = nullptr;
+    smo_key.clear();
+  }
+
+  // Make the private stream wait for work already enqueued on the caller's stream.
+  int begin() {
+    SVMD_CHECK(hipSetDevice(device));
+    if (has_ext) {
+      SVMD_CHECK(hipEventRecord(ev_in, ext));
+      SVMD_CHECK(hipStreamWaitEvent(stream, ev_in, 0));
+    }
+    return SVM_OK;
+  }
+  // Make the caller's stream wait for the private stream.
+  int end() {
+    if (has_ext) {
+      SVMD_CHECK(hipEventRecord(ev_out, stream));
+      SVMD_CHECK(hipStreamWaitEvent(ext, ev_out, 0));
+    }
+    return SVM_OK;
+  }
+  int ensure_ws(size_t bytes) {
+    if (bytes <= ws_bytes) return SVM_OK;
+    if (ws) {
+      SVMD_CHECK(hipStreamSynchronize(stream));
+      SVMD_CHECK(hipFree(ws));
+      ws = nullptr;
+      ws_bytes = 0;
+    }
+    const size_t sz = (bytes + 0xFFFFF) & ~size_t(0xFFFFF);
+    SVMD_CHECK(hipMalloc(&ws, sz));
+    ws_bytes = sz;
+    return SVM_OK;
+  }
+  int ensure_pinned(size_t bytes) {
+    if (bytes <= pinned_bytes) return SVM_OK;
+    if (pinned) {
+      SVMD_CHECK(hipStreamSynchronize(stream));
+      SVMD_CHECK(hipHostFree(pinned));
+      pinned = nullptr;
+      pinned_bytes = 0;
+    }
+    const size_t sz = (bytes + 0xFFFF) & ~size_t(0xFFFF);
+    SVMD_CHECK(hipHostMalloc(&pinned, sz, hipHostMallocDefault));
+    pinned_bytes = sz;
+    return SVM_OK;
+  }
+};
+
+#define SVMD_CTX(h)                                              \
+  auto* ctx = static_cast<svm355::DeviceCtx*>(h);                 \
+  if (!ctx) {                                                    \
+    svm355::set_error("null device context");                    \
+    return SVM_ERR_ARG;                                          \
+  }
+
+// Kernel launchers implemented in the .hip translation units (all enqueue on `s`).
+int launch_minmax(hipStream_t s, const double* X, int64_t n, int64_t d, int64_t ld, double* mn,
+                  double* mx, double* scratch, size_t scratch_doubles);
+int launch_scale_norms(hipStream_t s, double* X, int64_t n, int64_t d, int64_t ld, const double* mn,
+                       const double* mx, double* sqn);
+int launch_gather_rows(hipStream_t s, const double* src, int64_t ld, const int64_t* idx, int64_t k,
+                       double* dst);
+int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m, int64_t lda,
+                    const double* B, const double* nB, int64_t n, int64_t ldb, int64_t kdim,
+                    double gamma, double* K, int64_t ldk, bool sym_diag);
+int launch_gemv_rows(hipStream_t s, const double* K, int64_t ldk, int64_t m, int64_t n,
+                     const double* coef, double b, double* out);
+int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
+            int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
+
+}  // namespace svm355

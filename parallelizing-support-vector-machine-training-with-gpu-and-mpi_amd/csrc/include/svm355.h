@@ -1,0 +1,120 @@
+// svm355 — C ABI of the native runtime (CPU core + HIP/gfx950 device library).
+//
+// Everything the Python package and the native CLIs call goes through this header.
+// The CPU core (libsvm355_core.so) implements the reference semantics exactly and
+// doubles as the correctness oracle; the device library (libsvm355_hip.so) implements
+// the same contract on MI355X with hand-written CDNA4 kernels.
+//
+// Reference parity map (files under /root/reference/code):
+//   svm_csv_load        <- read_CSV                 main3.cpp:13-54, gpu_svm_main4.cu:16-59 (row limit)
+//   svm_minmax/scale    <- find_min_max/scale_features main3.cpp:57-89
+//   svm_rbf             <- kernel                   main3.cpp:92-104 (gamma made a parameter)
+//   svm_smo_train       <- SMO_train                main3.cpp:162-294, warm start mpi_svm_main3.cpp:155-290
+//   svm_decision        <- predict loop             main3.cpp:391-402
+//   svm_model_save      <- commented model dump     mpi_svm_main3.cpp:754-770
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVM_API __attribute__((visibility("default")))
+
+enum svm_status {
+  SVM_OK = 0,
+  SVM_ERR_IO = 1,
+  SVM_ERR_ARG = 2,
+  SVM_ERR_EMPTY = 3,
+  SVM_ERR_DEVICE = 4,
+  SVM_ERR_INTERNAL = 5,
+  SVM_ERR_OOM = 6,
+};
+
+// Why an SMO solve ended. Codes match the reference's stderr messages.
+enum svm_stop {
+  SVM_STOP_RUNNING = 0,
+  SVM_STOP_CONVERGED = 1,     // b_low <= b_high + 2*tau
+  SVM_STOP_NO_CANDIDATE = 2,  // "i_high or i_low not found; iteration stops"
+  SVM_STOP_INFEASIBLE = 3,    // "warning: infeasible U and V; iteration stops"
+  SVM_STOP_NONPOS_ETA = 4,    // "warning: non positive eta; iteration stops"
+  SVM_STOP_MAX_ITER = 5,      // "Too many iterations; stopping"
+};
+
+typedef struct svm_params {
+  double C;          // box constraint, reference default 10
+  double gamma;      // RBF width, reference default 0.00125
+  double tau;        // stop when b_low <= b_high + 2*tau, default 1e-5
+  double eps;        // set-membership / eta floor, default 1e-12
+  double sv_tol;     // alpha > sv_tol is a support vector, default 1e-8
+  int64_t max_iter;  // default 100000 (num_iter starts at 1)
+  int32_t n_threads; // CPU worker threads (1 = the serial reference baseline)
+  int32_t verbose;
+} svm_params;
+
+typedef struct svm_result {
+  int64_t iterations;  // the reference's printed num_iter (updates + 1)
+  double b;            // (b_high + b_low) / 2
+  double b_high;
+  double b_low;
+  int32_t stop_reason; // enum svm_stop
+  int32_t reserved;
+  int64_t n_sv;        // alpha > sv_tol
+  double seconds;      // solver wall time
+} svm_result;
+
+SVM_API const char* svm_last_error(void);
+SVM_API void svm_default_params(svm_params* p);
+SVM_API const char* svm_stop_message(int32_t reason);
+
+// ---------------------------------------------------------------- data I/O (L0)
+// Loads a CSV with a header row; the last column is the integer label.
+// limit < 0 reads every line; otherwise at most `limit` data lines are consumed
+// (skipped short lines count toward the limit, as gpu_svm_main4.cu:34-38).
+// y = +1 where label == positive_label, else -1 (main3.cpp:49-52 with positive_label=1).
+SVM_API void* svm_csv_load(const char* path, int64_t limit, int32_t positive_label, int32_t n_threads);
+SVM_API int svm_dataset_dims(void* h, int64_t* n, int64_t* d);
+SVM_API int svm_dataset_copy(void* h, double* X, int32_t* y, int32_t* raw_labels);
+SVM_API void svm_dataset_free(void* h);
+SVM_API int svm_csv_write(const char* path, const double* X, const int32_t* labels, int64_t n, int64_t d);
+
+// Deterministic MNIST-shaped generator: 28x28 (d=784) integer pixels 0..255, labels 0..9.
+SVM_API int svm_synth_mnist(uint64_t seed, int64_t n, double* X, int32_t* labels, int32_t n_threads);
+
+// ---------------------------------------------------------------- preprocessing (L1)
+SVM_API int svm_minmax(const double* X, int64_t n, int64_t d, double* mn, double* mx);
+SVM_API int svm_scale(double* X, int64_t n, int64_t d, const double* mn, const double* mx);
+
+// ---------------------------------------------------------------- kernel (L2)
+SVM_API double svm_rbf(const double* a, const double* b, int64_t d, double gamma);
+SVM_API int svm_rbf_matrix(const double* A, int64_t m, const double* B, int64_t n, int64_t d,
+                           double gamma, double* K, int32_t n_threads);
+
+// ---------------------------------------------------------------- SMO (L3)
+// alpha: in/out length n. warm=0: alpha reset to 0 and f = -y (main3.cpp:165-172).
+// warm=1: f_i = sum_{alpha_j != 0} alpha_j y_j K_ij - y_i (mpi_svm_main3.cpp:169-186).
+// trace (optional, may be NULL): receives (i_high, i_low) for each update, up to trace_cap pairs.
+SVM_API int svm_smo_train(const double* X, const int32_t* y, int64_t n, int64_t d, double* alpha,
+                          int32_t warm, const svm_params* p, svm_result* r, int64_t* trace,
+                          int64_t trace_cap);
+// Same solver on a precomputed kernel matrix K (n x n, row stride ldk).
+SVM_API int svm_smo_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n,
+                               double* alpha, int32_t warm, const svm_params* p, svm_result* r,
+                               int64_t* trace, int64_t trace_cap);
+
+// ---------------------------------------------------------------- evaluation (L4)
+// out[i] = sum_k alphas[k]*ys[k]*K(Xq_i, Xs_k) - b, summed in SV order from -b (main3.cpp:391-402).
+SVM_API int svm_decision(const double* Xs, const int32_t* ys, const double* alphas, int64_t nsv,
+                         const double* Xq, int64_t m, int64_t d, double gamma, double b,
+                         double* out, int32_t n_threads);
+// Indices with alpha > tol, ascending; returns the count (out may be NULL to count only).
+SVM_API int64_t svm_sv_indices(const double* alpha, int64_t n, double tol, int64_t* out);
+
+// ---------------------------------------------------------------- model files (C31)
+// Writes final_sv_ids.txt, final_sv_labels.txt, final_sv_alphas.txt, final_b.txt into dir.
+SVM_API int svm_model_save(const char* dir, const int64_t* ids, const int32_t* labels,
+                           const double* alphas, int64_t nsv, double b);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,86 @@
+// svm355 device library C ABI (libsvm355_hip.so, gfx950 / MI355X).
+//
+// All pointers named *_d are device pointers; every operation is enqueued on the context's
+// stream (optionally chained after an external stream, e.g. PyTorch's current stream, through
+// svmd_set_stream).  Feature matrices live on the device as row-major n x ld arrays with
+// ld = round_up(d, 16) and zero padding (svmd_padded_dim).
+//
+// Reference parity map (/root/reference/code):
+//   svmd_preprocess  <- find_min_max + scale_features kernels  gpu_svm_main3.cu:62-116, 557-598
+//   svmd_rbf_gram    <- calc_kernel_matrix (one row at a time) gpu_svm_main3.cu:137-147; here the
+//                       whole RBF Gram (or a cross-kernel block) on MFMA f64 tiles
+//   svmd_smo         <- SMO_train host loop + WSS/update kernels gpu_svm_main3.cu:152-272, 318-483;
+//                       here device-resident: fused f-update+WSS kernel + single-block step kernel,
+//                       replayed from a hipGraph with no per-iteration host round trip
+//   svmd_decision    <- predict + reduce_sum                   gpu_svm_main3.cu:277-315 (over SVs
+//                       only, MFMA cross-kernel + deterministic GEMV)
+#pragma once
+#include <stdint.h>
+
+#include "svm355.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct svmd_timing {
+  double h2d_ms, preprocess_ms, gram_ms, smo_ms, total_ms;
+} svmd_timing;
+
+SVM_API int64_t svmd_padded_dim(int64_t d);
+SVM_API int svmd_device_count(int32_t* count);
+
+// Plain device memory helpers for native callers that do not link the HIP runtime themselves.
+SVM_API void* svmd_alloc(void* ctx, int64_t bytes);
+SVM_API void svmd_free(void* ctx, void* ptr);
+SVM_API int svmd_memcpy_h2d(void* ctx, void* dst_d, const void* src_h, int64_t bytes);
+SVM_API int svmd_memcpy_d2h(void* ctx, void* dst_h, const void* src_d, int64_t bytes);  // synchronous
+
+SVM_API void* svmd_create(int32_t device);
+SVM_API void svmd_destroy(void* ctx);
+// stream = hipStream_t of the caller (may be NULL = legacy default stream).  Work enqueued by the
+// context is ordered after everything already on that stream, and the caller's stream waits for
+// the context's work before each call returns.
+SVM_API int svmd_set_stream(void* ctx, void* stream);
+SVM_API int svmd_synchronize(void* ctx);
+
+// Host (n x d, contiguous) -> device (n x ld, zero-padded).  X_d must hold n*ld doubles.
+SVM_API int svmd_upload_rows(void* ctx, const double* X_host, int64_t n, int64_t d, double* X_d, int64_t ld);
+
+// Column min/max over n rows (unless use_given != 0, then mn_d/mx_d are inputs), in-place min-max
+// scaling with the range < 1e-12 -> 1 rule, and squared row norms sqn_d (length n, may be NULL).
+SVM_API int svmd_preprocess(void* ctx, double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
+                            double* mx_d, double* sqn_d, int32_t use_given);
+SVM_API int svmd_row_norms(void* ctx, const double* X_d, int64_t n, int64_t d, int64_t ld, double* sqn_d);
+
+// K[i][j] = exp(-gamma * max(0, nA_i + nB_j - 2 A_i.B_j)) for i < m, j < n (row stride ldk).
+// sym_diag != 0 forces K[i][i] = 1 (use when A == B).  kdim must be a multiple of 16.
+SVM_API int svmd_rbf_gram(void* ctx, const double* A_d, const double* nA_d, int64_t m, int64_t lda,
+                          const double* B_d, const double* nB_d, int64_t n, int64_t ldb, int64_t kdim,
+                          double gamma, double* K_d, int64_t ldk, int32_t sym_diag);
+
+// SMO on a device kernel matrix.  alpha_d in/out (length n); y_d int32 +-1.
+// trace_host (optional): (i_high, i_low) per update, up to trace_cap pairs.
+SVM_API int svmd_smo(void* ctx, const double* K_d, int64_t ldk, const int32_t* y_d, int64_t n,
+                     double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
+                     int64_t* trace_host, int64_t trace_cap);
+
+// End-to-end training on preprocessed device rows: RBF Gram (allocated internally, or K_d if
+// non-NULL with ldk >= n) + SMO.  timing may be NULL.
+SVM_API int svmd_train(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
+                       int64_t kdim, const int32_t* y_d, double* alpha_d, int32_t warm,
+                       const svm_params* p, svm_result* r, double* K_d, int64_t ldk,
+                       svmd_timing* timing);
+
+// out_d[i] = sum_k coef_d[k] * K(Xq_i, Xs_k) - b, coef = alpha*y of the SVs.
+SVM_API int svmd_decision(void* ctx, const double* Xs_d, const double* ns_d, const double* coef_d,
+                          int64_t nsv, int64_t lds, const double* Xq_d, const double* nq_d, int64_t m,
+                          int64_t ldq, int64_t kdim, double gamma, double b, double* out_d);
+
+// dst[k] = src[idx[k]] rows (device gather), for SV compaction and cascade training-set assembly.
+SVM_API int svmd_gather_rows(void* ctx, const double* src_d, int64_t ld, const int64_t* idx_d,
+                             int64_t k, double* dst_d);
+
+#ifdef __cplusplus
+}
+#endif
