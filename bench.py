@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SMO train time on the MNIST-60k one-vs-rest RBF config (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 60000] [--topology star|tree]
+
+One "step" is one complete training run on the fixed synthetic 60k x 784 MNIST-shaped matrix
+(random-init is meaningless for an SVM; the data are a deterministic synthetic draw of MNIST's
+shape and value domain because MNIST itself is not available offline):
+
+* N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's
+  GPU "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram
+  on MFMA f64, device SMO to convergence.
+* N > 1: one rank per GPU (torchrun, RCCL over xGMI), the modified two-layer Cascade SVM
+  (mpi_svm_main2.cpp, default) or the classical tree (--topology tree).  Timed scope = a whole
+  cascade fit of each rank's partition (H2D, global scaling, all rounds to convergence).
+
+The timed region is bracketed by a barrier + device synchronisation on both sides and the
+maximum over ranks is reported.  value = seconds per training run (lower is better);
+vs_baseline = value / 58.570 s (the reference's single-GPU SMO time).
+Accuracy, #SV, b and iterations of the last run are reported alongside (parity fields).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REF_GPU_S = 58.570  # GPU SMO training time, 60k
+REF_SERIAL_S = 3285.662  # serial SMO training time, 60k
+REF_STAR_S = {4: 886.733, 8: 649.773, 16: 440.705, 32: 333.696, 64: 301.263}
+REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
+METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=60000, help="training rows (MNIST-60k config)")
+    ap.add_argument("--m", type=int, default=10000, help="test rows for the parity fields")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--topology", choices=["star", "tree"], default="star")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if a.gpus > 1:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run",
+                  file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from svm355 import SVC, SVMParams
+    from svm355.parallel.cascade import CascadeSVM, partition_bounds
+    from svm355.utils.data import synthetic_mnist
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    params = SVMParams()
+
+    if world == 1:
+        tr = synthetic_mnist(a.n, seed=a.seed)
+    else:
+        lo, hi = partition_bounds(a.n, world, rank)
+        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo)
+    te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
+
+    def barrier_sync():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier(device_ids=[local_rank])
+        torch.cuda.synchronize(dev)
+
+    model = None
+
+    def step():
+        nonlocal model
+        if world == 1:
+            model = SVC(device=str(dev)).fit(tr.X, tr.y)
+        else:
+            from svm355.parallel.transport import TorchDistTransport
+
+            t = TorchDistTransport(dev)
+            model = CascadeSVM(t, params, topology=a.topology, verbose=0)
+            lo, hi = partition_bounds(a.n, world, rank)
+            model.fit(tr.X, tr.y, np.arange(lo, hi), n_total=a.n)
+
+    for _ in range(a.warmup):
+        step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    ms = elapsed / a.steps * 1e3
+    value = ms / 1e3
+    extra = {}
+    if world == 1:
+        acc = model.score(te.X, te.y)
+        extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
+                 "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_}
+    else:
+        acc = model.score(te.X, te.y) if rank == 0 else None
+        s = model.summary()
+        extra = {"n_sv": s["n_sv"], "rounds": s["rounds"], "b": s["b"], "accuracy": acc,
+                 "sv_history": s["sv_history"], "round_ms": s["round_ms"], "converged": s["converged"]}
+        ref = (REF_STAR_S if a.topology == "star" else REF_TREE_S).get(world)
+        if ref:
+            extra["speedup_vs_ref_cascade_same_P"] = ref / value
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 6),
+            "unit": "s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(value / REF_GPU_S, 6),
+            "dtype": "fp64",
+            "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
+            "config": {
+                "model": "RBF SVM, first-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
+                "global_batch": a.n,
+                "seq_len": 784,
+                "parallelism": "single-gpu" if world == 1 else f"cascade-{a.topology}-dp{world}",
+            },
+            "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
+            "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
+            **extra,
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(s + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -80,7 +80,7 @@ _CORE_SIGS = {
     "svm_dataset_copy": (c_int32, [c_void_p, _P, _P, _P]),
     "svm_dataset_free": (None, [c_void_p]),
     "svm_csv_write": (c_int32, [c_char_p, _P, _P, c_int64, c_int64]),
-    "svm_synth_mnist": (c_int32, [c_uint64, c_int64, _P, _P, c_int32]),
+    "svm_synth_mnist": (c_int32, [c_uint64, c_int64, c_int64, _P, _P, c_int32]),
     "svm_minmax": (c_int32, [_P, c_int64, c_int64, _P, _P]),
     "svm_scale": (c_int32, [_P, c_int64, c_int64, _P, _P]),
     "svm_rbf": (c_double, [_P, _P, c_int64, c_double]),
@@ -107,7 +107,8 @@ _HIP_SIGS = {
     "svmd_set_stream": (c_int32, [c_void_p, c_void_p]),
     "svmd_synchronize": (c_int32, [c_void_p]),
     "svmd_upload_rows": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, c_int64]),
-    "svmd_preprocess": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int32]),
+    "svmd_minmax": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P]),
+    "svmd_preprocess":(c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int32]),
     "svmd_row_norms": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P]),
     "svmd_rbf_gram": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
                                 c_double, _P, c_int64, c_int32]),

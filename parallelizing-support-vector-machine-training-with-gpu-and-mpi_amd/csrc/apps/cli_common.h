@@ -104,17 +104,14 @@ inline bool load_split(const Options& o, bool train, Data& out) {
     long long n = train ? o.synth_train : o.synth_test;
     if (train && o.n_limit >= 0 && o.n_limit < n) n = o.n_limit;
     const long long off = train ? 0 : o.synth_train;
-    std::vector<double> Xall(size_t(n + off) * 784);
-    std::vector<int32_t> lab(size_t(n + off));
-    // Generate only the needed range by generating the prefix (cheap) — keeps one code path.
-    if (svm_synth_mnist(o.seed, n + off, Xall.data(), lab.data(), 0) != SVM_OK) {
+    out.n = n;
+    out.d = 784;
+    out.X.resize(size_t(n) * 784);
+    out.raw.resize(size_t(n));
+    if (svm_synth_mnist(o.seed, off, n, out.X.data(), out.raw.data(), 0) != SVM_OK) {
       fprintf(stderr, "%s\n", svm_last_error());
       return false;
     }
-    out.n = n;
-    out.d = 784;
-    out.X.assign(Xall.begin() + off * 784, Xall.end());
-    out.raw.assign(lab.begin() + off, lab.end());
     out.y.resize(size_t(n));
     for (long long i = 0; i < n; ++i) out.y[size_t(i)] = out.raw[size_t(i)] == o.positive_label ? 1 : -1;
     return true;

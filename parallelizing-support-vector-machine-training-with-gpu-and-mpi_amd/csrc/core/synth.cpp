@@ -167,8 +167,9 @@ void render(const Glyph& g, double thick, double ink, Rng& r, double* out) {
 
 }  // namespace
 
-extern "C" SVM_API int svm_synth_mnist(uint64_t seed, int64_t n, double* X, int32_t* labels, int32_t n_threads) {
-  if (n < 0 || (n > 0 && (!X || !labels))) {
+extern "C" SVM_API int svm_synth_mnist(uint64_t seed, int64_t offset, int64_t n, double* X, int32_t* labels,
+                                       int32_t n_threads) {
+  if (n < 0 || offset < 0 || (n > 0 && (!X || !labels))) {
     set_error("svm_synth_mnist: bad arguments");
     return SVM_ERR_ARG;
   }
@@ -194,7 +195,8 @@ extern "C" SVM_API int svm_synth_mnist(uint64_t seed, int64_t n, double* X, int3
 
   parallel_for(n, resolve_threads(n_threads), [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
-      uint64_t s = seed * 0x9E3779B97F4A7C15ull + uint64_t(i) * 0xD1B54A32D192ED03ull + 0x1234567ull;
+      const uint64_t gi = uint64_t(offset + i);  // global sample index
+      uint64_t s = seed * 0x9E3779B97F4A7C15ull + gi * 0xD1B54A32D192ED03ull + 0x1234567ull;
       Rng r(splitmix64(s));
       const double u = r.uni() * acc;
       int cls = 0;

@@ -143,6 +143,23 @@ SVM_API int svmd_upload_rows(void* h, const double* X_host, int64_t n, int64_t d
   return ctx->end();
 }
 
+SVM_API int svmd_minmax(void* h, const double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
+                        double* mx_d) {
+  SVMD_CTX(h);
+  if (n <= 0 || d <= 0 || ld < d || !mn_d || !mx_d) {
+    set_error("svmd_minmax: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  const size_t scratch = size_t(2) * size_t(d) * 2048;
+  rc = ctx->ensure_ws(scratch * 8);
+  if (rc) return rc;
+  rc = launch_minmax(ctx->stream, X_d, n, d, ld, mn_d, mx_d, static_cast<double*>(ctx->ws), scratch);
+  if (rc) return rc;
+  return ctx->end();
+}
+
 SVM_API int svmd_preprocess(void* h, double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
                             double* mx_d, double* sqn_d, int32_t use_given) {
   SVMD_CTX(h);

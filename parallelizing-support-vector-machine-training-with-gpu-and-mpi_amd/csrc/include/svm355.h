@@ -79,7 +79,9 @@ SVM_API void svm_dataset_free(void* h);
 SVM_API int svm_csv_write(const char* path, const double* X, const int32_t* labels, int64_t n, int64_t d);
 
 // Deterministic MNIST-shaped generator: 28x28 (d=784) integer pixels 0..255, labels 0..9.
-SVM_API int svm_synth_mnist(uint64_t seed, int64_t n, double* X, int32_t* labels, int32_t n_threads);
+// Writes global samples [offset, offset + n); sample i depends only on (seed, i).
+SVM_API int svm_synth_mnist(uint64_t seed, int64_t offset, int64_t n, double* X, int32_t* labels,
+                            int32_t n_threads);
 
 // ---------------------------------------------------------------- preprocessing (L1)
 SVM_API int svm_minmax(const double* X, int64_t n, int64_t d, double* mn, double* mx);

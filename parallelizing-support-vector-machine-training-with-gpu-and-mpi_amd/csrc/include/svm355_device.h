@@ -49,6 +49,8 @@ SVM_API int svmd_upload_rows(void* ctx, const double* X_host, int64_t n, int64_t
 
 // Column min/max over n rows (unless use_given != 0, then mn_d/mx_d are inputs), in-place min-max
 // scaling with the range < 1e-12 -> 1 rule, and squared row norms sqn_d (length n, may be NULL).
+SVM_API int svmd_minmax(void* ctx, const double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
+                        double* mx_d);
 SVM_API int svmd_preprocess(void* ctx, double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
                             double* mx_d, double* sqn_d, int32_t use_given);
 SVM_API int svmd_row_norms(void* ctx, const double* X_d, int64_t n, int64_t d, int64_t ld, double* sqn_d);

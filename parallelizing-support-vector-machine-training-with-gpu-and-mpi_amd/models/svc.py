@@ -1,0 +1,206 @@
+"""Kernel SVM estimator (RBF, one-vs-rest binary) with a CPU oracle backend and an MI355X backend.
+
+``SVC.fit`` runs the reference pipeline — min-max scaling fitted on the training rows
+(main3.cpp:57-89), first-order SMO with the reference stop rules (main3.cpp:162-294) — and keeps
+the support vectors (alpha > sv_tol, main3.cpp:297-304).  ``predict`` is sign(sum alpha y K - b)
+over the SVs (main3.cpp:391-402; the serial/GPU programs map 0 to -1, the cascades to +1 — see
+``zero_is_positive``).
+
+Backends
+  device="cpu"   native C++ oracle (bit-exact reference arithmetic), ``n_threads`` workers
+  device="cuda"  gfx950 kernels: H2D, fused min/max + scale + row norms, MFMA f64 RBF Gram kept
+                 resident in HBM, graph-replayed device SMO, MFMA decision function
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from ..utils.config import SVMParams
+from ..utils.data import MinMaxScaler
+
+
+def _resolve_device(device: str) -> str:
+    if device == "auto":
+        import torch
+
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    return device
+
+
+class SVC:
+    def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
+                 sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
+                 scale: bool = True, zero_is_positive: bool = False):
+        self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
+                                n_threads=n_threads if n_threads > 0 else (os.cpu_count() or 1))
+        self.device = device
+        self.scale = scale
+        self.zero_is_positive = zero_is_positive
+        self._dev = None  # device-side model state (torch tensors)
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X: np.ndarray, y: np.ndarray, alpha0: Optional[np.ndarray] = None) -> "SVC":
+        dev = _resolve_device(self.device)
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        if X.ndim != 2 or y.shape != (X.shape[0],):
+            raise ValueError("X must be (n, d) and y (n,)")
+        if not np.all(np.abs(y) == 1):
+            raise ValueError("labels must be +1/-1 (use svm355.utils.data.one_vs_rest)")
+        t0 = time.perf_counter()
+        if dev == "cpu":
+            self._fit_cpu(X, y, alpha0)
+        else:
+            self._fit_cuda(X, y, alpha0, dev)
+        self.fit_time_ = time.perf_counter() - t0
+        return self
+
+    def _finish(self, alpha: np.ndarray, y: np.ndarray, res) -> None:
+        self.alpha_ = alpha
+        self.support_ = np.flatnonzero(alpha > self.params.sv_tol).astype(np.int64)
+        self.dual_coef_ = alpha[self.support_] * y[self.support_]
+        self.support_labels_ = y[self.support_].astype(np.int32)
+        self.b_ = res.b
+        self.intercept_ = -res.b
+        self.n_iter_ = res.iterations
+        self.stop_reason_ = res.stop_reason
+        self.result_ = res
+
+    def _fit_cpu(self, X, y, alpha0):
+        from ..ops import cpu as C
+
+        if self.scale:
+            self.scaler_ = MinMaxScaler().fit(X)
+            Xs = self.scaler_.transform(X)
+        else:
+            self.scaler_ = None
+            Xs = X
+        alpha, res, _ = C.smo_train(Xs, y, self.params, alpha=alpha0, warm=alpha0 is not None)
+        self._finish(alpha, y, res)
+        self.support_vectors_ = Xs[self.support_].copy()
+        self.timings_ = {"smo_ms": res.seconds * 1e3}
+
+    def _fit_cuda(self, X, y, alpha0, dev):
+        import torch
+
+        from ..ops import device as D
+
+        device = torch.device(dev)
+        t0 = time.perf_counter()
+        Xd = D.upload_rows(X, device)
+        yd = torch.from_numpy(y).to(device)
+        d = X.shape[1]
+        if self.scale:
+            mn, mx, sqn = D.minmax_scale_(Xd, d)
+        else:
+            mn = mx = None
+            sqn = D.row_norms(Xd, d)
+        if alpha0 is not None:
+            alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
+        else:
+            alpha = torch.zeros(X.shape[0], dtype=torch.float64, device=device)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None)
+        a = alpha.cpu().numpy()
+        self._finish(a, y, res)
+        idx = torch.from_numpy(self.support_).to(device)
+        self._dev = {
+            "Xs": D.gather_rows(Xd, idx),
+            "ns": sqn[idx].contiguous(),
+            "coef": torch.from_numpy(self.dual_coef_).to(device),
+            "mn": mn,
+            "mx": mx,
+            "d": d,
+            "device": device,
+        }
+        if self.scale:
+            self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
+        else:
+            self.scaler_ = None
+        self.support_vectors_ = self._dev["Xs"][:, :d].cpu().numpy()
+        self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
+
+    # ------------------------------------------------------------------ inference
+    def decision_function(self, X: np.ndarray) -> np.ndarray:
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        if self._dev is not None:
+            from ..ops import device as D
+
+            dv = self._dev
+            Xq = D.upload_rows(X, dv["device"])
+            if self.scale:
+                _, _, nq = D.minmax_scale_(Xq, dv["d"], dv["mn"], dv["mx"])
+            else:
+                nq = D.row_norms(Xq, dv["d"])
+            return D.decision(dv["Xs"], dv["ns"], dv["coef"], Xq, nq, self.params.gamma, self.b_).cpu().numpy()
+        from ..ops import cpu as C
+
+        Xq = self.scaler_.transform(X) if self.scaler_ is not None else X
+        return C.decision(self.support_vectors_, self.support_labels_, self.alpha_[self.support_], Xq,
+                          self.params.gamma, self.b_, self.params.n_threads)
+
+    def predict(self, X: np.ndarray) -> np.ndarray:
+        dec = self.decision_function(X)
+        pos = dec >= 0 if self.zero_is_positive else dec > 0
+        return np.where(pos, 1, -1).astype(np.int32)
+
+    def score(self, X: np.ndarray, y: np.ndarray) -> float:
+        return float(np.mean(self.predict(X) == np.asarray(y)))
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, directory: str | os.PathLike, ids: Optional[np.ndarray] = None) -> None:
+        """Reference model files (final_sv_{ids,labels,alphas}.txt, final_b.txt) + loadable extras."""
+        from ..models.model_io import save_model
+
+        save_model(directory, ids=self.support_ if ids is None else ids, labels=self.support_labels_,
+                   alphas=self.alpha_[self.support_], b=self.b_, sv_rows=self.support_vectors_,
+                   scaler=self.scaler_, params=self.params, meta={"n_iter": self.n_iter_,
+                                                                  "stop_reason": self.stop_reason_})
+
+    @classmethod
+    def load(cls, directory: str | os.PathLike, device: str = "cpu") -> "SVC":
+        from ..models.model_io import load_model
+
+        m = load_model(directory)
+        p = m["params"]
+        svc = cls(C=p.C, gamma=p.gamma, tol=p.tau, eps=p.eps, sv_tol=p.sv_tol, max_iter=p.max_iter, device=device,
+                  scale=m["scaler"] is not None)
+        svc.scaler_ = m["scaler"]
+        svc.support_ = m["ids"]
+        svc.support_labels_ = m["labels"]
+        svc.b_ = m["b"]
+        svc.intercept_ = -m["b"]
+        svc.support_vectors_ = m["sv_rows"]
+        alphas = m["alphas"]
+        # alpha_ is indexed by training row; a loaded model only knows its SVs.
+        svc.alpha_ = np.zeros(int(svc.support_.max()) + 1 if len(svc.support_) else 0)
+        svc.alpha_[svc.support_] = alphas
+        svc.dual_coef_ = alphas * svc.support_labels_
+        if _resolve_device(device) != "cpu":
+            svc._upload_model(_resolve_device(device))
+        return svc
+
+    def _upload_model(self, dev: str) -> None:
+        import torch
+
+        from ..ops import device as D
+
+        device = torch.device(dev)
+        d = self.support_vectors_.shape[1]
+        Xs = D.upload_rows(self.support_vectors_, device)
+        self._dev = {
+            "Xs": Xs,
+            "ns": D.row_norms(Xs, d),
+            "coef": torch.from_numpy(np.ascontiguousarray(self.dual_coef_)).to(device),
+            "mn": torch.from_numpy(self.scaler_.min_).to(device) if self.scaler_ is not None else None,
+            "mx": torch.from_numpy(self.scaler_.max_).to(device) if self.scaler_ is not None else None,
+            "d": d,
+            "device": device,
+        }

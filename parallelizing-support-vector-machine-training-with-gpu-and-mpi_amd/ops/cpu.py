@@ -1,0 +1,90 @@
+"""CPU ops backed by the native core (libsvm355_core.so): the reference-exact oracle.
+
+These implement main3.cpp's serial semantics (SMO_train :162-294, warm start
+mpi_svm_main3.cpp:155-290, predict :391-402).  ``n_threads > 1`` parallelises the O(n) loops
+without changing any result bit.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from .. import _native as N
+from ..utils.config import SVMParams
+from .device import SMOResult
+
+
+def _c64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _c32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def smo_train(X: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[np.ndarray] = None,
+              warm: bool = False, trace_cap: int = 0, verbose: int = 0
+              ) -> Tuple[np.ndarray, SMOResult, Optional[np.ndarray]]:
+    """SMO on (already scaled) rows X with labels y in {+1,-1}.  Returns (alpha, result, trace)."""
+    X = _c64(X)
+    y = _c32(y)
+    n, d = X.shape
+    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    r = N.SvmResult()
+    trace = np.zeros((trace_cap, 2), dtype=np.int64) if trace_cap > 0 else None
+    p = params.to_struct(verbose)
+    N.check(N.core().svm_smo_train(N.ptr(X), N.ptr(y), n, d, N.ptr(a), int(warm), ctypes.byref(p), ctypes.byref(r),
+                                   N.ptr(trace) if trace is not None else None, trace_cap), "svm_smo_train")
+    res = SMOResult.from_struct(r)
+    if trace is not None:
+        trace = trace[: max(0, min(trace_cap, res.iterations - 1))]
+    return a, res, trace
+
+
+def smo_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[np.ndarray] = None,
+                   warm: bool = False, trace_cap: int = 0) -> Tuple[np.ndarray, SMOResult, Optional[np.ndarray]]:
+    K = _c64(K)
+    y = _c32(y)
+    n = y.shape[0]
+    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    r = N.SvmResult()
+    trace = np.zeros((trace_cap, 2), dtype=np.int64) if trace_cap > 0 else None
+    p = params.to_struct()
+    N.check(N.core().svm_smo_train_gram(N.ptr(K), K.shape[1], N.ptr(y), n, N.ptr(a), int(warm), ctypes.byref(p),
+                                        ctypes.byref(r), N.ptr(trace) if trace is not None else None, trace_cap),
+            "svm_smo_train_gram")
+    res = SMOResult.from_struct(r)
+    if trace is not None:
+        trace = trace[: max(0, min(trace_cap, res.iterations - 1))]
+    return a, res, trace
+
+
+def rbf_matrix(A: np.ndarray, B: np.ndarray, gamma: float, n_threads: int = 0) -> np.ndarray:
+    """Reference-exact RBF kernel matrix (direct sum of squared differences)."""
+    A = _c64(A)
+    B = _c64(B)
+    K = np.empty((A.shape[0], B.shape[0]))
+    N.check(N.core().svm_rbf_matrix(N.ptr(A), A.shape[0], N.ptr(B), B.shape[0], A.shape[1], float(gamma), N.ptr(K),
+                                    int(n_threads)), "svm_rbf_matrix")
+    return K
+
+
+def decision(Xs: np.ndarray, ys: np.ndarray, alphas: np.ndarray, Xq: np.ndarray, gamma: float, b: float,
+             n_threads: int = 0) -> np.ndarray:
+    Xs = _c64(Xs).reshape(-1, Xq.shape[1])
+    ys = _c32(ys)
+    alphas = _c64(alphas)
+    Xq = _c64(Xq)
+    out = np.empty(Xq.shape[0])
+    N.check(N.core().svm_decision(N.ptr(Xs), N.ptr(ys), N.ptr(alphas), Xs.shape[0], N.ptr(Xq), Xq.shape[0],
+                                  Xq.shape[1], float(gamma), float(b), N.ptr(out), int(n_threads)), "svm_decision")
+    return out
+
+
+def sv_indices(alpha: np.ndarray, tol: float = 1e-8) -> np.ndarray:
+    alpha = _c64(alpha)
+    out = np.empty(alpha.shape[0], dtype=np.int64)
+    k = N.core().svm_sv_indices(N.ptr(alpha), alpha.shape[0], float(tol), N.ptr(out))
+    return out[:k].copy()

@@ -1,0 +1,227 @@
+"""Device ops on PyTorch-ROCm tensors backed by the hand-written gfx950 kernels (libsvm355_hip.so).
+
+Every op enqueues on the tensor's device behind PyTorch's current stream (the device context is
+re-bound to ``torch.cuda.current_stream()`` on every call), so these compose with ordinary torch
+code.  Feature matrices are ``(n, ld)`` float64 with ``ld = padded_dim(d)`` (multiple of 16,
+zero-padded).  A missing or unloadable device library raises :class:`svm355._native.NativeError`:
+there is no eager/torch fallback for any of these kernels.
+
+Reference kernels these replace (/root/reference/code/gpu_svm_main3.cu): find_min_max :62-95,
+scale_features :100-116, calc_kernel_matrix :137-147, init/WSS/update kernels :152-272,
+predict + reduce_sum :277-315.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..utils.config import SVMParams
+
+
+@dataclass
+class SMOResult:
+    iterations: int
+    b: float
+    b_high: float
+    b_low: float
+    stop_reason: str
+    n_sv: int
+    seconds: float
+
+    @classmethod
+    def from_struct(cls, r: N.SvmResult) -> "SMOResult":
+        return cls(int(r.iterations), float(r.b), float(r.b_high), float(r.b_low),
+                   N.STOP_NAMES.get(int(r.stop_reason), str(r.stop_reason)), int(r.n_sv), float(r.seconds))
+
+
+class DeviceContext:
+    """One native device context (private HIP stream + workspace) per GPU per host thread
+    (thread-ranks of ``ThreadTransport`` sharing a GPU must not share a workspace)."""
+
+    _ctxs: dict = {}
+    _lock = threading.Lock()
+
+    def __init__(self, index: int):
+        self.index = index
+        self.lib = N.hip()
+        with torch.cuda.device(index):
+            self.handle = self.lib.svmd_create(index)
+        if not self.handle:
+            raise N.NativeError(f"svmd_create({index}) failed: {N.last_error()}")
+
+    @classmethod
+    def get(cls, device) -> "DeviceContext":
+        index = torch.device(device).index
+        if index is None:
+            index = torch.cuda.current_device()
+        key = (index, threading.get_ident())
+        with cls._lock:
+            ctx = cls._ctxs.get(key)
+            if ctx is None:
+                ctx = cls._ctxs[key] = DeviceContext(index)
+        return ctx
+
+    def bind(self) -> int:
+        stream = torch.cuda.current_stream(self.index)
+        N.check(self.lib.svmd_set_stream(self.handle, stream.cuda_stream), "svmd_set_stream")
+        return self.handle
+
+
+def _ctx_for(t: torch.Tensor) -> DeviceContext:
+    if not t.is_cuda:
+        raise ValueError("device op needs a GPU tensor")
+    return DeviceContext.get(t.device)
+
+
+def _check_rows(X: torch.Tensor, name: str = "X") -> None:
+    if X.dtype != torch.float64 or X.dim() != 2 or not X.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous 2-D float64 tensor, got {X.dtype} {tuple(X.shape)}")
+    if X.shape[1] % 16:
+        raise ValueError(f"{name} row length must be a multiple of 16 (use padded_dim), got {X.shape[1]}")
+
+
+def padded_dim(d: int) -> int:
+    return (int(d) + 15) // 16 * 16
+
+
+def available() -> bool:
+    """True if a GPU is visible and the device library loads."""
+    if not torch.cuda.is_available():
+        return False
+    N.hip()
+    return True
+
+
+def upload_rows(X: np.ndarray, device, ld: Optional[int] = None) -> torch.Tensor:
+    """Host (n, d) float64 -> device (n, ld) zero-padded rows (hipMemcpy2DAsync)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, d = X.shape
+    ld = padded_dim(d) if ld is None else ld
+    out = torch.empty((n, ld), dtype=torch.float64, device=device)
+    ctx = DeviceContext.get(out.device)
+    N.check(ctx.lib.svmd_upload_rows(ctx.bind(), N.ptr(X), n, d, N.ptr(out), ld), "svmd_upload_rows")
+    return out
+
+
+def minmax(X: torch.Tensor, d: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Column min/max of the first d columns (one streaming pass, per-block partials)."""
+    _check_rows(X)
+    ctx = _ctx_for(X)
+    mn = torch.empty(d, dtype=torch.float64, device=X.device)
+    mx = torch.empty(d, dtype=torch.float64, device=X.device)
+    N.check(ctx.lib.svmd_minmax(ctx.bind(), N.ptr(X), X.shape[0], d, X.shape[1], N.ptr(mn), N.ptr(mx)),
+            "svmd_minmax")
+    return mn, mx
+
+
+def minmax_scale_(X: torch.Tensor, d: int, mn: Optional[torch.Tensor] = None,
+                  mx: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """In-place min-max scaling of the first d columns; returns (min, max, squared row norms).
+
+    With mn/mx given they are used as-is (test data scaled with training statistics)."""
+    _check_rows(X)
+    ctx = _ctx_for(X)
+    n = X.shape[0]
+    use_given = mn is not None
+    if not use_given:
+        mn = torch.empty(d, dtype=torch.float64, device=X.device)
+        mx = torch.empty(d, dtype=torch.float64, device=X.device)
+    sqn = torch.empty(n, dtype=torch.float64, device=X.device)
+    N.check(ctx.lib.svmd_preprocess(ctx.bind(), N.ptr(X), n, d, X.shape[1], N.ptr(mn), N.ptr(mx), N.ptr(sqn),
+                                    int(use_given)), "svmd_preprocess")
+    return mn, mx, sqn
+
+
+def row_norms(X: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
+    _check_rows(X)
+    ctx = _ctx_for(X)
+    d = X.shape[1] if d is None else d
+    out = torch.empty(X.shape[0], dtype=torch.float64, device=X.device)
+    N.check(ctx.lib.svmd_row_norms(ctx.bind(), N.ptr(X), X.shape[0], d, X.shape[1], N.ptr(out)), "svmd_row_norms")
+    return out
+
+
+def rbf_gram(A: torch.Tensor, nA: torch.Tensor, B: torch.Tensor, nB: torch.Tensor, gamma: float,
+             symmetric: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K[i, j] = exp(-gamma ||A_i - B_j||^2) on MFMA f64 tiles (diagonal forced to 1 if symmetric)."""
+    _check_rows(A, "A")
+    _check_rows(B, "B")
+    if A.shape[1] != B.shape[1]:
+        raise ValueError("A and B row lengths differ")
+    m, n = A.shape[0], B.shape[0]
+    if out is None:
+        ldk = (n + 1) // 2 * 2
+        out = torch.empty((m, ldk), dtype=torch.float64, device=A.device)
+    ctx = _ctx_for(A)
+    N.check(ctx.lib.svmd_rbf_gram(ctx.bind(), N.ptr(A), N.ptr(nA), m, A.shape[1], N.ptr(B), N.ptr(nB), n,
+                                  B.shape[1], A.shape[1], float(gamma), N.ptr(out), out.stride(0), int(symmetric)),
+            "svmd_rbf_gram")
+    return out
+
+
+def smo(K: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, warm: bool = False,
+        n: Optional[int] = None, trace_cap: int = 0) -> Tuple[SMOResult, Optional[np.ndarray]]:
+    """Device-resident SMO on a kernel matrix; alpha is updated in place."""
+    n = K.shape[0] if n is None else n
+    if y.dtype != torch.int32 or alpha.dtype != torch.float64:
+        raise ValueError("y must be int32 (+-1) and alpha float64")
+    ctx = _ctx_for(K)
+    r = N.SvmResult()
+    trace = np.zeros((max(trace_cap, 0), 2), dtype=np.int64) if trace_cap > 0 else None
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_smo(ctx.bind(), N.ptr(K), K.stride(0), N.ptr(y), n, N.ptr(alpha), int(warm),
+                             ctypes.byref(p), ctypes.byref(r), N.ptr(trace) if trace is not None else None,
+                             trace_cap), "svmd_smo")
+    res = SMOResult.from_struct(r)
+    if trace is not None:
+        trace = trace[: max(0, min(trace_cap, res.iterations - 1))]
+    return res, trace
+
+
+def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams,
+          warm: bool = False, K: Optional[torch.Tensor] = None) -> Tuple[SMOResult, dict]:
+    """RBF Gram (into K, allocated by torch if None) + SMO.  Returns (result, timing dict in ms)."""
+    _check_rows(X)
+    n = X.shape[0]
+    if K is None:
+        K = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+    ctx = _ctx_for(X)
+    r = N.SvmResult()
+    tm = N.SvmdTiming()
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_train(ctx.bind(), N.ptr(X), N.ptr(sqn), n, X.shape[1], X.shape[1], N.ptr(y),
+                               N.ptr(alpha), int(warm), ctypes.byref(p), ctypes.byref(r), N.ptr(K), K.stride(0),
+                               ctypes.byref(tm)), "svmd_train")
+    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms}
+
+
+def decision(Xs: torch.Tensor, ns: torch.Tensor, coef: torch.Tensor, Xq: torch.Tensor, nq: torch.Tensor,
+             gamma: float, b: float) -> torch.Tensor:
+    """out[i] = sum_k coef[k] K(Xq_i, Xs_k) - b (MFMA cross-kernel + deterministic GEMV)."""
+    _check_rows(Xq, "Xq")
+    m = Xq.shape[0]
+    out = torch.empty(m, dtype=torch.float64, device=Xq.device)
+    nsv = Xs.shape[0]
+    ctx = _ctx_for(Xq)
+    N.check(ctx.lib.svmd_decision(ctx.bind(), N.ptr(Xs) if nsv else None, N.ptr(ns) if nsv else None,
+                                  N.ptr(coef) if nsv else None, nsv, Xq.shape[1], N.ptr(Xq), N.ptr(nq), m,
+                                  Xq.shape[1], Xq.shape[1], float(gamma), float(b), N.ptr(out)), "svmd_decision")
+    return out
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """dst[k] = src[idx[k]] (device row gather, idx int64 on the same device)."""
+    _check_rows(src, "src")
+    idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+    out = torch.empty((idx.numel(), src.shape[1]), dtype=torch.float64, device=src.device)
+    if idx.numel():
+        ctx = _ctx_for(src)
+        N.check(ctx.lib.svmd_gather_rows(ctx.bind(), N.ptr(src), src.shape[1], N.ptr(idx), idx.numel(),
+                                         N.ptr(out)), "svmd_gather_rows")
+    return out

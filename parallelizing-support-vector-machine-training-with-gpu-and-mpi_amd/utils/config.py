@@ -1,0 +1,39 @@
+"""Solver hyper-parameters (the reference's compile-time constants).
+
+| knob      | default  | reference site                                   |
+|-----------|----------|--------------------------------------------------|
+| C         | 10.0     | main3.cpp:163,342; gpu_svm_main3.cu:319,601      |
+| gamma     | 0.00125  | main3.cpp:95 (hard-coded inside kernel())        |
+| tau       | 1e-5     | main3.cpp:196,213 (stop: b_low <= b_high + 2 tau)|
+| eps       | 1e-12    | main3.cpp:109,128,165 (set membership, eta floor)|
+| sv_tol    | 1e-8     | main3.cpp:297,367 (alpha > sv_tol is an SV)      |
+| max_iter  | 100000   | main3.cpp:197-198 (num_iter starts at 1)         |
+| max_rounds| 50       | mpi_svm_main3.cpp:544, mpi_svm_main2.cpp:428     |
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass
+
+from .._native import params_struct
+
+
+@dataclass
+class SVMParams:
+    C: float = 10.0
+    gamma: float = 0.00125
+    tau: float = 1e-5
+    eps: float = 1e-12
+    sv_tol: float = 1e-8
+    max_iter: int = 100000
+    n_threads: int = 1
+
+    def to_struct(self, verbose: int = 0):
+        return params_struct(self.C, self.gamma, self.tau, self.eps, self.sv_tol, self.max_iter,
+                             self.n_threads, verbose)
+
+    def replace(self, **kw) -> "SVMParams":
+        return dataclasses.replace(self, **kw)
+
+    def as_dict(self) -> dict:
+        return dataclasses.asdict(self)

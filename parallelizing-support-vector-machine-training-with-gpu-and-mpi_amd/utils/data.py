@@ -1,0 +1,109 @@
+"""L0/L1 data layer: CSV datasets, MNIST-shaped synthetic data, min-max scaling.
+
+``load_csv`` mirrors ``read_CSV`` (main3.cpp:13-54, row-limited gpu_svm_main4.cu:16-59) through
+the native parser; ``MinMaxScaler`` mirrors ``find_min_max``/``scale_features`` (main3.cpp:57-89)
+including the ``range < 1e-12 -> 1`` rule.  ``synthetic_mnist`` produces a deterministic
+MNIST-shaped problem (784 integer pixels, digit labels 0-9) because the reference's MNIST CSVs are
+not part of the reference repository.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .. import _native as N
+
+MNIST_D = 784
+
+
+@dataclass
+class Dataset:
+    X: np.ndarray  # (n, d) float64, C-contiguous
+    y: np.ndarray  # (n,) int32 in {+1, -1}
+    labels: np.ndarray  # (n,) int32 raw labels
+
+    @property
+    def n(self) -> int:
+        return int(self.X.shape[0])
+
+    @property
+    def d(self) -> int:
+        return int(self.X.shape[1])
+
+    def subset(self, start: int, stop: int) -> "Dataset":
+        return Dataset(self.X[start:stop], self.y[start:stop], self.labels[start:stop])
+
+
+def one_vs_rest(labels: np.ndarray, positive_label: int = 1) -> np.ndarray:
+    """label == positive_label -> +1, else -1 (main3.cpp:49-52 with positive_label = 1)."""
+    return np.where(np.asarray(labels) == positive_label, 1, -1).astype(np.int32)
+
+
+def load_csv(path: str | os.PathLike, limit: Optional[int] = None, positive_label: int = 1,
+             n_threads: int = 0) -> Dataset:
+    lib = N.core()
+    h = lib.svm_csv_load(os.fsencode(str(path)), -1 if limit is None else int(limit), int(positive_label),
+                         int(n_threads))
+    if not h:
+        raise FileNotFoundError(N.last_error())
+    try:
+        n, d = ctypes.c_int64(), ctypes.c_int64()
+        N.check(lib.svm_dataset_dims(h, ctypes.byref(n), ctypes.byref(d)), "svm_dataset_dims")
+        X = np.empty((n.value, d.value), dtype=np.float64)
+        y = np.empty(n.value, dtype=np.int32)
+        lab = np.empty(n.value, dtype=np.int32)
+        N.check(lib.svm_dataset_copy(h, N.ptr(X), N.ptr(y), N.ptr(lab)), "svm_dataset_copy")
+    finally:
+        lib.svm_dataset_free(h)
+    return Dataset(X, y, lab)
+
+
+def write_csv(path: str | os.PathLike, X: np.ndarray, labels: np.ndarray) -> None:
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    labels = np.ascontiguousarray(labels, dtype=np.int32)
+    N.check(N.core().svm_csv_write(os.fsencode(str(path)), N.ptr(X), N.ptr(labels), X.shape[0], X.shape[1]),
+            "svm_csv_write")
+
+
+def synthetic_mnist(n: int, seed: int = 2024, offset: int = 0, positive_label: int = 1,
+                    n_threads: int = 0) -> Dataset:
+    """Rows [offset, offset + n) of the deterministic MNIST-shaped generator (see csrc/core/synth.cpp).
+
+    Row i depends only on (seed, i): a train split [0, N) and a test split [N, N + M) are disjoint
+    draws of the same distribution, and any rank can generate exactly its own partition.
+    """
+    X = np.empty((n, MNIST_D), dtype=np.float64)
+    lab = np.empty(n, dtype=np.int32)
+    N.check(N.core().svm_synth_mnist(int(seed), int(offset), int(n), N.ptr(X), N.ptr(lab), int(n_threads)),
+            "svm_synth_mnist")
+    return Dataset(X, one_vs_rest(lab, positive_label), lab)
+
+
+class MinMaxScaler:
+    """Column min-max scaling to [0, 1] with the reference's degenerate-range rule."""
+
+    def __init__(self, min_: Optional[np.ndarray] = None, max_: Optional[np.ndarray] = None):
+        self.min_ = min_
+        self.max_ = max_
+
+    def fit(self, X: np.ndarray) -> "MinMaxScaler":
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        self.min_ = np.empty(X.shape[1])
+        self.max_ = np.empty(X.shape[1])
+        N.check(N.core().svm_minmax(N.ptr(X), X.shape[0], X.shape[1], N.ptr(self.min_), N.ptr(self.max_)),
+                "svm_minmax")
+        return self
+
+    def transform(self, X: np.ndarray, copy: bool = True) -> np.ndarray:
+        X = np.array(X, dtype=np.float64, order="C", copy=copy)
+        if X.shape[0]:
+            N.check(N.core().svm_scale(N.ptr(X), X.shape[0], X.shape[1], N.ptr(self.min_), N.ptr(self.max_)),
+                    "svm_scale")
+        return X
+
+    def fit_transform(self, X: np.ndarray) -> np.ndarray:
+        return self.fit(X).transform(X)

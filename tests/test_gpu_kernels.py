@@ -1,0 +1,243 @@
+"""gfx950 kernels vs plain fp64 references, and the device SMO vs the CPU oracle.
+
+Numerics tests compare each HIP kernel with a PyTorch/numpy fp64 computation of the same op; the
+device SMO is checked bit-for-bit against the CPU oracle when both run on the same kernel matrix.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from svm355 import SVC, SVMParams
+from svm355.ops import cpu as C
+from svm355.utils.data import MinMaxScaler, synthetic_mnist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from svm355.ops import device as D
+
+    assert D.available(), "GPU visible but the HIP device library did not load"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def D():
+    from svm355.ops import device as D
+
+    return D
+
+
+@pytest.fixture(scope="module")
+def mn_data():
+    return synthetic_mnist(1500, seed=5), synthetic_mnist(500, seed=5, offset=1500)
+
+
+def test_native_library_is_loaded(dev):
+    from svm355 import _native as N
+
+    assert N._hip is not None
+    with open("/proc/self/maps") as f:
+        maps = f.read()
+    assert "libsvm355_hip.so" in maps
+
+
+def test_minmax_scale_norms(dev, D, mn_data):
+    tr, _ = mn_data
+    X = tr.X[:777].copy()
+    X[:, 5] = 3.0  # constant column
+    Xd = D.upload_rows(X, dev)
+    assert Xd.shape == (777, 784) and torch.all(Xd[:, 784:] == 0)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    sc = MinMaxScaler().fit(X)
+    np.testing.assert_array_equal(mn.cpu().numpy(), sc.min_)
+    np.testing.assert_array_equal(mx.cpu().numpy(), sc.max_)
+    Xs = sc.transform(X)
+    np.testing.assert_array_equal(Xd[:, :784].cpu().numpy(), Xs)  # true division: bit-identical
+    np.testing.assert_allclose(sqn.cpu().numpy(), (Xs ** 2).sum(1), rtol=1e-13)
+    # test data with the training statistics
+    Xq = D.upload_rows(X[:50] * 1.1, dev)
+    D.minmax_scale_(Xq, 784, mn, mx)
+    np.testing.assert_array_equal(Xq[:, :784].cpu().numpy(), sc.transform(X[:50] * 1.1))
+
+
+def test_minmax_odd_width(dev, D):
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(1000, 37))
+    Xd = D.upload_rows(X, dev)
+    assert Xd.shape[1] == 48
+    mn, mx = D.minmax(Xd, 37)
+    np.testing.assert_array_equal(mn.cpu().numpy(), X.min(0))
+    np.testing.assert_array_equal(mx.cpu().numpy(), X.max(0))
+
+
+@pytest.mark.parametrize("m,n,d", [(300, 257, 784), (128, 128, 16), (1, 5, 33), (517, 1029, 100)])
+def test_rbf_gram_vs_fp64_reference(dev, D, m, n, d):
+    rng = np.random.default_rng(m + n + d)
+    A = rng.uniform(0, 1, size=(m, d))
+    B = rng.uniform(0, 1, size=(n, d))
+    gamma = 0.5 / d
+    Ad, Bd = D.upload_rows(A, dev), D.upload_rows(B, dev)
+    K = D.rbf_gram(Ad, D.row_norms(Ad, d), Bd, D.row_norms(Bd, d), gamma)
+    ref = C.rbf_matrix(A, B, gamma)
+    np.testing.assert_allclose(K[:, :n].cpu().numpy(), ref, rtol=0, atol=2e-14)
+
+
+def test_rbf_gram_symmetric_diag_exact(dev, D, mn_data):
+    tr, _ = mn_data
+    X = MinMaxScaler().fit_transform(tr.X[:600])
+    Xd = D.upload_rows(X, dev)
+    nrm = D.row_norms(Xd, 784)
+    K = D.rbf_gram(Xd, nrm, Xd, nrm, 0.00125, symmetric=True)[:, :600].cpu().numpy()
+    assert np.all(np.diag(K) == 1.0)
+    np.testing.assert_array_equal(K, K.T)  # exactly symmetric
+    np.testing.assert_allclose(K, C.rbf_matrix(X, X, 0.00125), rtol=0, atol=1e-13)
+
+
+def test_gather_rows(dev, D):
+    X = torch.arange(40 * 32, dtype=torch.float64, device=dev).reshape(40, 32)
+    idx = torch.tensor([5, 0, 39, 5], device=dev)
+    assert torch.equal(D.gather_rows(X, idx), X[idx])
+
+
+def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data):
+    tr, _ = mn_data
+    X = MinMaxScaler().fit_transform(tr.X[:900])
+    y = tr.y[:900]
+    p = SVMParams(n_threads=8)
+    K = C.rbf_matrix(X, X, p.gamma, 8)
+    a_cpu, r_cpu, t_cpu = C.smo_train_gram(K, y, p, trace_cap=200000)
+    Kd = torch.from_numpy(K).to(dev)
+    yd = torch.from_numpy(y).to(dev)
+    ad = torch.zeros(900, dtype=torch.float64, device=dev)
+    r_gpu, t_gpu = D.smo(Kd, yd, ad, p, trace_cap=200000)
+    assert r_gpu.iterations == r_cpu.iterations
+    assert r_gpu.stop_reason == r_cpu.stop_reason == "converged"
+    np.testing.assert_array_equal(t_gpu, t_cpu)
+    np.testing.assert_array_equal(ad.cpu().numpy(), a_cpu)
+    assert r_gpu.b == r_cpu.b
+
+
+def test_device_smo_warm_start_bit_identical(dev, D, mn_data):
+    tr, _ = mn_data
+    X = MinMaxScaler().fit_transform(tr.X[:700])
+    y = tr.y[:700]
+    p = SVMParams(n_threads=8)
+    K = C.rbf_matrix(X, X, p.gamma, 8)
+    a_cold, _, _ = C.smo_train_gram(K, y, p)
+    a0 = a_cold * 0.5
+    a_cpu, r_cpu, _ = C.smo_train_gram(K, y, p, alpha=a0, warm=True)
+    ad = torch.from_numpy(a0.copy()).to(dev)
+    r_gpu, _ = D.smo(torch.from_numpy(K).to(dev), torch.from_numpy(y).to(dev), ad, p, warm=True)
+    assert r_gpu.iterations == r_cpu.iterations
+    np.testing.assert_array_equal(ad.cpu().numpy(), a_cpu)
+    assert r_gpu.b == r_cpu.b
+
+
+def test_device_smo_stop_reasons(dev, D, mn_data):
+    tr, _ = mn_data
+    X = MinMaxScaler().fit_transform(tr.X[:300])
+    K = torch.from_numpy(C.rbf_matrix(X, X, 0.00125)).to(dev)
+    y = torch.from_numpy(tr.y[:300]).to(dev)
+    a = torch.zeros(300, dtype=torch.float64, device=dev)
+    r, tr_ = D.smo(K, y, a, SVMParams(max_iter=7), trace_cap=50)
+    assert r.stop_reason == "max_iter" and r.iterations == 8 and tr_.shape == (7, 2)
+    r, _ = D.smo(K, torch.ones(300, dtype=torch.int32, device=dev), a, SVMParams())
+    assert r.stop_reason == "no_candidate"
+
+
+def test_device_train_matches_oracle(dev, D, mn_data):
+    """Full device path (MFMA Gram + SMO): same optimum as the oracle (K differs in the last ulps)."""
+    tr, _ = mn_data
+    sc = MinMaxScaler().fit(tr.X)
+    a_cpu, r_cpu, _ = C.smo_train(sc.transform(tr.X), tr.y, SVMParams(n_threads=8))
+    Xd = D.upload_rows(tr.X, dev)
+    _, _, sqn = D.minmax_scale_(Xd, 784)
+    ad = torch.zeros(tr.n, dtype=torch.float64, device=dev)
+    r_gpu, tm = D.train(Xd, sqn, torch.from_numpy(tr.y).to(dev), ad, SVMParams())
+    a_gpu = ad.cpu().numpy()
+    assert r_gpu.stop_reason == "converged"
+    assert abs(r_gpu.iterations - r_cpu.iterations) <= max(5, r_cpu.iterations // 50)
+    s_cpu = set(np.flatnonzero(a_cpu > 1e-8).tolist())
+    s_gpu = set(np.flatnonzero(a_gpu > 1e-8).tolist())
+    assert len(s_cpu ^ s_gpu) <= 2
+    assert abs(r_gpu.b - r_cpu.b) < 1e-6 * max(1, abs(r_cpu.b))
+    np.testing.assert_allclose(a_gpu, a_cpu, atol=1e-6)
+
+
+def test_decision_vs_fp64_reference(dev, D, mn_data):
+    tr, te = mn_data
+    sc = MinMaxScaler().fit(tr.X)
+    Xs, Xq = sc.transform(tr.X[:333]), sc.transform(te.X[:211])
+    rng = np.random.default_rng(3)
+    coef = rng.uniform(-10, 10, 333)
+    Xsd, Xqd = D.upload_rows(Xs, dev), D.upload_rows(Xq, dev)
+    out = D.decision(Xsd, D.row_norms(Xsd, 784), torch.from_numpy(coef).to(dev), Xqd, D.row_norms(Xqd, 784),
+                     0.00125, 0.75).cpu().numpy()
+    ref = C.rbf_matrix(Xq, Xs, 0.00125) @ coef - 0.75
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-11)
+
+
+def test_svc_cuda_matches_cpu(dev, mn_data):
+    tr, te = mn_data
+    g = SVC(device="cuda").fit(tr.X, tr.y)
+    c = SVC(device="cpu", n_threads=8).fit(tr.X, tr.y)
+    assert abs(g.b_ - c.b_) < 1e-6 * max(1, abs(c.b_))
+    assert len(set(g.support_.tolist()) ^ set(c.support_.tolist())) <= 2
+    np.testing.assert_allclose(g.decision_function(te.X), c.decision_function(te.X), atol=1e-5)
+    assert g.score(te.X, te.y) == c.score(te.X, te.y)
+
+
+def test_svc_cuda_save_load(tmp_path, dev, mn_data):
+    tr, te = mn_data
+    g = SVC(device="cuda").fit(tr.X, tr.y)
+    g.save(tmp_path / "m")
+    g2 = SVC.load(tmp_path / "m", device="cuda")
+    np.testing.assert_allclose(g2.decision_function(te.X), g.decision_function(te.X), atol=1e-12)
+
+
+def test_cascade_thread_ranks_on_one_gpu(dev, mn_data):
+    from svm355.parallel.cascade import CascadeSVM, partition_bounds
+    from svm355.parallel.transport import run_threads
+
+    tr, te = mn_data
+
+    def fn(t):
+        lo, hi = partition_bounds(tr.n, t.world, t.rank)
+        c = CascadeSVM(t, SVMParams(), topology="star", verbose=0)
+        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=tr.n)
+        return c.summary(), c.score(te.X, te.y)
+
+    out = run_threads(2, fn, device_for_rank=lambda r: dev)
+    assert out[0][0]["converged"] and out[0][0]["n_sv"] == out[1][0]["n_sv"]
+    single = SVC(device="cuda").fit(tr.X, tr.y)
+    assert abs(out[0][0]["n_sv"] - len(single.support_)) <= max(3, len(single.support_) // 50)
+    assert out[0][1] >= single.score(te.X, te.y) - 0.01
+
+
+def test_cascade_rccl_single_rank_group(dev, mn_data):
+    """TorchDistTransport over the nccl (= RCCL) backend, world size 1, both topologies."""
+    import torch.distributed as dist
+
+    from svm355.parallel.cascade import CascadeSVM
+    from svm355.parallel.transport import TorchDistTransport
+
+    tr, te = mn_data
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        t = TorchDistTransport(dev)
+        for topo in ("star", "tree"):
+            c = CascadeSVM(t, SVMParams(), topology=topo, verbose=0)
+            c.fit(tr.X, tr.y, np.arange(tr.n), n_total=tr.n)
+            assert c.result.converged
+            assert c.score(te.X, te.y) > 0.95
+    finally:
+        dist.destroy_process_group()
