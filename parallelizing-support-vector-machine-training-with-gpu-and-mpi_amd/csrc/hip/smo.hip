@@ -20,6 +20,8 @@
 // operation by operation (built with -ffp-contract=off), so on an identical kernel matrix the
 // trajectory is bit-identical to the CPU oracle.
 #include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "ctx.h"
@@ -259,6 +261,430 @@ __global__ __launch_bounds__(256) void warm_f_kernel(const double* __restrict__ 
   f[i] = sum - static_cast<double>(y[i]);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Persistent SMO: the whole solve in ONE launch.
+//
+// G workgroups (G <= #CUs, all co-resident) each own a contiguous slice of the training points and
+// keep f, alpha and y of that slice in registers for the entire solve.  One iteration:
+//   1. local masked argmin over I_high / argmax over I_low of the slice (wave64 butterfly + LDS),
+//      carrying alpha of the winners;
+//   2. publish the workgroup's two candidates as ten 8-byte {epoch, 32-bit payload} granules with
+//      agent-scope relaxed (sc1) stores — a granule is written by one store and needs no fence;
+//   3. wave 0 of EVERY workgroup sweeps all G candidate records (relaxed agent loads, s_sleep
+//      between polls) until every tag equals the epoch, and reduces them with the lowest-index
+//      rule: every workgroup obtains the identical (i_high, i_low, b_high, b_low, alpha_h, alpha_l);
+//   4. every workgroup evaluates the stop tests and the two-variable update redundantly (same
+//      inputs, same instruction sequence -> same bits), issuing the K11/K22/K12 and y loads in the
+//      same memory round trip as its slice of rows K[i_high,:] and K[i_low,:];
+//   5. the owners of i_high / i_low update their register alpha; every slice applies the f update.
+// Records are double-buffered by epoch parity (a workgroup can be at most one epoch ahead of the
+// slowest reader).  Every spin is bounded; a timeout sets *err and all workgroups drain.
+// Per iteration this costs one HBM round trip plus one all-to-all granule exchange, instead of two
+// kernel boundaries and a single-workgroup tail (smo_select_kernel + smo_step_kernel).
+constexpr int kGranules = 10;    // per candidate record
+constexpr int kRecStride = 16;   // granules per record slot (128 B)
+constexpr int kMaxG = 64;        // one sweep pass: lane L of wave 0 reads workgroup L's record
+constexpr uint32_t kSentinel = 0x7FFFFFFFu;  // "no candidate" index (n < 2^31)
+
+__device__ __forceinline__ uint32_t lo32(double x) { return uint32_t(__double_as_longlong(x)); }
+__device__ __forceinline__ uint32_t hi32(double x) { return uint32_t(uint64_t(__double_as_longlong(x)) >> 32); }
+__device__ __forceinline__ double mk64(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+}
+
+// ---- wave64 arg-reductions on (double value, uint32 index) without LDS traffic.
+// Steps: DPP quad_perm xor1, xor2, row_half_mirror (8), row_mirror (16), then the gfx950
+// v_permlane16_swap / v_permlane32_swap for the 32- and 64-lane halves.  After each step every
+// lane holds the best of its group (lexicographic (value, index): the serial lowest-index rule),
+// so the result is schedule-independent and identical in every lane.
+struct VI {
+  double v;
+  uint32_t i;
+};
+
+template <bool MIN>
+__device__ __forceinline__ bool better(VI a, VI b) {  // does b replace a?
+  return MIN ? (b.v < a.v || (b.v == a.v && b.i < a.i)) : (b.v > a.v || (b.v == a.v && b.i < a.i));
+}
+template <bool MIN>
+__device__ __forceinline__ VI pick(VI a, VI b) {
+  return better<MIN>(a, b) ? b : a;
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(x), CTRL, 0xF, 0xF, false));
+}
+template <bool MIN, int CTRL>
+__device__ __forceinline__ VI step_dpp(VI a) {
+  const VI b{mk64(dpp32<CTRL>(lo32(a.v)), dpp32<CTRL>(hi32(a.v))), dpp32<CTRL>(a.i)};
+  return pick<MIN>(a, b);
+}
+template <bool MIN, bool S32>
+__device__ __forceinline__ VI step_swap(VI a) {
+  const uint32_t l = lo32(a.v), h = hi32(a.v);
+  if constexpr (S32) {
+    const auto L = __builtin_amdgcn_permlane32_swap(l, l, false, false);
+    const auto H = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+    const auto I = __builtin_amdgcn_permlane32_swap(a.i, a.i, false, false);
+    return pick<MIN>(VI{mk64(L[0], H[0]), I[0]}, VI{mk64(L[1], H[1]), I[1]});
+  } else {
+    const auto L = __builtin_amdgcn_permlane16_swap(l, l, false, false);
+    const auto H = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+    const auto I = __builtin_amdgcn_permlane16_swap(a.i, a.i, false, false);
+    return pick<MIN>(VI{mk64(L[0], H[0]), I[0]}, VI{mk64(L[1], H[1]), I[1]});
+  }
+}
+template <bool MIN>
+__device__ __forceinline__ VI wave_arg(VI a) {  // requires a full wave (EXEC = all 64 lanes)
+  a = step_dpp<MIN, 0xB1>(a);   // quad_perm [1,0,3,2]
+  a = step_dpp<MIN, 0x4E>(a);   // quad_perm [2,3,0,1]
+  a = step_dpp<MIN, 0x141>(a);  // row_half_mirror
+  a = step_dpp<MIN, 0x140>(a);  // row_mirror
+  a = step_swap<MIN, false>(a);
+  a = step_swap<MIN, true>(a);
+  return a;
+}
+// Value held by the lane whose index is the (uniform) winner index; 0 if it is the sentinel.
+__device__ __forceinline__ double winner_alpha(uint32_t my_i, double my_a, uint32_t win) {
+  const unsigned long long m = __ballot(my_i == win && win != kSentinel);
+  if (!m) return 0.0;
+  const int src = __builtin_ctzll(m);
+  return mk64(uint32_t(__builtin_amdgcn_readlane(int(lo32(my_a)), src)),
+              uint32_t(__builtin_amdgcn_readlane(int(hi32(my_a)), src)));
+}
+
+struct PersistShared {
+  double wv[2][4], wa[2][4];  // per-wave candidates [min|max][wave]
+  uint32_t wi[2][4];
+  double gv[2], ga[2];        // global winners of the current epoch
+  uint32_t gi[2];
+  int timeout;
+};
+
+// Diagnostic build (STAMP = true, SVM355_PSMO_STAMP=1): workgroup 0 / lane 0 accumulates
+// s_memtime deltas per phase over epochs [kStampFrom, kStampFrom + kStampCount) into stamps[0..7]
+// (stamps[7] = s_memrealtime delta, 100 MHz, for the clock).  Never used in timed runs.
+constexpr uint32_t kStampFrom = 200, kStampCount = 2000;
+#define PSTAMP(k)                                                                   \
+  do {                                                                              \
+    if (STAMP && stamping) {                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      unsigned long long ts_;                                                       \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      sacc[k] += ts_ - sprev;                                                       \
+      sprev = ts_;                                                                  \
+    }                                                                               \
+  } while (0)
+
+template <int E, bool STAMP>
+__global__ __launch_bounds__(256) void smo_persistent_kernel(
+    const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
+    double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
+    SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
+    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps) {
+  __shared__ PersistShared sh;
+  unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = 0, rt0 = 0;
+  bool stamping = false;
+  const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t lo = int64_t(g) * slice, hi_end = std::min<int64_t>(n, lo + slice);
+  const double c_hi = C - eps, c_lo = 0.0 + eps;
+  const double inf = __builtin_inf();
+
+  double fr[E], ar[E];
+  int32_t yr[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t i = lo + t + 256 * e;
+    const bool ok = i < hi_end;
+    fr[e] = ok ? f[i] : 0.0;
+    ar[e] = ok ? alpha[i] : 0.0;
+    yr[e] = ok ? y[i] : 0;  // y = 0 is in neither set
+  }
+  if (t == 0) sh.timeout = 0;
+  int64_t num_iter = st->num_iter;
+  double b_high = st->b_high, b_low = st->b_low;
+  int32_t stop = SVM_STOP_RUNNING;
+
+  for (uint32_t epoch = 1;; ++epoch) {
+    if (STAMP) {
+      const bool on = blockIdx.x == 0 && threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
+      if (on && !stamping) rt0 = __builtin_amdgcn_s_memrealtime();
+      if (!on && stamping) sacc[7] = __builtin_amdgcn_s_memrealtime() - rt0;
+      stamping = on;
+      if (stamping) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sprev)::"memory");
+    }
+    // ---- 1. local selection over the register slice (ascending index within a thread)
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+    double amn = 0.0, amx = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t i = uint32_t(lo + t + 256 * e);
+      const double a = ar[e], fi = fr[e];
+      const int32_t yi = yr[e];
+      const bool in_high = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
+      const bool in_low = (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi);
+      if (in_high && fi < mn.v) {
+        mn = VI{fi, i};
+        amn = a;
+      }
+      if (in_low && fi > mx.v) {
+        mx = VI{fi, i};
+        amx = a;
+      }
+    }
+    {
+      const VI wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
+      const double awmn = winner_alpha(mn.i, amn, wmn.i), awmx = winner_alpha(mx.i, amx, wmx.i);
+      PSTAMP(0);
+      if (lane == 0) {
+        sh.wv[0][w] = wmn.v;
+        sh.wi[0][w] = wmn.i;
+        sh.wa[0][w] = awmn;
+        sh.wv[1][w] = wmx.v;
+        sh.wi[1][w] = wmx.i;
+        sh.wa[1][w] = awmx;
+      }
+    }
+    __syncthreads();
+    PSTAMP(1);
+    unsigned long long* rec = slots + (size_t(epoch & 1) * kMaxG) * kRecStride;
+    if (w == 0) {
+      // ---- 2. merge the 4 waves and publish this workgroup's record (lanes 0..9, one granule each)
+      VI a{sh.wv[0][0], sh.wi[0][0]}, b{sh.wv[1][0], sh.wi[1][0]};
+      double aa = sh.wa[0][0], ba = sh.wa[1][0];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const VI ca{sh.wv[0][k], sh.wi[0][k]}, cb{sh.wv[1][k], sh.wi[1][k]};
+        if (better<true>(a, ca)) {
+          a = ca;
+          aa = sh.wa[0][k];
+        }
+        if (better<false>(b, cb)) {
+          b = cb;
+          ba = sh.wa[1][k];
+        }
+      }
+      if (lane < kGranules) {
+        // Branch-free payload selection (no divergent switch).
+        uint32_t pay = lo32(a.v);
+        pay = lane == 1 ? hi32(a.v) : pay;
+        pay = lane == 2 ? a.i : pay;
+        pay = lane == 3 ? lo32(aa) : pay;
+        pay = lane == 4 ? hi32(aa) : pay;
+        pay = lane == 5 ? lo32(b.v) : pay;
+        pay = lane == 6 ? hi32(b.v) : pay;
+        pay = lane == 7 ? b.i : pay;
+        pay = lane == 8 ? lo32(ba) : pay;
+        pay = lane == 9 ? hi32(ba) : pay;
+        __hip_atomic_store(rec + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      PSTAMP(2);
+      // ---- 3. lane L polls workgroup L's record until its ten tags equal the epoch
+      VI gm{inf, kSentinel}, gx{-inf, kSentinel};
+      double agm = 0.0, agx = 0.0;
+      bool timed_out = false;
+      if (lane < G) {
+        const unsigned long long* r = rec + size_t(lane) * kRecStride;
+        uint32_t v[kGranules];
+        for (int64_t spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < kGranules; ++k) {
+            const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[k] = uint32_t(x);
+            ok &= uint32_t(x >> 32) == epoch;
+          }
+          if (ok) break;
+          if (spins > spin_limit) {
+            timed_out = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!timed_out) {
+          gm = VI{mk64(v[0], v[1]), v[2]};
+          agm = mk64(v[3], v[4]);
+          gx = VI{mk64(v[5], v[6]), v[7]};
+          agx = mk64(v[8], v[9]);
+        }
+      }
+      const bool any_to = __any(timed_out);
+      PSTAMP(3);
+      const VI wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
+      const double awgm = winner_alpha(gm.i, agm, wgm.i), awgx = winner_alpha(gx.i, agx, wgx.i);
+      if (lane == 0) {
+        sh.gv[0] = wgm.v;
+        sh.gi[0] = wgm.i;
+        sh.ga[0] = awgm;
+        sh.gv[1] = wgx.v;
+        sh.gi[1] = wgx.i;
+        sh.ga[1] = awgx;
+        if (any_to) {
+          sh.timeout = 1;
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    __syncthreads();
+    PSTAMP(4);
+    if (sh.timeout) {
+      stop = -1;
+      break;
+    }
+    const uint32_t uih = sh.gi[0], uil = sh.gi[1];
+    // ---- 4. stop tests and the two-variable update (identical in every workgroup)
+    if (uih == kSentinel || uil == kSentinel) {
+      stop = SVM_STOP_NO_CANDIDATE;
+      break;
+    }
+    const int64_t ih = uih, il = uil;
+    const double bh = sh.gv[0], bl = sh.gv[1];
+    b_high = bh;
+    b_low = bl;
+    if (bl <= bh + 2.0 * tau) {
+      stop = SVM_STOP_CONVERGED;
+      break;
+    }
+    // One memory round trip: scalars + this slice of rows i_high and i_low.
+    const int32_t yh = y[ih], yl = y[il];
+    const double K11 = K[ih * ldk + ih], K22 = K[il * ldk + il], K12 = K[ih * ldk + il];
+    double kh[E], kl[E];
+    const double* Kh = K + ih * ldk;
+    const double* Kl = K + il * ldk;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = lo + t + 256 * e;
+      const bool ok = i < hi_end;
+      kh[e] = ok ? Kh[i] : 0.0;
+      kl[e] = ok ? Kl[i] : 0.0;
+    }
+    PSTAMP(5);
+    const double ah = sh.ga[0], al = sh.ga[1];
+    const int s = yh * yl;
+    const double eta = K11 + K22 - 2.0 * K12;
+    double U, V;
+    if (s == -1) {
+      U = fmax(0.0, al - ah);
+      V = fmin(C, C + al - ah);
+    } else {
+      U = fmax(0.0, al + ah - C);
+      V = fmin(C, al + ah);
+    }
+    if (!(U <= V + 1e-12)) {
+      stop = SVM_STOP_INFEASIBLE;
+      break;
+    }
+    if (eta <= eps) {
+      stop = SVM_STOP_NONPOS_ETA;
+      break;
+    }
+    double al_new = al + double(yl) * (bh - bl) / eta;
+    if (al_new > V) al_new = V;
+    if (al_new < U) al_new = U;
+    const double ah_new = ah + double(s) * (al - al_new);
+    const double ch = (ah_new - ah) * double(yh);
+    const double cl = (al_new - al) * double(yl);
+    // ---- 5. apply: f for the whole slice, alpha for the owners
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = lo + t + 256 * e;
+      fr[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
+      if (i == ih) ar[e] = ah_new;
+      if (i == il) ar[e] = al_new;
+    }
+    PSTAMP(6);
+    if (g == 0 && t == 0 && trace && num_iter - 1 < trace_cap) {
+      trace[2 * (num_iter - 1)] = ih;
+      trace[2 * (num_iter - 1) + 1] = il;
+    }
+    ++num_iter;
+    if (num_iter > max_iter) {
+      stop = SVM_STOP_MAX_ITER;
+      break;
+    }
+  }
+  // Write the slice back; workgroup 0 publishes the final state (visible at kernel end).
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t i = lo + t + 256 * e;
+    if (i < hi_end) {
+      f[i] = fr[e];
+      alpha[i] = ar[e];
+    }
+  }
+  if (STAMP && g == 0 && t == 0)
+    for (int k = 0; k < 8; ++k) stamps[k] = sacc[k];
+  if (g == 0 && t == 0) {
+    st->num_iter = num_iter;
+    st->b_high = b_high;
+    st->b_low = b_low;
+    st->pending = 0;
+    st->stop = stop < 0 ? SVM_STOP_RUNNING : stop;
+  }
+}
+
+}  // namespace
+
+namespace {
+
+// Launch the persistent solver if the problem fits its register slices; returns false otherwise.
+template <int E>
+int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
+                        double* f, int64_t n, int64_t slice, unsigned long long* slots, SmoState* st, double C,
+                        double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(err) + 8;
+  const char* sv = getenv("SVM355_PSMO_STAMP");
+  if (sv && atoi(sv))
+    hipLaunchKernelGGL((smo_persistent_kernel<E, true>), dim3(G), dim3(256), 0, s, K, ldk, y, alpha, f, n, slice, slots,
+                       st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
+  else
+    hipLaunchKernelGGL((smo_persistent_kernel<E, false>), dim3(G), dim3(256), 0, s, K, ldk, y, alpha, f, n, slice,
+                       slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
+
+int persistent_grid(int64_t n, int* G_out, int* E_out) {
+  // Elements per thread E in {1,...,16}; workgroups G <= 64 (all co-resident; one sweep pass).
+  int target = 64;
+  if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
+  for (int E : {1, 2, 4, 8, 16}) {
+    const int64_t per_wg = int64_t(256) * E;
+    const int64_t G = (n + per_wg - 1) / per_wg;
+    if (G <= target) {
+      *G_out = int(std::max<int64_t>(1, G));
+      *E_out = E;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t* dtrace, int64_t tcap,
+               std::chrono::steady_clock::time_point t0) {
+  if (!fin.stop) {
+    set_error("svmd_smo: solver did not stop within its budget");
+    return SVM_ERR_INTERNAL;
+  }
+  if (tcap) {
+    const int64_t nt = std::min<int64_t>(fin.num_iter - 1, tcap);
+    if (nt > 0) SVMD_CHECK(hipMemcpy(trace, dtrace, size_t(nt) * 16, hipMemcpyDeviceToHost));
+  }
+  if (r) {
+    r->iterations = fin.num_iter;
+    r->b_high = fin.b_high;
+    r->b_low = fin.b_low;
+    r->b = (fin.b_high + fin.b_low) / 2;
+    r->stop_reason = fin.stop;
+    r->reserved = 0;
+    r->n_sv = -1;  // filled by the caller (needs alpha on the host or a device count)
+    r->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return SVM_OK;
+}
+
 }  // namespace
 
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
@@ -280,7 +706,9 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   const size_t off_idx = off_state + al(sizeof(SmoState));
   const size_t off_cnt = off_idx + al(size_t(n) * 8);
   const size_t off_trace = off_cnt + al(8);
-  const size_t total = off_trace + al(size_t(tcap) * 16);
+  const size_t off_slots = off_trace + al(size_t(tcap) * 16);
+  const size_t slot_bytes = size_t(2) * kMaxG * kRecStride * 8 + 256;  // records + error word + stamps
+  const size_t total = off_slots + al(slot_bytes);
   int rc = ctx->ensure_ws(total);
   if (rc) return rc;
   rc = ctx->ensure_pinned(sizeof(SmoState) * 3);
@@ -303,6 +731,45 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
     hipLaunchKernelGGL(warm_f_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, K, ldk, y, alpha,
                        idx, cnt, f, n);
     SVMD_LAUNCH_CHECK();
+  }
+
+  // ---- persistent single-launch solver (default when the slices fit in registers)
+  int G = 0, E = 0;
+  const char* mode = getenv("SVM355_SMO");
+  const bool want_persistent = !(mode && strcmp(mode, "graph") == 0);
+  if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E)) {
+    auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
+    auto* err = reinterpret_cast<unsigned*>(ws + off_slots + size_t(2) * kMaxG * kRecStride * 8);
+    SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));  // epochs restart at 1 every launch
+    const int64_t slice = int64_t(256) * E;
+    int lrc = SVM_ERR_INTERNAL;
+    switch (E) {
+      case 1: lrc = launch_persistent_e<1>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
+      case 2: lrc = launch_persistent_e<2>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
+      case 4: lrc = launch_persistent_e<4>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
+      case 8: lrc = launch_persistent_e<8>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
+      default: lrc = launch_persistent_e<16>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
+    }
+    if (lrc) return lrc;
+    SmoState* hst = static_cast<SmoState*>(ctx->pinned);
+    unsigned herr = 0;
+    SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipMemcpyAsync(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipStreamSynchronize(s));
+    if (herr) {
+      set_error("svmd_smo: persistent solver timed out waiting for a workgroup record (G=%d)", G);
+      return SVM_ERR_DEVICE;
+    }
+    if (const char* sv = getenv("SVM355_PSMO_STAMP"); sv && atoi(sv)) {
+      unsigned long long hs[8];
+      SVMD_CHECK(hipMemcpy(hs, reinterpret_cast<unsigned long long*>(err) + 8, sizeof(hs), hipMemcpyDeviceToHost));
+      const double cnt = double(kStampCount), mhz = hs[7] ? double(hs[0] + hs[1] + hs[2] + hs[3] + hs[4] + hs[5] + hs[6]) / (double(hs[7]) / 100.0) : 0.0;
+      fprintf(stderr, "[psmo stamps G=%d E=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
+              "globalred+barrier2 %.0f | loads %.0f | update %.0f | clock %.0f MHz | us/iter %.3f\n", G, E,
+              hs[0] / cnt, hs[1] / cnt, hs[2] / cnt, hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, hs[6] / cnt, mhz,
+              double(hs[7]) / 100.0 / cnt);
+    }
+    return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
   }
 
   // Graph of kChunk iterations, cached per context for identical arguments.
@@ -368,26 +835,7 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
     return SVM_ERR_DEVICE;
   }
   SVMD_CHECK(hipMemcpy(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost));
-  const SmoState fin = hst[2];
-  if (!fin.stop) {
-    set_error("svmd_smo: solver did not stop within the replay budget");
-    return SVM_ERR_INTERNAL;
-  }
-  if (tcap) {
-    const int64_t nt = std::min<int64_t>(fin.num_iter - 1, tcap);
-    if (nt > 0) SVMD_CHECK(hipMemcpy(trace, dtrace, size_t(nt) * 16, hipMemcpyDeviceToHost));
-  }
-  if (r) {
-    r->iterations = fin.num_iter;
-    r->b_high = fin.b_high;
-    r->b_low = fin.b_low;
-    r->b = (fin.b_high + fin.b_low) / 2;
-    r->stop_reason = fin.stop;
-    r->reserved = 0;
-    r->n_sv = -1;  // filled by the caller (needs alpha on the host or a device count)
-    r->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-  return SVM_OK;
+  return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
 }
 
 }  // namespace svm355

@@ -104,7 +104,18 @@ def test_gather_rows(dev, D):
     assert torch.equal(D.gather_rows(X, idx), X[idx])
 
 
-def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data):
+@pytest.fixture
+def smo_mode(request, monkeypatch):
+    mode, wg = request.param
+    monkeypatch.setenv("SVM355_SMO", mode)
+    if wg:
+        monkeypatch.setenv("SVM355_PSMO_WG", str(wg))
+    return request.param
+
+
+@pytest.mark.parametrize("smo_mode", [("persistent", None), ("persistent", 1), ("persistent", 3), ("graph", None)],
+                         indirect=True, ids=["persistent", "persistent-G1", "persistent-G2", "graph"])
+def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data, smo_mode):
     tr, _ = mn_data
     X = MinMaxScaler().fit_transform(tr.X[:900])
     y = tr.y[:900]
@@ -120,6 +131,26 @@ def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data):
     np.testing.assert_array_equal(t_gpu, t_cpu)
     np.testing.assert_array_equal(ad.cpu().numpy(), a_cpu)
     assert r_gpu.b == r_cpu.b
+
+
+def test_persistent_vs_graph_many_workgroups(dev, D, monkeypatch):
+    """Many workgroups (G = 40 at n = 20000): both device paths bit-identical."""
+    tr = synthetic_mnist(20000, seed=9)
+    Xd = D.upload_rows(tr.X, dev)
+    _, _, sqn = D.minmax_scale_(Xd, 784)
+    K = D.rbf_gram(Xd, sqn, Xd, sqn, 0.00125, symmetric=True)
+    yd = torch.from_numpy(tr.y).to(dev)
+    out = {}
+    for mode in ("persistent", "graph"):
+        monkeypatch.setenv("SVM355_SMO", mode)
+        monkeypatch.setenv("SVM355_PSMO_WG", "64")
+        a = torch.zeros(tr.n, dtype=torch.float64, device=dev)
+        r, trc = D.smo(K, yd, a, SVMParams(), n=tr.n, trace_cap=1000000)
+        out[mode] = (r, trc, a.cpu().numpy())
+    (r1, t1, a1), (r2, t2, a2) = out["persistent"], out["graph"]
+    assert r1.iterations == r2.iterations and r1.b == r2.b and r1.stop_reason == "converged"
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(a1, a2)
 
 
 def test_device_smo_warm_start_bit_identical(dev, D, mn_data):
