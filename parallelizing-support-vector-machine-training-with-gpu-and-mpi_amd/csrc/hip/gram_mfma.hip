@@ -32,7 +32,22 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <bool SYM>
+// Upper-triangle tile enumeration: id -> (tm, tn) with tn >= tm, row-major (row tm holds T - tm
+// tiles starting at offset(tm) = tm*T - tm*(tm-1)/2).
+__device__ __forceinline__ void tri_tile(int64_t id, int64_t T, int64_t& tm, int64_t& tn) {
+  const double b = double(2 * T + 1);
+  int64_t r = int64_t((b - sqrt(b * b - 8.0 * double(id))) * 0.5);
+  auto off = [T](int64_t x) { return x * T - x * (x - 1) / 2; };
+  while (r > 0 && off(r) > id) --r;
+  while (off(r + 1) <= id) ++r;
+  tm = r;
+  tn = r + (id - off(r));
+}
+
+// SYM: force K_ii = 1.  TRI: A == B, compute only tiles tn >= tm and also store each off-diagonal
+// tile transposed (staged through LDS so the mirror rows are written as coalesced 32-B runs) —
+// half the MFMA work of the full Gram.
+template <bool SYM, bool TRI>
 __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
     const double* __restrict__ A, const double* __restrict__ nA, int64_t m, int64_t lda,
     const double* __restrict__ B, const double* __restrict__ nB, int64_t n, int64_t ldb, int64_t kdim,
@@ -40,13 +55,19 @@ __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
   __shared__ __attribute__((aligned(16))) double As[BM * LS];
   __shared__ __attribute__((aligned(16))) double Bs[BN * LS];
 
-  const int64_t nwg = tiles_m * tiles_n;
-  const int64_t wg = xcd_remap(blockIdx.x, nwg);
-  const int64_t band = GROUP_M * tiles_n;
-  const int64_t first_m = (wg / band) * GROUP_M;
-  const int64_t gsz = std::min<int64_t>(tiles_m - first_m, GROUP_M);
-  const int64_t tm = first_m + (wg % band) % gsz;
-  const int64_t tn = (wg % band) / gsz;
+  int64_t tm, tn;
+  if (TRI) {
+    const int64_t nwg = tiles_m * (tiles_m + 1) / 2;
+    tri_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tm, tn);
+  } else {
+    const int64_t nwg = tiles_m * tiles_n;
+    const int64_t wg = xcd_remap(blockIdx.x, nwg);
+    const int64_t band = GROUP_M * tiles_n;
+    const int64_t first_m = (wg / band) * GROUP_M;
+    const int64_t gsz = std::min<int64_t>(tiles_m - first_m, GROUP_M);
+    tm = first_m + (wg % band) % gsz;
+    tn = (wg % band) / gsz;
+  }
   const int64_t bm = tm * BM, bn = tn * BN;
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
@@ -110,29 +131,61 @@ __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
   }
 
   // Epilogue: f64 16x16x4 C/D layout is col = lane & 15, row = (lane >> 4) + 4 * reg.
-  double nb[4];
+  double nb[4], na[4][4];
 #pragma unroll
   for (int nj = 0; nj < 4; ++nj) {
     const int64_t gj = bn + wc * 64 + nj * 16 + lr;
     nb[nj] = gj < n ? nB[gj] : 0.0;
   }
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
+  for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t gi = bm + wr * 64 + mi * 16 + lg + 4 * r;
-      if (gi >= m) continue;
-      const double na = nA[gi];
-      double* krow = K + gi * ldk;
+      na[mi][r] = gi < m ? nA[gi] : 0.0;
+    }
+  const bool mirror = TRI && tm != tn;
+  double* scr = As + w * (16 * 17);  // per-wave 16x16 transpose buffer (+1 pad)
+  if (mirror) __syncthreads();       // every wave is done reading the k-loop's LDS tiles
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        const int64_t gj = bn + wc * 64 + nj * 16 + lr;
-        if (gj >= n) continue;
-        double dist = na + nb[nj] - 2.0 * acc[mi][nj][r];
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int64_t gj = bn + wc * 64 + nj * 16 + lr;
+      double kv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gi = bm + wr * 64 + mi * 16 + lg + 4 * r;
+        double dist = na[mi][r] + nb[nj] - 2.0 * acc[mi][nj][r];
         dist = dist > 0.0 ? dist : 0.0;
-        double kv = exp(neg_gamma * dist);
-        if (SYM && gi == gj) kv = 1.0;
-        krow[gj] = kv;
+        kv[r] = exp(neg_gamma * dist);
+        if (SYM && gi == gj) kv[r] = 1.0;
+        if (gi < m && gj < n) K[gi * ldk + gj] = kv[r];
+      }
+      if (mirror) {
+        // Transpose the 16x16 sub-tile through LDS: scr[c][r] = tile[r][c].
+#pragma unroll
+        for (int r = 0; r < 4; ++r) scr[lr * 17 + lg + 4 * r] = kv[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int row = lane >> 2, c0 = (lane & 3) * 4;
+        const int64_t grow = bn + wc * 64 + nj * 16 + row;      // mirrored row  (an original column)
+        const int64_t gcol = bm + wr * 64 + mi * 16 + c0;       // mirrored cols (original rows)
+        if (grow < n) {
+          double* dst = K + grow * ldk + gcol;
+          const double* s = scr + row * 17 + c0;
+          if (gcol + 3 < m) {
+            *reinterpret_cast<double2*>(dst) = double2{s[0], s[1]};
+            *reinterpret_cast<double2*>(dst + 2) = double2{s[2], s[3]};
+          } else {
+            for (int q = 0; q < 4; ++q)
+              if (gcol + q < m) dst[q] = s[q];
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
   }
@@ -172,11 +225,16 @@ int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m,
     set_error("rbf_gram: problem too large for one launch");
     return SVM_ERR_ARG;
   }
-  if (sym_diag)
-    hipLaunchKernelGGL(rbf_gram_kernel<true>, dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
+  const char* tv = getenv("SVM355_GRAM_TRI");
+  const bool tri = sym_diag && A == B && nA == nB && m == n && lda == ldb && !(tv && tv[0] == '0');
+  if (tri)
+    hipLaunchKernelGGL((rbf_gram_kernel<true, true>), dim3(unsigned(tiles_m * (tiles_m + 1) / 2)), dim3(256), 0, s,
+                       A, nA, m, lda, B, nB, n, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n);
+  else if (sym_diag)
+    hipLaunchKernelGGL((rbf_gram_kernel<true, false>), dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
                        n, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL(rbf_gram_kernel<false>, dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
+    hipLaunchKernelGGL((rbf_gram_kernel<false, false>), dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
                        n, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n);
   SVMD_LAUNCH_CHECK();
   return SVM_OK;
