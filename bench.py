@@ -46,6 +46,9 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend for N > 1 (gloo: CPU-staged exchanges, for rehearsals of the "
+                         "multi-rank path on fewer GPUs than ranks)")
     a = ap.parse_args(argv)
 
     import torch
@@ -58,8 +61,10 @@ def main(argv=None):
             print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run",
                   file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % max(1, ndev)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
 
     from svm355 import SVC, SVMParams
     from svm355.parallel.cascade import CascadeSVM, partition_bounds
@@ -69,7 +74,11 @@ def main(argv=None):
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    comm_dev = dev if a.backend == "nccl" else torch.device("cpu")
     params = SVMParams()
 
     if world == 1:
@@ -82,7 +91,10 @@ def main(argv=None):
     def barrier_sync():
         torch.cuda.synchronize(dev)
         if dist is not None:
-            dist.barrier(device_ids=[local_rank])
+            if a.backend == "nccl":
+                dist.barrier(device_ids=[dev_index])
+            else:
+                dist.barrier()
         torch.cuda.synchronize(dev)
 
     model = None
@@ -94,8 +106,8 @@ def main(argv=None):
         else:
             from svm355.parallel.transport import TorchDistTransport
 
-            t = TorchDistTransport(dev)
-            model = CascadeSVM(t, params, topology=a.topology, verbose=0)
+            t = TorchDistTransport(comm_dev)
+            model = CascadeSVM(t, params, topology=a.topology, verbose=0, device=dev)
             lo, hi = partition_bounds(a.n, world, rank)
             model.fit(tr.X, tr.y, np.arange(lo, hi), n_total=a.n)
 
@@ -108,7 +120,7 @@ def main(argv=None):
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 

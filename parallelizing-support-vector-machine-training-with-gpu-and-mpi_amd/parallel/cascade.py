@@ -50,7 +50,8 @@ class _CpuBackend:
         self.width = d
 
     def to_rows(self, X: np.ndarray, device) -> torch.Tensor:
-        return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float64))
+        # Always a private copy: rows are scaled in place and must not alias the caller's array.
+        return torch.from_numpy(np.array(X, dtype=np.float64, order="C", copy=True))
 
     def local_minmax(self, X: torch.Tensor):
         from ..utils.data import MinMaxScaler
@@ -210,10 +211,14 @@ class CascadeSVM:
     def __init__(self, transport: Transport, params: Optional[SVMParams] = None, topology: str = "star",
                  max_rounds: int = 50, backend: str = "auto", verbose: int = 1,
                  log: Optional[Callable[[str], None]] = None, checkpoint_dir: Optional[str] = None,
-                 resume: bool = False):
+                 resume: bool = False, device=None):
+        """``device`` is where rows live and solves run (default: the transport's device).  A
+        compute device different from the transport's (e.g. GPU compute with a gloo CPU group)
+        stages every exchanged buffer through the transport device."""
         if topology not in ("star", "tree"):
             raise ValueError("topology must be 'star' (modified two-layer) or 'tree' (classical)")
         self.t = transport
+        self.device = torch.device(device) if device is not None else transport.device
         self.params = params or SVMParams()
         self.topology = topology
         self.max_rounds = max_rounds
@@ -232,8 +237,24 @@ class CascadeSVM:
         if self.t.rank == 0 and self.verbose >= level:
             self._log(msg)
 
+    # ---- communication helpers (stage through the transport device when it differs)
+    def _c(self, x: torch.Tensor) -> torch.Tensor:
+        return x if x.device == self.t.device else x.to(self.t.device)
+
+    def _d(self, x: torch.Tensor) -> torch.Tensor:
+        return x if x.device == self.device else x.to(self.device)
+
+    def _bcast_set(self, S: Optional[SVSet], width: int) -> SVSet:
+        payload = self._c(S.pack()) if self.t.rank == 0 else None
+        return SVSet.unpack(self._d(self.t.broadcast_rows(payload, width + 3)), width)
+
+    def _allreduce(self, x: torch.Tensor, op: str) -> torch.Tensor:
+        y = self._c(x.clone())
+        self.t.allreduce_(y, op)
+        return self._d(y)
+
     def _make_backend(self, d: int):
-        dev = self.t.device
+        dev = self.device
         name = self.backend_name
         if name == "auto":
             name = "hip" if dev.type == "cuda" else "cpu"
@@ -281,7 +302,7 @@ class CascadeSVM:
         else:
             payload, rnd, b, gids = None, 0, 0.0, set()
         rnd = self.t.broadcast_int(rnd)
-        G = SVSet.unpack(self.t.broadcast_rows(payload, be.width + 3), be.width)
+        G = SVSet.unpack(self._d(self.t.broadcast_rows(payload, be.width + 3)), be.width)
         return rnd, b, G, gids
 
     # ------------------------------------------------------------------ fit
@@ -299,20 +320,20 @@ class CascadeSVM:
         self.log(f"[rank 0] Running {name} with {t.world} processes")
         if n_total:
             self.log(f"[rank 0] total samples = {n_total}, features = {d}")
-        part = SVSet(be.to_rows(X_part, t.device), np.ascontiguousarray(y_part, np.int32),
+        part = SVSet(be.to_rows(X_part, self.device), np.ascontiguousarray(y_part, np.int32),
                      np.zeros(X_part.shape[0]), np.ascontiguousarray(ids_part, np.int64))
         be.sync()
         t.barrier()
 
         t0 = time.perf_counter()  # M3 :526 — after data distribution, before scaling
         mn, mx = be.local_minmax(part.X)
-        t.allreduce_(mn, "min")
-        t.allreduce_(mx, "max")
+        mn = self._allreduce(mn, "min")
+        mx = self._allreduce(mx, "max")
         be.scale_(part.X, mn, mx)
 
         solves: list = []
-        res = CascadeResult(SVSet.empty(be.width, t.device), 0.0, 0, False, mn=mn, mx=mx)
-        G = SVSet.empty(be.width, t.device)  # global SV set (meaningful on rank 0; broadcast each round)
+        res = CascadeResult(SVSet.empty(be.width, self.device), 0.0, 0, False, mn=mn, mx=mx)
+        G = SVSet.empty(be.width, self.device)  # global SV set (meaningful on rank 0; broadcast each round)
         global_ids: set = set()
         b = 0.0
         start_round = 0
@@ -327,17 +348,17 @@ class CascadeSVM:
             shown = rnd if self.topology == "star" else rnd + 1
             self.log(f"=== Round {shown} ===")
             # Broadcast the global SV set (count + one packed buffer) from rank 0.
-            G = SVSet.unpack(t.broadcast_rows(G.pack() if t.rank == 0 else None, be.width + 3), be.width)
+            G = self._bcast_set(G, be.width)
             if self.topology == "star":
                 S = merge_unseen(be, G, part)
                 local, _ = self._solve(be, S, "local", shown, solves)
-                gathered = t.gather_rows(local.pack(), dst=0)
+                gathered = t.gather_rows(self._c(local.pack()), dst=0)
                 same = 0
                 if t.rank == 0:
                     merged = local
                     seen = set(local.ids.tolist())
                     for src in range(1, t.world):  # source order 1..P-1 (M2 :578)
-                        w = SVSet.unpack(gathered[src], be.width)
+                        w = SVSet.unpack(self._d(gathered[src]), be.width)
                         keep = [i for i, g in enumerate(w.ids.tolist()) if g not in seen]
                         seen.update(w.ids[keep].tolist())
                         merged = _concat(be, merged, _subset(be, w, np.asarray(keep, np.int64), zero_alpha=True))
@@ -364,9 +385,9 @@ class CascadeSVM:
                             b = b_local
                     if step < t.world:
                         if t.rank % (2 * step) == step:
-                            t.send_rows(cur.pack(), t.rank - step)
+                            t.send_rows(self._c(cur.pack()), t.rank - step)
                         elif t.rank % (2 * step) == 0:
-                            recv = SVSet.unpack(t.recv_rows(t.rank + step, be.width + 3), be.width)
+                            recv = SVSet.unpack(self._d(t.recv_rows(t.rank + step, be.width + 3)), be.width)
                     step *= 2
                 same = 0
                 if t.rank == 0:
@@ -390,7 +411,7 @@ class CascadeSVM:
         # Share the final model with every rank (the reference keeps it on rank 0 only).
         b_t = torch.tensor([b], dtype=torch.float64, device=t.device)
         t.broadcast_(b_t, 0)
-        G = SVSet.unpack(t.broadcast_rows(G.pack() if t.rank == 0 else None, be.width + 3), be.width)
+        G = self._bcast_set(G, be.width)
         be.sync()
         t1 = time.perf_counter()
         res.sv, res.b, res.rounds, res.converged = G, float(b_t.item()), rnd, converged
@@ -404,7 +425,7 @@ class CascadeSVM:
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
         r, be = self.result, self._be
-        Xq = be.to_rows(np.ascontiguousarray(X, dtype=np.float64), self.t.device)
+        Xq = be.to_rows(np.ascontiguousarray(X, dtype=np.float64), self.device)
         be.scale_(Xq, r.mn, r.mx)
         if len(r.sv) == 0:
             return np.full(X.shape[0], -r.b)

@@ -80,6 +80,14 @@ def test_cascade_threads_converge_to_single_solve(data, topology, world):
     assert acc0 > 0.95
 
 
+def test_fit_and_score_do_not_mutate_inputs(data):
+    tr, te = data
+    X0, T0 = tr.X.copy(), te.X.copy()
+    _run(2, "star", tr, te)
+    np.testing.assert_array_equal(tr.X, X0)
+    np.testing.assert_array_equal(te.X, T0)
+
+
 def test_tree_rejects_non_power_of_two(data):
     tr, te = data
     with pytest.raises(ValueError, match="power-of-2"):
