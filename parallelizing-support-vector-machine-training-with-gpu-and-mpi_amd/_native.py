@@ -116,6 +116,11 @@ _HIP_SIGS = {
                            POINTER(SvmResult), _P, c_int64]),
     "svmd_train": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32,
                              POINTER(SvmParams), POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming)]),
+    "svmd_train_q": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32,
+                               POINTER(SvmParams), POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming),
+                               _P, _P, c_int64, c_int32, POINTER(c_int32)]),
+    "svmd_rbf_gram_q": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int64, c_double, _P,
+                                  c_int64, c_int32, POINTER(c_int32)]),
     "svmd_decision": (c_int32, [c_void_p, _P, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
                                 c_double, c_double, _P]),
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),

@@ -9,6 +9,7 @@
 //   --C --gamma --tau --eps --sv-tol --max-iter --positive-label --threads
 //   --model-dir D    write final_sv_{ids,labels,alphas}.txt and final_b.txt
 //   --json F         machine-readable summary
+//   --gram auto|fp64|int  (svm_gpu) RBF Gram path: exact-integer int8 MFMA for pixel data, or FP64 MFMA
 #pragma once
 #include <chrono>
 #include <cstdio>
@@ -31,13 +32,15 @@ struct Options {
   int positive_label = 1;
   svm_params p{};
   bool quiet = false;
+  int gram_mode = 0;  // svm_gpu: 0 auto (exact-integer int8 MFMA Gram for pixel data), 1 fp64, 2 int
 };
 
 inline void usage(const char* prog) {
   fprintf(stderr,
           "usage: %s [--dataset P | --train F --test F | --synthetic N[,M] [--seed S]] [--n-limit N]\n"
           "          [--C 10] [--gamma 0.00125] [--tau 1e-5] [--eps 1e-12] [--sv-tol 1e-8]\n"
-          "          [--max-iter 100000] [--positive-label 1] [--threads T] [--model-dir D] [--json F]\n",
+          "          [--max-iter 100000] [--positive-label 1] [--threads T] [--model-dir D] [--json F]\n"
+          "          [--gram auto|fp64|int]\n",
           prog);
 }
 
@@ -75,6 +78,10 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
     else if (a == "--model-dir") o.model_dir = next("--model-dir");
     else if (a == "--json") o.json = next("--json");
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--gram") {
+      const std::string g = next("--gram");
+      o.gram_mode = g == "fp64" ? 1 : g == "int" ? 2 : 0;
+    }
     else if (a == "-h" || a == "--help") {
       usage(argv[0]);
       exit(0);

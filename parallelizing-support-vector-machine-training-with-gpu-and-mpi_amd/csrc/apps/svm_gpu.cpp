@@ -79,7 +79,12 @@ int main(int argc, char** argv) {
   CK(svmd_preprocess(dev.ctx, Xd, n, d, ld, mn, mx, sqn, 0));
   svm_result r{};
   svmd_timing tm{};
-  CK(svmd_train(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm));
+  std::vector<double> mnh(static_cast<size_t>(d)), mxh(static_cast<size_t>(d));
+  CK(svmd_memcpy_d2h(dev.ctx, mnh.data(), mn, d * 8));
+  CK(svmd_memcpy_d2h(dev.ctx, mxh.data(), mx, d * 8));
+  int32_t int_gram = 0;
+  CK(svmd_train_q(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm, mnh.data(), mxh.data(), d,
+                  o.gram_mode, &int_gram));
   CK(svmd_synchronize(dev.ctx));
   const auto t1 = std::chrono::steady_clock::now();
   if (r.stop_reason != SVM_STOP_CONVERGED) fprintf(stderr, "%s\n", svm_stop_message(r.stop_reason));
@@ -134,8 +139,8 @@ int main(int argc, char** argv) {
   printf("The prediction time: %.3f milliseconds\n", pred_ms);
   printf("The elapsed time: %.3f milliseconds\n", train_ms + pred_ms);
   if (!o.quiet)
-    fprintf(stderr, "[svm_gpu] gram %.3f ms, smo %.3f ms, iterations %lld\n", tm.gram_ms, tm.smo_ms,
-            (long long)r.iterations);
+    fprintf(stderr, "[svm_gpu] gram %.3f ms (%s), smo %.3f ms, iterations %lld\n", tm.gram_ms,
+            int_gram ? "int8-exact" : "fp64", tm.smo_ms, (long long)r.iterations);
   if (!o.model_dir.empty()) {
     std::vector<int32_t> lab(static_cast<size_t>(nsv));
     std::vector<double> as(static_cast<size_t>(nsv));
@@ -147,7 +152,8 @@ int main(int argc, char** argv) {
       fprintf(stderr, "%s\n", svm_last_error());
   }
   char extra[256];
-  snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f", tm.gram_ms, tm.smo_ms);
+  snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f, \"gram_path\": \"%s\"", tm.gram_ms,
+           tm.smo_ms, int_gram ? "int8-exact" : "fp64");
   cli::write_json(o.json, "svm_gpu", o, n, d, r, correct, m, train_ms, pred_ms, train_ms + pred_ms, extra);
   return 0;
 }

@@ -1,5 +1,6 @@
 // C ABI of the device library: context management and the end-to-end device training path.
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -218,11 +219,45 @@ SVM_API int svmd_smo(void* h, const double* K_d, int64_t ldk, const int32_t* y_d
   return ctx->end();
 }
 
-SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
-                       const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p,
-                       svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing) {
-  SVMD_CTX(h);
-  const svm_params q = resolve(p);
+// Gram selection: mode 0 = auto (exact-integer path when the scaled rows are integer multiples of
+// 1/r_j, else FP64), 1 = FP64 only, 2 = integer path required.  SVM355_GRAM=fp64|int overrides
+// the auto mode.  mn/mx (host, d values) are the min-max statistics the rows were scaled with.
+static int gram_any(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
+                    const double* mn_h, const double* mx_h, int64_t d, int32_t mode, double gamma, double* K,
+                    int64_t ldk, int32_t* used_out) {
+  if (mode == 0) {
+    if (const char* g = getenv("SVM355_GRAM")) {
+      if (!strcmp(g, "fp64")) mode = 1;
+      if (!strcmp(g, "int")) mode = 2;
+    }
+  }
+  bool used = false;
+  if (mode != 1 && mn_h && mx_h) {
+    QuantPlan P;
+    if (plan_quant(mn_h, mx_h, d, &P)) {
+      int rc = ctx->ensure_ws(igram_workspace(n, P));
+      if (rc) return rc;
+      rc = run_igram(ctx->stream, X_d, n, ld, P, gamma, K, ldk, ctx->ws, &used);
+      if (rc) return rc;
+    }
+  }
+  if (!used && mode == 2) {
+    set_error("integer Gram path requested but the rows are not integer-valued in [0, 255] after scaling");
+    return SVM_ERR_ARG;
+  }
+  if (used_out) *used_out = used ? 1 : 0;
+  if (used) return SVM_OK;
+  if (!sqn_d) {
+    set_error("FP64 Gram path needs the squared row norms");
+    return SVM_ERR_ARG;
+  }
+  return launch_rbf_gram(ctx->stream, X_d, sqn_d, n, ld, X_d, sqn_d, n, ld, kdim, gamma, K, ldk, true);
+}
+
+static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
+                      const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params& q, svm_result* r,
+                      double* K_d, int64_t ldk, svmd_timing* timing, const double* mn_h, const double* mx_h,
+                      int64_t d, int32_t gram_mode, int32_t* gram_used) {
   const auto t0 = std::chrono::steady_clock::now();
   int rc = ctx->begin();
   if (rc) return rc;
@@ -238,7 +273,7 @@ SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t 
     }
     owned = true;
   }
-  rc = launch_rbf_gram(ctx->stream, X_d, sqn_d, n, ld, X_d, sqn_d, n, ld, kdim, q.gamma, K, ldk, true);
+  rc = gram_any(ctx, X_d, sqn_d, n, ld, kdim, mn_h, mx_h, d, gram_mode, q.gamma, K, ldk, gram_used);
   if (!rc && timing) {
     const hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
@@ -268,6 +303,34 @@ SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t 
     timing->total_ms = ms_since(t0);
     timing->smo_ms = timing->total_ms - t_gram;
   }
+  return ctx->end();
+}
+
+SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
+                       const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p,
+                       svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing) {
+  SVMD_CTX(h);
+  return train_impl(ctx, X_d, sqn_d, n, ld, kdim, y_d, alpha_d, warm, resolve(p), r, K_d, ldk, timing, nullptr,
+                    nullptr, 0, 1, nullptr);
+}
+
+SVM_API int svmd_train_q(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
+                         const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
+                         double* K_d, int64_t ldk, svmd_timing* timing, const double* mn_h, const double* mx_h,
+                         int64_t d, int32_t gram_mode, int32_t* gram_used) {
+  SVMD_CTX(h);
+  return train_impl(ctx, X_d, sqn_d, n, ld, kdim, y_d, alpha_d, warm, resolve(p), r, K_d, ldk, timing, mn_h, mx_h,
+                    d, gram_mode, gram_used);
+}
+
+SVM_API int svmd_rbf_gram_q(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
+                            int64_t kdim, const double* mn_h, const double* mx_h, int64_t d, double gamma,
+                            double* K_d, int64_t ldk, int32_t gram_mode, int32_t* gram_used) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = gram_any(ctx, X_d, sqn_d, n, ld, kdim, mn_h, mx_h, d, gram_mode, gamma, K_d, ldk, gram_used);
+  if (rc) return rc;
   return ctx->end();
 }
 

@@ -93,6 +93,21 @@ int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m,
                     double gamma, double* K, int64_t ldk, bool sym_diag);
 int launch_gemv_rows(hipStream_t s, const double* K, int64_t ldk, int64_t m, int64_t n,
                      const double* coef, double b, double* out);
+// Exact-integer Gram path (igram.hip).
+struct QuantPlan {
+  bool ok = false;
+  double w0 = 0.0;          // base weight 1/r^2 shared by the int8 part
+  int kc = 0, kq = 0;       // correction columns (multiple of 16), total int8 columns (multiple of 64)
+  int n_corr = 0;           // real correction columns
+  std::vector<int32_t> perm;  // permuted column order (-1 = zero pad)
+  std::vector<double> rmul;   // r_j per permuted column (scaled value * r_j = integer)
+  std::vector<double> delta;  // w_j - w0 per correction column
+  std::vector<double> cen;    // centre floor(r_j / 2) of each correction column's integer range
+};
+bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P);
+size_t igram_workspace(int64_t n, const QuantPlan& P);
+int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const QuantPlan& P, double gamma, double* K,
+              int64_t ldk, void* ws, bool* used);
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
 

@@ -16,6 +16,7 @@
 // Workgroup ids are remapped so that consecutive tiles of a GROUP_M x tiles_n band land on one XCD
 // (shared L2 for the A row-panel), per the CDNA4 XCD round-robin dispatch.
 #include "ctx.h"
+#include "tile_map.h"
 
 namespace svm355 {
 namespace {
@@ -25,24 +26,6 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int LS = 18;  // padded LDS row stride (doubles)
 constexpr int GROUP_M = 8;
-
-__device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
-  // Bijective: blocks that share an XCD (orig % 8) get a contiguous range of logical ids.
-  const int64_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
-// Upper-triangle tile enumeration: id -> (tm, tn) with tn >= tm, row-major (row tm holds T - tm
-// tiles starting at offset(tm) = tm*T - tm*(tm-1)/2).
-__device__ __forceinline__ void tri_tile(int64_t id, int64_t T, int64_t& tm, int64_t& tn) {
-  const double b = double(2 * T + 1);
-  int64_t r = int64_t((b - sqrt(b * b - 8.0 * double(id))) * 0.5);
-  auto off = [T](int64_t x) { return x * T - x * (x - 1) / 2; };
-  while (r > 0 && off(r) > id) --r;
-  while (off(r + 1) <= id) ++r;
-  tm = r;
-  tn = r + (id - off(r));
-}
 
 // SYM: force K_ii = 1.  TRI: A == B, compute only tiles tn >= tm and also store each off-diagonal
 // tile transposed (staged through LDS so the mirror rows are written as coalesced 32-B runs) —

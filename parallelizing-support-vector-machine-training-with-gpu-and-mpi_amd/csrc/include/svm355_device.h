@@ -74,6 +74,22 @@ SVM_API int svmd_train(void* ctx, const double* X_d, const double* sqn_d, int64_
                        const svm_params* p, svm_result* r, double* K_d, int64_t ldk,
                        svmd_timing* timing);
 
+// As svmd_train, with the Gram path selectable: gram_mode 0 = auto (exact-integer int8-MFMA Gram when
+// the scaled rows are integer multiples of 1/(mx_j - mn_j) in [0, 255] — MNIST pixels — else FP64),
+// 1 = FP64 only, 2 = integer path required.  mn_h/mx_h: host min/max (d values) the rows were
+// scaled with (NULL -> FP64).  *gram_used (optional) = 1 if the integer path ran.
+SVM_API int svmd_train_q(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
+                         int64_t kdim, const int32_t* y_d, double* alpha_d, int32_t warm,
+                         const svm_params* p, svm_result* r, double* K_d, int64_t ldk,
+                         svmd_timing* timing, const double* mn_h, const double* mx_h, int64_t d,
+                         int32_t gram_mode, int32_t* gram_used);
+
+// Symmetric RBF Gram of n preprocessed rows with the same path selection as svmd_train_q.
+SVM_API int svmd_rbf_gram_q(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
+                            int64_t kdim, const double* mn_h, const double* mx_h, int64_t d,
+                            double gamma, double* K_d, int64_t ldk, int32_t gram_mode,
+                            int32_t* gram_used);
+
 // out_d[i] = sum_k coef_d[k] * K(Xq_i, Xs_k) - b, coef = alpha*y of the SVs.
 SVM_API int svmd_decision(void* ctx, const double* Xs_d, const double* ns_d, const double* coef_d,
                           int64_t nsv, int64_t lds, const double* Xq_d, const double* nq_d, int64_t m,

@@ -36,12 +36,13 @@ def _resolve_device(device: str) -> str:
 class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 scale: bool = True, zero_is_positive: bool = False):
+                 scale: bool = True, zero_is_positive: bool = False, gram: str = "auto"):
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else (os.cpu_count() or 1))
         self.device = device
         self.scale = scale
         self.zero_is_positive = zero_is_positive
+        self.gram = gram  # "auto" | "fp64" | "int" (device backend Gram path, see ops.device.train)
         self._dev = None  # device-side model state (torch tensors)
 
     # ------------------------------------------------------------------ fit
@@ -107,7 +108,7 @@ class SVC:
             alpha = torch.zeros(X.shape[0], dtype=torch.float64, device=device)
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
-        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None)
+        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram)
         a = alpha.cpu().numpy()
         self._finish(a, y, res)
         idx = torch.from_numpy(self.support_).to(device)

@@ -184,9 +184,26 @@ def smo(K: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams
     return res, trace
 
 
+GRAM_MODES = {"auto": 0, "fp64": 1, "int": 2}
+
+
+def _host_stats(mn, mx):
+    if mn is None or mx is None:
+        return None, None, 0
+    a = np.ascontiguousarray(mn.detach().cpu().numpy() if isinstance(mn, torch.Tensor) else mn, dtype=np.float64)
+    b = np.ascontiguousarray(mx.detach().cpu().numpy() if isinstance(mx, torch.Tensor) else mx, dtype=np.float64)
+    return a, b, int(a.shape[0])
+
+
 def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams,
-          warm: bool = False, K: Optional[torch.Tensor] = None) -> Tuple[SMOResult, dict]:
-    """RBF Gram (into K, allocated by torch if None) + SMO.  Returns (result, timing dict in ms)."""
+          warm: bool = False, K: Optional[torch.Tensor] = None, mn=None, mx=None,
+          gram: str = "auto") -> Tuple[SMOResult, dict]:
+    """RBF Gram (into K, allocated by torch if None) + SMO.  Returns (result, timing dict in ms).
+
+    ``mn``/``mx`` are the min/max the rows were scaled with; with them the exact-integer Gram
+    (int8 MFMA + FP64 correction, igram.hip) runs when the rows are integer-valued pixels
+    (``gram="auto"``), ``gram="fp64"`` forces the FP64 MFMA Gram, ``gram="int"`` requires the
+    integer path."""
     _check_rows(X)
     n = X.shape[0]
     if K is None:
@@ -195,10 +212,31 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
     r = N.SvmResult()
     tm = N.SvmdTiming()
     p = params.to_struct()
-    N.check(ctx.lib.svmd_train(ctx.bind(), N.ptr(X), N.ptr(sqn), n, X.shape[1], X.shape[1], N.ptr(y),
-                               N.ptr(alpha), int(warm), ctypes.byref(p), ctypes.byref(r), N.ptr(K), K.stride(0),
-                               ctypes.byref(tm)), "svmd_train")
-    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms}
+    a, b, d = _host_stats(mn, mx)
+    used = ctypes.c_int32(0)
+    N.check(ctx.lib.svmd_train_q(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
+                                 X.shape[1], N.ptr(y), N.ptr(alpha), int(warm), ctypes.byref(p), ctypes.byref(r),
+                                 N.ptr(K), K.stride(0), ctypes.byref(tm), N.ptr(a), N.ptr(b), d,
+                                 GRAM_MODES[gram], ctypes.byref(used)), "svmd_train_q")
+    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
+                                      "gram_path": "int8-exact" if used.value else "fp64"}
+
+
+def rbf_gram_sym(X: torch.Tensor, sqn: Optional[torch.Tensor], gamma: float, mn=None, mx=None,
+                 gram: str = "auto", out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, str]:
+    """Symmetric RBF Gram of preprocessed rows with the svmd_train_q path selection.
+    Returns (K, path) with path "int8-exact" or "fp64"."""
+    _check_rows(X)
+    n = X.shape[0]
+    if out is None:
+        out = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+    ctx = _ctx_for(X)
+    a, b, d = _host_stats(mn, mx)
+    used = ctypes.c_int32(0)
+    N.check(ctx.lib.svmd_rbf_gram_q(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
+                                    X.shape[1], N.ptr(a), N.ptr(b), d, float(gamma), N.ptr(out), out.stride(0),
+                                    GRAM_MODES[gram], ctypes.byref(used)), "svmd_rbf_gram_q")
+    return out, ("int8-exact" if used.value else "fp64")
 
 
 def decision(Xs: torch.Tensor, ns: torch.Tensor, coef: torch.Tensor, Xq: torch.Tensor, nq: torch.Tensor,

@@ -272,3 +272,74 @@ def test_cascade_rccl_single_rank_group(dev, mn_data):
             assert c.score(te.X, te.y) > 0.95
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- exact-integer Gram (igram.hip)
+def _exact_rbf(P: np.ndarray, mn: np.ndarray, mx: np.ndarray, gamma: float) -> np.ndarray:
+    """K from the integer pixels: dist = sum_j (q_aj - q_bj)^2 / r_j^2 with exact integer differences."""
+    r = mx - mn
+    r = np.where(r < 1e-12, 1.0, r)
+    Q = P - mn  # exact integers
+    w = 1.0 / (r * r)
+    d2 = np.zeros((P.shape[0], P.shape[0]))
+    for j in range(P.shape[1]):  # per-column exact squared differences, weighted in fp64
+        dq = Q[:, j][:, None] - Q[:, j][None, :]
+        d2 += w[j] * dq * dq
+    return np.exp(-gamma * d2)
+
+
+def _int_data(n, d, seed, ranges):
+    rng = np.random.default_rng(seed)
+    hi = rng.choice(ranges, size=d)
+    P = np.floor(rng.random((n, d)) * (hi + 1)).astype(np.float64)
+    P[0] = 0.0
+    P[1] = hi  # every column attains [0, hi]
+    return P
+
+
+@pytest.mark.parametrize("n,d,ranges,seed", [
+    (700, 784, [255], 1),                  # no correction columns (kc = 0)
+    (1031, 784, [255] * 9 + [254, 200], 2),  # ~18% correction columns
+    (300, 100, [255] * 6 + [17, 3, 1], 3),  # several distinct ranges, small d
+    (129, 40, [100], 4),                   # base range != 255
+])
+def test_int_gram_matches_exact(dev, D, n, d, ranges, seed):
+    P = _int_data(n, d, seed, ranges)
+    P[:, 3] = 7.0  # constant column
+    Xd = D.upload_rows(P, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, d)
+    gamma = 0.00125 * 784 / d
+    K, path = D.rbf_gram_sym(Xd, sqn, gamma, mn=mn, mx=mx, gram="int")
+    assert path == "int8-exact"
+    Kh = K[:, :n].cpu().numpy()
+    ref = _exact_rbf(P, P.min(0), P.max(0), gamma)
+    assert np.abs(Kh - ref).max() <= 2e-15
+    np.testing.assert_array_equal(np.diag(Kh), 1.0)
+    np.testing.assert_array_equal(Kh, Kh.T)  # mirror stores
+    Kf, pf = D.rbf_gram_sym(Xd, sqn, gamma, mn=mn, mx=mx, gram="fp64")
+    assert pf == "fp64"
+    assert np.abs(Kf[:, :n].cpu().numpy() - ref).max() <= 1e-13
+
+
+def test_int_gram_falls_back_on_real_valued_data(dev, D):
+    rng = np.random.default_rng(9)
+    X = rng.random((300, 50)) * 3.0
+    Xd = D.upload_rows(X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 50)
+    K, path = D.rbf_gram_sym(Xd, sqn, 0.1, mn=mn, mx=mx, gram="auto")
+    assert path == "fp64"
+    with pytest.raises(Exception):
+        D.rbf_gram_sym(Xd, sqn, 0.1, mn=mn, mx=mx, gram="int")
+
+
+def test_svc_int_gram_matches_fp64_gram(dev, mn_data):
+    tr, te = mn_data
+    a = SVC(device="cuda:0", gram="int").fit(tr.X, tr.y)
+    b = SVC(device="cuda:0", gram="fp64").fit(tr.X, tr.y)
+    c = SVC(device="cpu").fit(tr.X, tr.y)
+    assert a.timings_["gram_path"] == "int8-exact" and b.timings_["gram_path"] == "fp64"
+    assert a.stop_reason_ == "converged"
+    assert set(a.support_.tolist()) == set(c.support_.tolist())
+    assert abs(a.b_ - c.b_) <= 1e-7 * max(1.0, abs(c.b_))
+    assert abs(a.b_ - b.b_) <= 1e-7 * max(1.0, abs(c.b_))
+    np.testing.assert_array_equal(a.predict(te.X), c.predict(te.X))
