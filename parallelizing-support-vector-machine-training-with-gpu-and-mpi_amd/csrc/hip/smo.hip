@@ -292,57 +292,81 @@ __device__ __forceinline__ double mk64(uint32_t lo, uint32_t hi) {
   return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
 }
 
-// ---- wave64 arg-reductions on (double value, uint32 index) without LDS traffic.
-// Steps: DPP quad_perm xor1, xor2, row_half_mirror (8), row_mirror (16), then the gfx950
-// v_permlane16_swap / v_permlane32_swap for the 32- and 64-lane halves.  After each step every
-// lane holds the best of its group (lexicographic (value, index): the serial lowest-index rule),
-// so the result is schedule-independent and identical in every lane.
+// ---- wave64 arg-reductions on (double value, uint32 index) without LDS traffic, in two cheap
+// stages: (1) the wave-wide min (max) VALUE with one v_min_f64 (v_max_f64) per step, (2) the
+// smallest index among the lanes holding that value with one v_min_u32 per step.  The result is
+// the lexicographic (value, lowest index) winner — the serial tie rule — identical in every lane
+// and independent of the schedule.  Steps: DPP quad_perm xor1, xor2, row_half_mirror (8),
+// row_mirror (16), then the gfx950 v_permlane16_swap / v_permlane32_swap for the 32/64-lane halves.
 struct VI {
   double v;
   uint32_t i;
 };
 
-template <bool MIN>
-__device__ __forceinline__ bool better(VI a, VI b) {  // does b replace a?
-  return MIN ? (b.v < a.v || (b.v == a.v && b.i < a.i)) : (b.v > a.v || (b.v == a.v && b.i < a.i));
-}
-template <bool MIN>
-__device__ __forceinline__ VI pick(VI a, VI b) {
-  return better<MIN>(a, b) ? b : a;
-}
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
   return uint32_t(__builtin_amdgcn_mov_dpp(int(x), CTRL, 0xF, 0xF, false));
 }
-template <bool MIN, int CTRL>
-__device__ __forceinline__ VI step_dpp(VI a) {
-  const VI b{mk64(dpp32<CTRL>(lo32(a.v)), dpp32<CTRL>(hi32(a.v))), dpp32<CTRL>(a.i)};
-  return pick<MIN>(a, b);
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+  return mk64(dpp32<CTRL>(lo32(x)), dpp32<CTRL>(hi32(x)));
 }
+template <bool MIN>
+__device__ __forceinline__ double vbest(double a, double b) {
+  return MIN ? fmin(a, b) : fmax(a, b);
+}
+// v_permlane{16,32}_swap with both operands = x returns, in every lane, its own value and its
+// partner's (in an order that depends on the row): combine both.
 template <bool MIN, bool S32>
-__device__ __forceinline__ VI step_swap(VI a) {
-  const uint32_t l = lo32(a.v), h = hi32(a.v);
+__device__ __forceinline__ double swap_best64(double x) {
+  const uint32_t l = lo32(x), h = hi32(x);
   if constexpr (S32) {
     const auto L = __builtin_amdgcn_permlane32_swap(l, l, false, false);
     const auto H = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-    const auto I = __builtin_amdgcn_permlane32_swap(a.i, a.i, false, false);
-    return pick<MIN>(VI{mk64(L[0], H[0]), I[0]}, VI{mk64(L[1], H[1]), I[1]});
+    return vbest<MIN>(mk64(L[0], H[0]), mk64(L[1], H[1]));
   } else {
     const auto L = __builtin_amdgcn_permlane16_swap(l, l, false, false);
     const auto H = __builtin_amdgcn_permlane16_swap(h, h, false, false);
-    const auto I = __builtin_amdgcn_permlane16_swap(a.i, a.i, false, false);
-    return pick<MIN>(VI{mk64(L[0], H[0]), I[0]}, VI{mk64(L[1], H[1]), I[1]});
+    return vbest<MIN>(mk64(L[0], H[0]), mk64(L[1], H[1]));
   }
 }
-template <bool MIN>
+template <bool S32>
+__device__ __forceinline__ uint32_t swap_min32(uint32_t x) {
+  if constexpr (S32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return min(r[0], r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return min(r[0], r[1]);
+  }
+}
+// L = number of leading lanes that may hold candidates (1..64, power of two): reductions over the
+// NW per-wave results of one workgroup need only log2(NW) steps.
+template <bool MIN, int L = 64>
 __device__ __forceinline__ VI wave_arg(VI a) {  // requires a full wave (EXEC = all 64 lanes)
-  a = step_dpp<MIN, 0xB1>(a);   // quad_perm [1,0,3,2]
-  a = step_dpp<MIN, 0x4E>(a);   // quad_perm [2,3,0,1]
-  a = step_dpp<MIN, 0x141>(a);  // row_half_mirror
-  a = step_dpp<MIN, 0x140>(a);  // row_mirror
-  a = step_swap<MIN, false>(a);
-  a = step_swap<MIN, true>(a);
-  return a;
+  double m = a.v;
+  if (L > 1) m = vbest<MIN>(m, dpp64<0xB1>(m));   // quad_perm [1,0,3,2]
+  if (L > 2) m = vbest<MIN>(m, dpp64<0x4E>(m));   // quad_perm [2,3,0,1]
+  if (L > 4) m = vbest<MIN>(m, dpp64<0x141>(m));  // row_half_mirror
+  if (L > 8) m = vbest<MIN>(m, dpp64<0x140>(m));  // row_mirror
+  if (L > 16) m = swap_best64<MIN, false>(m);
+  if (L > 32) m = swap_best64<MIN, true>(m);
+  uint32_t i = a.v == m ? a.i : 0xFFFFFFFFu;
+  if (L > 1) i = min(i, dpp32<0xB1>(i));
+  if (L > 2) i = min(i, dpp32<0x4E>(i));
+  if (L > 4) i = min(i, dpp32<0x141>(i));
+  if (L > 8) i = min(i, dpp32<0x140>(i));
+  if (L > 16) i = swap_min32<false>(i);
+  if (L > 32) i = swap_min32<true>(i);
+  return VI{m, i};
+}
+template <bool MIN>
+__device__ __forceinline__ bool better(VI a, VI b) {  // does b replace a?
+  return MIN ? (b.v < a.v || (b.v == a.v && b.i < a.i)) : (b.v > a.v || (b.v == a.v && b.i < a.i));
+}
+__device__ __forceinline__ double first_lane(double x) {
+  return mk64(uint32_t(__builtin_amdgcn_readfirstlane(int(lo32(x)))),
+              uint32_t(__builtin_amdgcn_readfirstlane(int(hi32(x)))));
 }
 // Value held by the lane whose index is the (uniform) winner index; 0 if it is the sentinel.
 __device__ __forceinline__ double winner_alpha(uint32_t my_i, double my_a, uint32_t win) {
@@ -354,9 +378,9 @@ __device__ __forceinline__ double winner_alpha(uint32_t my_i, double my_a, uint3
 }
 
 struct PersistShared {
-  double wv[2][4], wa[2][4];  // per-wave candidates [min|max][wave]
-  uint32_t wi[2][4];
-  double gv[2], ga[2];        // global winners of the current epoch
+  double wv[2][16], wa[2][16];  // per-wave candidates [min|max][wave]
+  uint32_t wi[2][16];
+  double gv[2], ga[2];          // global winners of the current epoch
   uint32_t gi[2];
   int timeout;
 };
@@ -377,12 +401,15 @@ constexpr uint32_t kStampFrom = 200, kStampCount = 2000;
     }                                                                               \
   } while (0)
 
-template <int E, bool STAMP>
-__global__ __launch_bounds__(256) void smo_persistent_kernel(
+// NT threads per workgroup (NW = NT/64 waves), E register-resident elements per thread:
+// element e of thread t is training point lo + t + NT*e of the workgroup's slice.
+template <int NT, int E, bool STAMP>
+__global__ __launch_bounds__(NT) void smo_persistent_kernel(
     const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
     double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
     SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
     int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps) {
+  constexpr int NW = NT / 64;
   __shared__ PersistShared sh;
   unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = 0, rt0 = 0;
   bool stamping = false;
@@ -395,7 +422,7 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
   int32_t yr[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const int64_t i = lo + t + 256 * e;
+    const int64_t i = lo + t + NT * e;
     const bool ok = i < hi_end;
     fr[e] = ok ? f[i] : 0.0;
     ar[e] = ok ? alpha[i] : 0.0;
@@ -419,7 +446,7 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
     double amn = 0.0, amx = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const uint32_t i = uint32_t(lo + t + 256 * e);
+      const uint32_t i = uint32_t(lo + t + NT * e);
       const double a = ar[e], fi = fr[e];
       const int32_t yi = yr[e];
       const bool in_high = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
@@ -450,20 +477,33 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
     PSTAMP(1);
     unsigned long long* rec = slots + (size_t(epoch & 1) * kMaxG) * kRecStride;
     if (w == 0) {
-      // ---- 2. merge the 4 waves and publish this workgroup's record (lanes 0..9, one granule each)
-      VI a{sh.wv[0][0], sh.wi[0][0]}, b{sh.wv[1][0], sh.wi[1][0]};
-      double aa = sh.wa[0][0], ba = sh.wa[1][0];
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        const VI ca{sh.wv[0][k], sh.wi[0][k]}, cb{sh.wv[1][k], sh.wi[1][k]};
-        if (better<true>(a, ca)) {
-          a = ca;
-          aa = sh.wa[0][k];
+      // ---- 2. merge the NW waves and publish this workgroup's record (lanes 0..9, one granule each)
+      VI a{inf, kSentinel}, b{-inf, kSentinel};
+      double aa = 0.0, ba = 0.0;
+      if (NW == 1) {
+        a = VI{sh.wv[0][0], sh.wi[0][0]};
+        b = VI{sh.wv[1][0], sh.wi[1][0]};
+        aa = sh.wa[0][0];
+        ba = sh.wa[1][0];
+      } else {
+        VI ca{inf, kSentinel}, cb{-inf, kSentinel};
+        double caa = 0.0, cba = 0.0;
+        if (lane < NW) {
+          ca = VI{sh.wv[0][lane], sh.wi[0][lane]};
+          cb = VI{sh.wv[1][lane], sh.wi[1][lane]};
+          caa = sh.wa[0][lane];
+          cba = sh.wa[1][lane];
         }
-        if (better<false>(b, cb)) {
-          b = cb;
-          ba = sh.wa[1][k];
-        }
+        // Lanes 0..NW-1 hold the wave results: log2(NW) steps leave the merge in lane 0, which is
+        // broadcast (readfirstlane) so every publishing lane sees the same record.
+        a = wave_arg<true, NW>(ca);
+        b = wave_arg<false, NW>(cb);
+        aa = winner_alpha(ca.i, caa, a.i);
+        ba = winner_alpha(cb.i, cba, b.i);
+        a = VI{first_lane(a.v), uint32_t(__builtin_amdgcn_readfirstlane(int(a.i)))};
+        b = VI{first_lane(b.v), uint32_t(__builtin_amdgcn_readfirstlane(int(b.i)))};
+        aa = first_lane(aa);
+        ba = first_lane(ba);
       }
       if (lane < kGranules) {
         // Branch-free payload selection (no divergent switch).
@@ -555,7 +595,7 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
     const double* Kl = K + il * ldk;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int64_t i = lo + t + 256 * e;
+      const int64_t i = lo + t + NT * e;
       const bool ok = i < hi_end;
       kh[e] = ok ? Kh[i] : 0.0;
       kl[e] = ok ? Kl[i] : 0.0;
@@ -589,7 +629,7 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
     // ---- 5. apply: f for the whole slice, alpha for the owners
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int64_t i = lo + t + 256 * e;
+      const int64_t i = lo + t + NT * e;
       fr[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
       if (i == ih) ar[e] = ah_new;
       if (i == il) ar[e] = al_new;
@@ -608,7 +648,7 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
   // Write the slice back; workgroup 0 publishes the final state (visible at kernel end).
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const int64_t i = lo + t + 256 * e;
+    const int64_t i = lo + t + NT * e;
     if (i < hi_end) {
       f[i] = fr[e];
       alpha[i] = ar[e];
@@ -629,37 +669,61 @@ __global__ __launch_bounds__(256) void smo_persistent_kernel(
 
 namespace {
 
-// Launch the persistent solver if the problem fits its register slices; returns false otherwise.
-template <int E>
+// Launch the persistent solver for a (threads per workgroup NT, elements per thread E) shape.
+template <int NT, int E>
 int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
-                        double* f, int64_t n, int64_t slice, unsigned long long* slots, SmoState* st, double C,
-                        double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
+                        double* f, int64_t n, unsigned long long* slots, SmoState* st, double C, double eps,
+                        double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(err) + 8;
+  const int64_t slice = int64_t(NT) * E;
   const char* sv = getenv("SVM355_PSMO_STAMP");
   if (sv && atoi(sv))
-    hipLaunchKernelGGL((smo_persistent_kernel<E, true>), dim3(G), dim3(256), 0, s, K, ldk, y, alpha, f, n, slice, slots,
-                       st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
-  else
-    hipLaunchKernelGGL((smo_persistent_kernel<E, false>), dim3(G), dim3(256), 0, s, K, ldk, y, alpha, f, n, slice,
+    hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true>), dim3(G), dim3(NT), 0, s, K, ldk, y, alpha, f, n, slice,
                        slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
+  else
+    hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false>), dim3(G), dim3(NT), 0, s, K, ldk, y, alpha, f, n,
+                       slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
   SVMD_LAUNCH_CHECK();
   return SVM_OK;
 }
 
-int persistent_grid(int64_t n, int* G_out, int* E_out) {
-  // Elements per thread E in {1,...,16}; workgroups G <= 64 (all co-resident; one sweep pass).
+// Grid shape: NT threads per workgroup (SVM355_PSMO_NT, default kDefaultNT), the smallest E in
+// {1, 2, 4, 8, 16} (capped per NT) with G = ceil(n / (NT*E)) <= target workgroups (SVM355_PSMO_WG,
+// default 64; all co-resident, one sweep pass).
+constexpr int kDefaultNT = 512;
+int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out) {
   int target = 64;
   if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
-  for (int E : {1, 2, 4, 8, 16}) {
-    const int64_t per_wg = int64_t(256) * E;
+  int nt = kDefaultNT;
+  if (const char* v = getenv("SVM355_PSMO_NT")) nt = atoi(v);
+  if (nt != 256 && nt != 512 && nt != 1024) nt = kDefaultNT;
+  const int emax = nt == 256 ? 16 : nt == 512 ? 8 : 4;
+  for (int E = 1; E <= emax; E *= 2) {
+    const int64_t per_wg = int64_t(nt) * E;
     const int64_t G = (n + per_wg - 1) / per_wg;
     if (G <= target) {
       *G_out = int(std::max<int64_t>(1, G));
       *E_out = E;
+      *NT_out = nt;
       return 1;
     }
   }
   return 0;
+}
+
+int launch_persistent(hipStream_t s, int NT, int E, int G, const double* K, int64_t ldk, const int32_t* y,
+                      double* alpha, double* f, int64_t n, unsigned long long* slots, SmoState* st, double C,
+                      double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
+#define SVM_PSMO_CASE(nt, e)                                                                                 \
+  if (NT == nt && E == e)                                                                                    \
+    return launch_persistent_e<nt, e>(s, G, K, ldk, y, alpha, f, n, slots, st, C, eps, tau, max_iter, trace, \
+                                      tcap, err);
+  SVM_PSMO_CASE(256, 1) SVM_PSMO_CASE(256, 2) SVM_PSMO_CASE(256, 4) SVM_PSMO_CASE(256, 8) SVM_PSMO_CASE(256, 16)
+  SVM_PSMO_CASE(512, 1) SVM_PSMO_CASE(512, 2) SVM_PSMO_CASE(512, 4) SVM_PSMO_CASE(512, 8)
+  SVM_PSMO_CASE(1024, 1) SVM_PSMO_CASE(1024, 2) SVM_PSMO_CASE(1024, 4)
+#undef SVM_PSMO_CASE
+  set_error("persistent SMO: no kernel for NT=%d E=%d", NT, E);
+  return SVM_ERR_INTERNAL;
 }
 
 int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t* dtrace, int64_t tcap,
@@ -734,22 +798,15 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   }
 
   // ---- persistent single-launch solver (default when the slices fit in registers)
-  int G = 0, E = 0;
+  int G = 0, E = 0, NT = 0;
   const char* mode = getenv("SVM355_SMO");
   const bool want_persistent = !(mode && strcmp(mode, "graph") == 0);
-  if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E)) {
+  if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT)) {
     auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
     auto* err = reinterpret_cast<unsigned*>(ws + off_slots + size_t(2) * kMaxG * kRecStride * 8);
     SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));  // epochs restart at 1 every launch
-    const int64_t slice = int64_t(256) * E;
-    int lrc = SVM_ERR_INTERNAL;
-    switch (E) {
-      case 1: lrc = launch_persistent_e<1>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
-      case 2: lrc = launch_persistent_e<2>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
-      case 4: lrc = launch_persistent_e<4>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
-      case 8: lrc = launch_persistent_e<8>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
-      default: lrc = launch_persistent_e<16>(s, G, K, ldk, y, alpha, f, n, slice, slots, st, p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, err); break;
-    }
+    const int lrc = launch_persistent(s, NT, E, G, K, ldk, y, alpha, f, n, slots, st, p.C, p.eps, p.tau, p.max_iter,
+                                      dtrace, tcap, err);
     if (lrc) return lrc;
     SmoState* hst = static_cast<SmoState*>(ctx->pinned);
     unsigned herr = 0;
@@ -764,8 +821,8 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
       unsigned long long hs[8];
       SVMD_CHECK(hipMemcpy(hs, reinterpret_cast<unsigned long long*>(err) + 8, sizeof(hs), hipMemcpyDeviceToHost));
       const double cnt = double(kStampCount), mhz = hs[7] ? double(hs[0] + hs[1] + hs[2] + hs[3] + hs[4] + hs[5] + hs[6]) / (double(hs[7]) / 100.0) : 0.0;
-      fprintf(stderr, "[psmo stamps G=%d E=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
-              "globalred+barrier2 %.0f | loads %.0f | update %.0f | clock %.0f MHz | us/iter %.3f\n", G, E,
+      fprintf(stderr, "[psmo stamps NT=%d G=%d E=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
+              "globalred+barrier2 %.0f | loads %.0f | update %.0f | clock %.0f MHz | us/iter %.3f\n", NT, G, E,
               hs[0] / cnt, hs[1] / cnt, hs[2] / cnt, hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, hs[6] / cnt, mhz,
               double(hs[7]) / 100.0 / cnt);
     }
