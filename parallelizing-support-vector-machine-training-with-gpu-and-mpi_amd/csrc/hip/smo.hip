@@ -665,6 +665,190 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Single-workgroup SMO for small problems (n <= NT * E, e.g. the cascade's merge solves on the
+// gathered support vectors).  No cross-workgroup exchange at all: one NT-thread workgroup keeps
+// the whole problem in registers and an iteration is
+//   local scan -> wave64 two-stage arg-reduction -> per-wave record in LDS (double-buffered by
+//   iteration parity) -> ONE __syncthreads -> every wave reduces the NT/64 records itself (identical
+//   inputs and instruction sequence -> identical winners in every wave, no second barrier) ->
+//   update scalars + one memory round trip for K11/K22/K12 and the two kernel rows -> f update.
+// The arithmetic is the persistent kernel's (main3.cpp:235-275 order), so the trajectory is the
+// same bit for bit.
+struct SingleShared {
+  double wv[2][2][16], wa[2][2][16];  // [parity][min|max][wave]
+  uint32_t wi[2][2][16];
+};
+
+template <int kSingleNT, int E, bool STAMP>
+__global__ __launch_bounds__(kSingleNT) void smo_single_kernel(
+    const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
+    double* __restrict__ f, int64_t n, SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter,
+    int64_t* __restrict__ trace, int64_t trace_cap, unsigned long long* __restrict__ stamps) {
+  constexpr int NW = kSingleNT / 64;
+  __shared__ SingleShared sh;
+  unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = 0, rt0 = 0;
+  bool stamping = false;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double c_hi = C - eps, c_lo = 0.0 + eps;
+  const double inf = __builtin_inf();
+  double fr[E], ar[E];
+  int32_t yr[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t i = t + kSingleNT * e;
+    const bool ok = i < n;
+    fr[e] = ok ? f[i] : 0.0;
+    ar[e] = ok ? alpha[i] : 0.0;
+    yr[e] = ok ? y[i] : 0;
+  }
+  int64_t num_iter = st->num_iter;
+  double b_high = st->b_high, b_low = st->b_low;
+  int32_t stop = SVM_STOP_RUNNING;
+  for (uint32_t it = 0;; ++it) {
+    const int par = it & 1;
+    if (STAMP) {
+      const uint32_t epoch = it + 1;
+      const bool on = threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
+      if (on && !stamping) rt0 = __builtin_amdgcn_s_memrealtime();
+      if (!on && stamping) sacc[7] = __builtin_amdgcn_s_memrealtime() - rt0;
+      stamping = on;
+      if (stamping) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sprev)::"memory");
+    }
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+    double amn = 0.0, amx = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t i = uint32_t(t + kSingleNT * e);
+      const double a = ar[e], fi = fr[e];
+      const int32_t yi = yr[e];
+      const bool in_high = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
+      const bool in_low = (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi);
+      if (in_high && fi < mn.v) {
+        mn = VI{fi, i};
+        amn = a;
+      }
+      if (in_low && fi > mx.v) {
+        mx = VI{fi, i};
+        amx = a;
+      }
+    }
+    {
+      const VI wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
+      const double awmn = winner_alpha(mn.i, amn, wmn.i), awmx = winner_alpha(mx.i, amx, wmx.i);
+      PSTAMP(0);
+      if (lane == 0) {
+        sh.wv[par][0][w] = wmn.v;
+        sh.wi[par][0][w] = wmn.i;
+        sh.wa[par][0][w] = awmn;
+        sh.wv[par][1][w] = wmx.v;
+        sh.wi[par][1][w] = wmx.i;
+        sh.wa[par][1][w] = awmx;
+      }
+    }
+    __syncthreads();
+    PSTAMP(1);
+    VI ca{inf, kSentinel}, cb{-inf, kSentinel};
+    double caa = 0.0, cba = 0.0;
+    if (lane < NW) {
+      ca = VI{sh.wv[par][0][lane], sh.wi[par][0][lane]};
+      cb = VI{sh.wv[par][1][lane], sh.wi[par][1][lane]};
+      caa = sh.wa[par][0][lane];
+      cba = sh.wa[par][1][lane];
+    }
+    const VI ga = wave_arg<true, NW>(ca), gb = wave_arg<false, NW>(cb);
+    const double aga = first_lane(winner_alpha(ca.i, caa, ga.i)), agb = first_lane(winner_alpha(cb.i, cba, gb.i));
+    const uint32_t uih = uint32_t(__builtin_amdgcn_readfirstlane(int(ga.i)));
+    const uint32_t uil = uint32_t(__builtin_amdgcn_readfirstlane(int(gb.i)));
+    if (uih == kSentinel || uil == kSentinel) {
+      stop = SVM_STOP_NO_CANDIDATE;
+      break;
+    }
+    PSTAMP(2);
+    const int64_t ih = uih, il = uil;
+    const double bh = first_lane(ga.v), bl = first_lane(gb.v);
+    b_high = bh;
+    b_low = bl;
+    if (bl <= bh + 2.0 * tau) {
+      stop = SVM_STOP_CONVERGED;
+      break;
+    }
+    const int32_t yh = y[ih], yl = y[il];
+    const double K11 = K[ih * ldk + ih], K22 = K[il * ldk + il], K12 = K[ih * ldk + il];
+    double kh[E], kl[E];
+    const double* Kh = K + ih * ldk;
+    const double* Kl = K + il * ldk;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = t + kSingleNT * e;
+      const bool ok = i < n;
+      kh[e] = ok ? Kh[i] : 0.0;
+      kl[e] = ok ? Kl[i] : 0.0;
+    }
+    PSTAMP(3);
+    const double ah = aga, al = agb;
+    const int s = yh * yl;
+    const double eta = K11 + K22 - 2.0 * K12;
+    double U, V;
+    if (s == -1) {
+      U = fmax(0.0, al - ah);
+      V = fmin(C, C + al - ah);
+    } else {
+      U = fmax(0.0, al + ah - C);
+      V = fmin(C, al + ah);
+    }
+    if (!(U <= V + 1e-12)) {
+      stop = SVM_STOP_INFEASIBLE;
+      break;
+    }
+    if (eta <= eps) {
+      stop = SVM_STOP_NONPOS_ETA;
+      break;
+    }
+    double al_new = al + double(yl) * (bh - bl) / eta;
+    if (al_new > V) al_new = V;
+    if (al_new < U) al_new = U;
+    const double ah_new = ah + double(s) * (al - al_new);
+    const double ch = (ah_new - ah) * double(yh);
+    const double cl = (al_new - al) * double(yl);
+    PSTAMP(4);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = t + kSingleNT * e;
+      fr[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
+      if (i == ih) ar[e] = ah_new;
+      if (i == il) ar[e] = al_new;
+    }
+    PSTAMP(5);
+    if (t == 0 && trace && num_iter - 1 < trace_cap) {
+      trace[2 * (num_iter - 1)] = ih;
+      trace[2 * (num_iter - 1) + 1] = il;
+    }
+    ++num_iter;
+    if (num_iter > max_iter) {
+      stop = SVM_STOP_MAX_ITER;
+      break;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t i = t + kSingleNT * e;
+    if (i < n) {
+      f[i] = fr[e];
+      alpha[i] = ar[e];
+    }
+  }
+  if (STAMP && t == 0)
+    for (int q = 0; q < 8; ++q) stamps[q] = sacc[q];
+  if (t == 0) {
+    st->num_iter = num_iter;
+    st->b_high = b_high;
+    st->b_low = b_low;
+    st->pending = 0;
+    st->stop = stop;
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -691,6 +875,8 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
 // {1, 2, 4, 8, 16} (capped per NT) with G = ceil(n / (NT*E)) <= target workgroups (SVM355_PSMO_WG,
 // default 64; all co-resident, one sweep pass).
 constexpr int kDefaultNT = 512;
+constexpr int64_t kSingleDefaultMax = 4096;  // auto mode: single workgroup up to this n (tuned on MI355X)
+constexpr int kSingleDefaultNT = 512;
 int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out) {
   int target = 64;
   if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
@@ -800,6 +986,53 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   // ---- persistent single-launch solver (default when the slices fit in registers)
   int G = 0, E = 0, NT = 0;
   const char* mode = getenv("SVM355_SMO");
+  // ---- single-workgroup solver for small problems (no cross-workgroup exchange)
+  const bool force_single = mode && strcmp(mode, "single") == 0;
+  int64_t single_max = kSingleDefaultMax;
+  if (const char* v = getenv("SVM355_SMO_SINGLE_MAX")) single_max = atoll(v);
+  if ((force_single || !mode || strcmp(mode, "auto") == 0) && (force_single || n <= single_max) && n <= 8192) {
+    int snt = kSingleDefaultNT;
+    if (const char* v = getenv("SVM355_SMO_SINGLE_NT")) snt = atoi(v);
+    if (snt != 256 && snt != 512 && snt != 1024) snt = kSingleDefaultNT;
+    int e = 1;
+    while (int64_t(snt) * e < n) e *= 2;
+    const char* stv = getenv("SVM355_PSMO_STAMP");
+    const bool stamp = stv && atoi(stv);
+    auto* sstamps = reinterpret_cast<unsigned long long*>(ws + off_slots);
+#define SVM_SINGLE_CASE(nt, ee)                                                                                     \
+  else if (snt == nt && e == ee) {                                                                                  \
+    if (stamp)                                                                                                      \
+      hipLaunchKernelGGL((smo_single_kernel<nt, ee, true>), dim3(1), dim3(nt), 0, s, K, ldk, y, alpha, f, n, st,    \
+                         p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, sstamps);                                     \
+    else                                                                                                            \
+      hipLaunchKernelGGL((smo_single_kernel<nt, ee, false>), dim3(1), dim3(nt), 0, s, K, ldk, y, alpha, f, n, st,   \
+                         p.C, p.eps, p.tau, p.max_iter, dtrace, tcap, sstamps);                                     \
+  }
+    if (false) {
+    }
+    SVM_SINGLE_CASE(256, 1) SVM_SINGLE_CASE(256, 2) SVM_SINGLE_CASE(256, 4) SVM_SINGLE_CASE(256, 8)
+    SVM_SINGLE_CASE(256, 16) SVM_SINGLE_CASE(256, 32)
+    SVM_SINGLE_CASE(512, 1) SVM_SINGLE_CASE(512, 2) SVM_SINGLE_CASE(512, 4) SVM_SINGLE_CASE(512, 8) SVM_SINGLE_CASE(512, 16)
+    SVM_SINGLE_CASE(1024, 1) SVM_SINGLE_CASE(1024, 2) SVM_SINGLE_CASE(1024, 4) SVM_SINGLE_CASE(1024, 8)
+    else {
+      set_error("single-workgroup SMO: n = %lld too large for %d threads", (long long)n, snt);
+      return SVM_ERR_INTERNAL;
+    }
+#undef SVM_SINGLE_CASE
+    SVMD_LAUNCH_CHECK();
+    SmoState* hst = static_cast<SmoState*>(ctx->pinned);
+    SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipStreamSynchronize(s));
+    if (stamp) {
+      unsigned long long hs[8];
+      SVMD_CHECK(hipMemcpy(hs, sstamps, sizeof(hs), hipMemcpyDeviceToHost));
+      const double cnt = double(kStampCount);
+      fprintf(stderr, "[single stamps NT=%d E=%d] cycles/iter: scan+wavered %.0f | barrier %.0f | blockred %.0f | "
+              "loads %.0f | scalar %.0f | update %.0f | us/iter %.3f\n", snt, e, hs[0] / cnt, hs[1] / cnt, hs[2] / cnt,
+              hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, double(hs[7]) / 100.0 / cnt);
+    }
+    return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
+  }
   const bool want_persistent = !(mode && strcmp(mode, "graph") == 0);
   if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT)) {
     auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);

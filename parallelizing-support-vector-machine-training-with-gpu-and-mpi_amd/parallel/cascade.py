@@ -97,6 +97,7 @@ class _HipBackend:
         self.d = d
         self.width = D.padded_dim(d)
         self.device = device
+        self.stats = None  # host (min, max) the rows were scaled with -> exact-integer Gram path
 
     def to_rows(self, X: np.ndarray, device) -> torch.Tensor:
         return self.D.upload_rows(X, self.device, self.width)
@@ -109,6 +110,8 @@ class _HipBackend:
         return self.D.minmax(X, self.d)
 
     def scale_(self, X: torch.Tensor, mn: torch.Tensor, mx: torch.Tensor) -> None:
+        if self.stats is None:
+            self.stats = (mn.detach().cpu().numpy().copy(), mx.detach().cpu().numpy().copy())
         if X.shape[0]:
             self.D.minmax_scale_(X, self.d, mn, mx)
 
@@ -119,7 +122,8 @@ class _HipBackend:
         yd = torch.from_numpy(np.ascontiguousarray(y, dtype=np.int32)).to(self.device)
         ad = torch.from_numpy(np.ascontiguousarray(alpha, dtype=np.float64)).to(self.device)
         K = torch.empty((m, (m + 1) // 2 * 2), dtype=torch.float64, device=self.device)
-        res, _ = D.train(X, sqn, yd, ad, self.params, warm=True, K=K)
+        mn, mx = self.stats if self.stats is not None else (None, None)
+        res, _ = D.train(X, sqn, yd, ad, self.params, warm=True, K=K, mn=mn, mx=mx)
         del K
         return ad.cpu().numpy(), res
 

@@ -113,8 +113,9 @@ def smo_mode(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("smo_mode", [("persistent", None), ("persistent", 1), ("persistent", 3), ("graph", None)],
-                         indirect=True, ids=["persistent", "persistent-G1", "persistent-G2", "graph"])
+@pytest.mark.parametrize("smo_mode", [("persistent", None), ("persistent", 1), ("persistent", 3), ("graph", None),
+                                      ("single", None)],
+                         indirect=True, ids=["persistent", "persistent-G1", "persistent-G2", "graph", "single"])
 def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data, smo_mode):
     tr, _ = mn_data
     X = MinMaxScaler().fit_transform(tr.X[:900])
@@ -148,6 +149,26 @@ def test_persistent_vs_graph_many_workgroups(dev, D, monkeypatch):
         r, trc = D.smo(K, yd, a, SVMParams(), n=tr.n, trace_cap=1000000)
         out[mode] = (r, trc, a.cpu().numpy())
     (r1, t1, a1), (r2, t2, a2) = out["persistent"], out["graph"]
+    assert r1.iterations == r2.iterations and r1.b == r2.b and r1.stop_reason == "converged"
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(a1, a2)
+
+
+@pytest.mark.parametrize("n", [3000, 7000])
+def test_single_workgroup_smo_matches_persistent(dev, D, monkeypatch, n):
+    """The single-workgroup solver (E = 4 and 8 register elements) follows the persistent trajectory."""
+    tr = synthetic_mnist(n, seed=11)
+    Xd = D.upload_rows(tr.X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    K, _ = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    yd = torch.from_numpy(tr.y).to(dev)
+    out = {}
+    for mode in ("single", "persistent"):
+        monkeypatch.setenv("SVM355_SMO", mode)
+        a = torch.zeros(n, dtype=torch.float64, device=dev)
+        r, trc = D.smo(K, yd, a, SVMParams(), n=n, trace_cap=200000)
+        out[mode] = (r, trc, a.cpu().numpy())
+    (r1, t1, a1), (r2, t2, a2) = out["single"], out["persistent"]
     assert r1.iterations == r2.iterations and r1.b == r2.b and r1.stop_reason == "converged"
     np.testing.assert_array_equal(t1, t2)
     np.testing.assert_array_equal(a1, a2)
