@@ -46,6 +46,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--cascade", action="store_true",
+                    help="run the cascade path even on one rank (rehearsal of the RCCL code path)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N > 1 (gloo: CPU-staged exchanges, for rehearsals of the "
                          "multi-rank path on fewer GPUs than ranks)")
@@ -70,8 +72,9 @@ def main(argv=None):
     from svm355.parallel.cascade import CascadeSVM, partition_bounds
     from svm355.utils.data import synthetic_mnist
 
+    use_cascade = world > 1 or a.cascade
     dist = None
-    if world > 1:
+    if use_cascade:
         import torch.distributed as dist
 
         if a.backend == "nccl":
@@ -81,7 +84,7 @@ def main(argv=None):
     comm_dev = dev if a.backend == "nccl" else torch.device("cpu")
     params = SVMParams()
 
-    if world == 1:
+    if not use_cascade:
         tr = synthetic_mnist(a.n, seed=a.seed)
     else:
         lo, hi = partition_bounds(a.n, world, rank)
@@ -101,7 +104,7 @@ def main(argv=None):
 
     def step():
         nonlocal model
-        if world == 1:
+        if not use_cascade:
             model = SVC(device=str(dev)).fit(tr.X, tr.y)
         else:
             from svm355.parallel.transport import TorchDistTransport
@@ -127,7 +130,7 @@ def main(argv=None):
     ms = elapsed / a.steps * 1e3
     value = ms / 1e3
     extra = {}
-    if world == 1:
+    if not use_cascade:
         acc = model.score(te.X, te.y)
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
                  "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_}
@@ -157,7 +160,7 @@ def main(argv=None):
                 "model": "RBF SVM, first-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,
-                "parallelism": "single-gpu" if world == 1 else f"cascade-{a.topology}-dp{world}",
+                "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{world}",
             },
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),

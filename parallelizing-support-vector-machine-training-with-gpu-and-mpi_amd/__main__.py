@@ -1,0 +1,202 @@
+"""Command-line entry points: ``python -m svm355 {serial,gpu,sweep,cascade} [options]``.
+
+serial   the reference's serial program (code/main3.cpp) -> native ``bin/svm_serial``
+gpu      the single-GPU program (code/gpu_svm_main3.cu; ``--n-limit N`` = gpu_svm_main4.cu) ->
+         native ``bin/svm_gpu``
+sweep    the training-set-size sweep of code/gpu_svm4.sh (n = 10k, 20k, ..., 60k on one GPU),
+         printing the reference's Table 2 layout (training / prediction seconds per n)
+cascade  the MPI Cascade programs (code/mpi_svm_main2.cpp ``--topology star`` = modified two-layer,
+         code/mpi_svm_main3.cpp ``--topology tree`` = classical), one process per GPU over
+         torch.distributed (RCCL/xGMI; ``--backend gloo`` for CPU ranks).  Run it under
+         ``torchrun --nproc-per-node P`` or pass ``--gpus P`` and it launches torchrun itself.
+         stdout follows the reference's ``[rank 0] ...`` lines.
+
+The native CLIs take the options listed in ``csrc/apps/cli_common.h`` (``--dataset``,
+``--synthetic N[,M]``, ``--C``, ``--gamma``, ``--tau``, ``--model-dir``, ``--json`` ...).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+
+
+def _native(name: str, args) -> int:
+    exe = PKG / "bin" / name
+    if not exe.exists():
+        from . import build
+
+        build.build_all(hip=name != "svm_serial")
+    return subprocess.call([str(exe), *args])
+
+
+def _sweep(argv) -> int:
+    ap = argparse.ArgumentParser(prog="svm355 sweep", description="gpu_svm4.sh: n = 10k..60k on one GPU")
+    ap.add_argument("--sizes", default="10000,20000,30000,40000,50000,60000")
+    ap.add_argument("--out", default=None, help="write the per-n JSON summaries to this file")
+    a, rest = ap.parse_known_args(argv)
+    exe = PKG / "bin" / "svm_gpu"
+    if not exe.exists():
+        from . import build
+
+        build.build_all()
+    rows = []
+    tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"svm355_sweep_{os.getpid()}.json"
+    for n in [int(v) for v in a.sizes.split(",")]:
+        rc = subprocess.call([str(exe), "--n-limit", str(n), "--json", str(tmp), "--quiet", *rest],
+                             stdout=subprocess.DEVNULL)
+        if rc:
+            return rc
+        rows.append(json.loads(tmp.read_text()))
+    tmp.unlink(missing_ok=True)
+    print(f"{'n train':>8} {'train (s)':>10} {'predict (s)':>12} {'iterations':>11} {'#SV':>6} {'accuracy':>9} gram")
+    for r in rows:
+        print(f"{r['n']:>8} {r['training_ms'] / 1e3:>10.3f} {r['prediction_ms'] / 1e3:>12.3f} {r['iterations']:>11} "
+              f"{r['n_sv']:>6} {r['accuracy']:>9.4f} {r.get('gram_path', '')}")
+    if a.out:
+        Path(a.out).write_text(json.dumps(rows, indent=1) + "\n")
+    return 0
+
+
+def _cascade(argv) -> int:
+    ap = argparse.ArgumentParser(prog="svm355 cascade", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--topology", choices=["star", "tree"], default="star",
+                    help="star = modified two-layer (mpi_svm_main2), tree = classical (mpi_svm_main3)")
+    ap.add_argument("--dataset", default="mnist3", help="CSV prefix: P_train_data.csv / P_test_data.csv")
+    ap.add_argument("--train", default=None)
+    ap.add_argument("--test", default=None)
+    ap.add_argument("--synthetic", default=None, help="N[,M]: MNIST-shaped synthetic data instead of CSVs")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--positive-label", type=int, default=1)
+    ap.add_argument("--C", type=float, default=10.0)
+    ap.add_argument("--gamma", type=float, default=0.00125)
+    ap.add_argument("--tau", type=float, default=1e-5)
+    ap.add_argument("--max-rounds", type=int, default=50)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--cpu", action="store_true", help="solve on CPU ranks (native oracle) instead of GPUs")
+    ap.add_argument("--gpus", type=int, default=0, help="launch torchrun with this many ranks (if not under it)")
+    ap.add_argument("--model-dir", default=None)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--checkpoint-dir", default=None, help="per-round cascade state (resume with --resume)")
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("-v", "--verbose", type=int, default=1)
+    a = ap.parse_args(argv)
+
+    if "RANK" not in os.environ and a.gpus > 0:
+        # Not under a launcher: start one (a child process — never exec from here).
+        fwd, skip = [], False
+        for x in argv:
+            if skip:
+                skip = False
+            elif x == "--gpus":
+                skip = True
+            elif not x.startswith("--gpus="):
+                fwd.append(x)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
+               "-m", "svm355", "cascade", *fwd]
+        return subprocess.call(cmd, cwd=str(PKG.parent))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from .parallel.cascade import CascadeSVM, partition_bounds
+    from .parallel.transport import TorchDistTransport
+    from .utils.config import SVMParams
+    from .utils.data import load_csv, synthetic_mnist
+
+    if "RANK" not in os.environ:  # single process: a world of one
+        os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                           "MASTER_PORT": os.environ.get("MASTER_PORT", "29534")})
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = not a.cpu and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    backend = a.backend if use_gpu else "gloo"
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    comm_dev = dev if backend == "nccl" else torch.device("cpu")
+
+    if a.synthetic:
+        parts = a.synthetic.split(",")
+        n_total, m = int(parts[0]), int(parts[1]) if len(parts) > 1 else 10000
+        lo, hi = partition_bounds(n_total, world, rank)
+        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo, positive_label=a.positive_label)
+        te = synthetic_mnist(m, seed=a.seed, offset=n_total, positive_label=a.positive_label) if rank == 0 else None
+    else:
+        full = load_csv(a.train or f"{a.dataset}_train_data.csv", positive_label=a.positive_label)
+        n_total = full.n
+        if n_total == 0:
+            print("Error: No data read from file.", file=sys.stderr)
+            return 1
+        lo, hi = partition_bounds(n_total, world, rank)
+        tr = full.subset(lo, hi)
+        te = load_csv(a.test or f"{a.dataset}_test_data.csv", positive_label=a.positive_label) if rank == 0 else None
+
+    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=os.cpu_count() or 1)
+    model = CascadeSVM(TorchDistTransport(comm_dev), params, topology=a.topology, max_rounds=a.max_rounds,
+                       verbose=a.verbose, checkpoint_dir=a.checkpoint_dir, resume=a.resume, device=dev)
+    t0 = time.perf_counter()
+    res = model.fit(tr.X, tr.y, np.arange(lo, hi), n_total=n_total)
+    t1 = time.perf_counter()
+    out = {}
+    if rank == 0:
+        acc = None
+        if te is not None and te.n:
+            pred = model.predict(te.X)
+            correct = int((pred == te.y).sum())
+            acc = correct / te.n
+            print(f"[rank 0] Test accuracy (final model) = {acc} ({correct}/{te.n})")
+        else:
+            print("[rank 0] No test data found or test file empty.")
+        t2 = time.perf_counter()
+        train_ms, pred_ms = res.train_ms, (t2 - t1) * 1e3
+        print(f"[rank 0] Final global SV count = {len(res.sv)}")
+        print(f"[rank 0] Cascade finished in {res.rounds} rounds")
+        print(f"[rank 0] training time = {int(train_ms)} ms")
+        print(f"[rank 0] prediction time = {int(pred_ms)} ms")
+        print(f"[rank 0] elapsed time = {int(train_ms + pred_ms)} ms")
+        out = {"program": f"svm355 cascade ({a.topology})", "world": world, "n": n_total, **model.summary(),
+               "accuracy": acc, "training_ms": train_ms, "prediction_ms": pred_ms, "fit_wall_ms": (t1 - t0) * 1e3}
+        if a.json:
+            Path(a.json).write_text(json.dumps(out) + "\n")
+        if a.model_dir:
+            model.save(a.model_dir)
+    dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] in ("-h", "--help"):
+        print(__doc__)
+        return 0
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "serial":
+        return _native("svm_serial", rest)
+    if cmd == "gpu":
+        return _native("svm_gpu", rest)
+    if cmd == "sweep":
+        return _sweep(rest)
+    if cmd == "cascade":
+        return _cascade(rest)
+    print(f"unknown command {cmd!r}\n\n{__doc__}", file=sys.stderr)
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

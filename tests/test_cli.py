@@ -1,0 +1,54 @@
+"""CLI entry points (python -m svm355 ...): reference stdout contract and JSON summaries (CPU)."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _run(args, tmp_path, timeout=600):
+    env = dict(os.environ, MASTER_PORT=str(29600 + os.getpid() % 300))
+    r = subprocess.run([sys.executable, "-m", "svm355", *args], cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_cli_help(tmp_path):
+    out = _run(["--help"], tmp_path)
+    assert "serial" in out and "cascade" in out
+
+
+def test_cli_serial_reference_lines(tmp_path):
+    js = tmp_path / "s.json"
+    out = _run(["serial", "--synthetic", "600,200", "--json", str(js), "--model-dir", str(tmp_path / "m")], tmp_path)
+    lines = [l.split("=")[0].split(":")[0].strip() for l in out.strip().splitlines()]
+    assert lines == ["n", "n_features", "number of iterations", "b", "(b_high - b_low)/2*1e10", "Final SV count",
+                     "Test accuracy", "Training time", "Prediction time", "Total Runtime"]
+    s = json.loads(js.read_text())
+    assert s["stop_reason"] == "converged" and s["n"] == 600
+    for f in ("final_sv_ids.txt", "final_sv_labels.txt", "final_sv_alphas.txt", "final_b.txt"):
+        assert (tmp_path / "m" / f).exists()
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_cli_cascade_single_rank_cpu(tmp_path, topology):
+    js = tmp_path / "c.json"
+    out = _run(["cascade", "--synthetic", "700,200", "--cpu", "--topology", topology, "--json", str(js)], tmp_path)
+    assert "[rank 0] Running" in out and "[rank 0] Final b = " in out
+    assert "[rank 0] Cascade finished in" in out and "[rank 0] training time =" in out
+    s = json.loads(js.read_text())
+    assert s["converged"] and s["world"] == 1 and s["accuracy"] > 0.9
+
+
+def test_cli_cascade_two_ranks_gloo(tmp_path):
+    js = tmp_path / "c2.json"
+    out = _run(["cascade", "--synthetic", "900,200", "--cpu", "--gpus", "2", "--backend", "gloo",
+                "--json", str(js)], tmp_path, timeout=900)
+    assert "[rank 0] Running modified CascadeSVM with 2 processes" in out
+    s = json.loads(js.read_text())
+    assert s["converged"] and s["world"] == 2
