@@ -96,13 +96,15 @@ int launch_gemv_rows(hipStream_t s, const double* K, int64_t ldk, int64_t m, int
 // Exact-integer Gram path (igram.hip).
 struct QuantPlan {
   bool ok = false;
-  double w0 = 0.0;          // base weight 1/r^2 shared by the int8 part
-  int kc = 0, kq = 0;       // correction columns (multiple of 16), total int8 columns (multiple of 64)
-  int n_corr = 0;           // real correction columns
+  double w0 = 0.0;            // weight 1/r^2 of the main (exact-integer) column group
+  int kq = 0;                 // int8 columns (multiple of 64)
+  int main0 = 0;              // first column of the main group (extra groups before it, multiple of 32)
+  int n_groups = 0;
   std::vector<int32_t> perm;  // permuted column order (-1 = zero pad)
   std::vector<double> rmul;   // r_j per permuted column (scaled value * r_j = integer)
-  std::vector<double> delta;  // w_j - w0 per correction column
-  std::vector<double> cen;    // centre floor(r_j / 2) of each correction column's integer range
+  std::vector<double> off;    // centring offset floor(r_j / 2)
+  std::vector<double> wx;     // 1/r_j^2 for extra-group columns (0 for main / pad)
+  std::vector<double> step_w; // per 32-column k-step below main0: group weight at its last step, else 0
 };
 bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P);
 size_t igram_workspace(int64_t n, const QuantPlan& P);

@@ -2,26 +2,26 @@
 //
 // MNIST-shaped inputs are integer pixel intensities, and after the reference's min-max scaling
 // (main3.cpp:74-89) feature j of every row is x_j = q_j / r_j with q_j = p_j - min_j an integer in
-// [0, r_j] and r_j = max_j - min_j.  So
+// [0, r_j] and r_j = max_j - min_j <= 255.  Grouping the columns by range (weight w_g = 1 / r_g^2):
 //
-//     ||x_a - x_b||^2 = sum_j w_j (q_aj - q_bj)^2,           w_j = 1 / r_j^2
-//                     = w0 * D_ab + sum_{j in corr} (w_j - w0) (q_aj - q_bj)^2
+//     ||x_a - x_b||^2 = sum_g w_g sum_{j in g} (q_aj - q_bj)^2
 //
-// where w0 is the weight shared by most columns (r_j = 255 on MNIST) and
-// D_ab = sum_j (q_aj - q_bj)^2 = N_a + N_b - 2 * I_ab is an EXACT integer: I_ab = sum_j q'_aj q'_bj
-// on biased int8 operands q' = q - 128 (the bias cancels in the difference) is one
-// v_mfma_i32_32x32x32_i8 GEMM with int32 accumulation.  The few columns whose range differs
-// ("correction" columns, <= 12% on MNIST-shaped data) are placed first in a permuted column order
-// and their weighted term is an FP64 v_mfma_f64_16x16x4_f64 GEMM fed from the SAME staged int8
-// tiles (converted in registers and scaled by sqrt|delta_j|, delta_j = w_j - w0).  The distance is therefore
-// computed without the catastrophic ||a||^2 + ||b||^2 - 2ab cancellation of the plain FP64 path
-// (gram_mfma.hip): the integer part is exact and the FP64 part is small, so every kernel value is
-// FP64-accurate (tests/test_gpu_kernels.py checks |K - K_exact| <= 1e-15).
+// Every column is stored as ONE signed byte, centred on ceil(r_j / 2) (differences are invariant
+// to the shift), and every group's cross term I_g = sum_{j in g} q'_aj q'_bj is an exact int32
+// v_mfma_i32_32x32x32_i8 accumulation:
+//   * the MAIN group (the most common range: r = 255 on MNIST) is accumulated last and kept as an
+//     integer: D0 = N0_a + N0_b - 2 I0 is the EXACT integer sum of squared differences;
+//   * every other group ("extra" columns, each group padded to a 32-column k-step) is flushed at
+//     its last k-step into an FP64 accumulator X += w_g * I_g that lives in the same 32x32
+//     accumulator layout (no lane shuffles), with per-row weighted norms WN = sum w_g N_g.
+// dist = w0 * D0 + (WN_a + WN_b - 2 X): the dominant part is exact, the extra part is small
+// (centred operands), so every kernel value is FP64-accurate (tests/test_gpu_kernels.py checks
+// |K - K_exact| <= 2e-15) and the Gram is exactly symmetric.  No FP64 MFMA work remains.
 //
 // Reference: calc_kernel_matrix (gpu_svm_main3.cu:137-147) evaluates one FP64 row per launch with
 // a d-long scalar loop per thread.  Here the whole upper-triangular Gram is produced in one launch
-// (128x128 tiles, 4 waves of 64x64, XCD-aware tile order), the mirror half is written through an
-// LDS transpose, and the FP64 MFMA work is ~8x smaller than the plain FP64 Gram.
+// (128x128 tiles split into two 128x64 workgroups of 4 waves x 32x64 = 2 MFMA 32x32 tiles per
+// wave, XCD-aware tile order) and the mirror half is written through a per-wave LDS transpose.
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -35,30 +35,31 @@ namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int QBM = 128;        // tile rows / cols
-constexpr int QBK = 64;         // int8 columns per LDS stage
+constexpr int QBK = 64;         // int8 columns per LDS stage (two 32-deep MFMA k-steps)
 constexpr int QLS = QBK + 16;   // LDS row stride in bytes (80: conflict-free ds_read_b128 rows)
-constexpr int kMaxCorr = 1024;  // correction columns kept in LDS (scales, centres)
-constexpr int kStageBytes = 2 * QBM * QLS + kMaxCorr * 24;
-constexpr int kEpiBytes = 4 * 32 * 33 * 4 + 4 * 16 * 17 * 8;  // int transpose + mirror scratch
-constexpr int kSmemBytes = kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes;
+constexpr int QBN = 64;         // columns per workgroup (half of a 128x128 tile)
+constexpr int kMaxSteps = 128;  // 32-column k-steps (kq <= 4096)
+// staging tiles + step weights + row/col norms of the tile, then the per-wave transpose images
+constexpr int kStageBytes = (QBM + QBN) * QLS + kMaxSteps * 8 + (QBM + QBN) * 12;
+constexpr int kSmemBytes = kStageBytes + 4 * 32 * 33 * 8;
 
-// ---- quantisation: one wave per row.  Writes the permuted biased int8 row, N = sum q'^2 (exact)
-// and cN = sum_{k < kc} delta_k (q_k - c_k)^2 (correction operand centred on c_k = floor(r_k / 2),
-// which keeps the FP64 correction terms small); flags any value that is not an integer in [0, 255].
+// ---- quantisation: one wave per row.  Writes the permuted centred int8 row q'_k = q_k - off_k,
+// N0 = sum_{main} q'^2 (exact int) and WN = sum_{extra} w_k q'^2; flags any value that is not an
+// integer in [0, 255] (the caller then uses the FP64 Gram).
 __global__ __launch_bounds__(256) void quantize_rows_kernel(
     const double* __restrict__ X, int64_t n, int64_t ld, const int32_t* __restrict__ perm,
-    const double* __restrict__ rmul, const double* __restrict__ delta, const double* __restrict__ cen, int kc,
-    int kq, int8_t* __restrict__ Q, int32_t* __restrict__ Nq, double* __restrict__ cN, unsigned* __restrict__ fail) {
+    const double* __restrict__ rmul, const double* __restrict__ off, const double* __restrict__ wx, int main0,
+    int kq, int8_t* __restrict__ Q, int32_t* __restrict__ N0, double* __restrict__ WN, unsigned* __restrict__ fail) {
   const int lane = threadIdx.x & 63;
   const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const double* xr = X + row * ld;
   int32_t* qr = reinterpret_cast<int32_t*>(Q + row * int64_t(kq));
   int32_t nacc = 0;
-  double cacc = 0.0;
+  double wacc = 0.0;
   bool bad = false;
   for (int w = lane; w < kq / 4; w += 64) {
     uint32_t word = 0;
@@ -71,215 +72,167 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
         const double v = xr[j] * rmul[k];
         const double q = rint(v);
         bad |= !(fabs(v - q) <= 1e-6) || q < 0.0 || q > 255.0;
-        qq = int(q) - 128;
-        nacc += qq * qq;
-        if (k < kc) {
-          const double qc = q - cen[k];  // centred correction operand (exact)
-          cacc += delta[k] * (qc * qc);
-        }
+        qq = int(q - off[k]);
+        if (k >= main0)
+          nacc += qq * qq;
+        else
+          wacc += wx[k] * double(qq * qq);
       }
       word |= uint32_t(uint8_t(int8_t(qq))) << (8 * b);
     }
     qr[w] = int32_t(word);
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nacc += __shfl_xor(nacc, off, kWave);
-  cacc = wave_sum(cacc);
+  for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o, kWave);
+  wacc = wave_sum(wacc);
   if (lane == 0) {
-    Nq[row] = nacc;
-    cN[row] = cacc;
+    N0[row] = nacc;
+    WN[row] = wacc;
   }
   if (__any(bad) && lane == 0) atomicOr(fail, 1u);
 }
 
-__device__ __forceinline__ double sbyte(uint32_t w, int s) {  // signed byte s of w -> double
-  return double(int32_t(w << (24 - 8 * s)) >> 24);
-}
-
-// Upper-triangular tiles of K = exp(-gamma * dist) for the n quantised rows, each off-diagonal
-// tile also stored transposed.  kc = correction columns (multiple of 16, <= kMaxCorr), kq = total
-// int8 columns (multiple of QBK).
-template <bool CORR>
+// Upper-triangular 128x128 tiles of K = exp(-gamma * dist), each split into two 128x64 halves
+// (one workgroup each: 4 waves x 32 rows x 64 columns, 2 MFMA 32x32 tiles per wave), each
+// off-diagonal tile also stored transposed.  kq = int8 columns (multiple of QBK); columns
+// [0, main0) are the extra groups (main0 a multiple of 32), step_w[s] = weight of k-step s's group
+// if s is the LAST k-step of its group (flush), else 0.
+template <bool EXTRA>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
-    const int8_t* __restrict__ Q, int64_t n, int kq, int kc, const int32_t* __restrict__ Nq,
-    const double* __restrict__ cN, const double* __restrict__ delta, const double* __restrict__ cen, double w0,
-    double neg_gamma,
+    const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
+    const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
     double* __restrict__ K, int64_t ldk, int64_t tiles) {
   __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
-  char* As = smem;
-  char* Bs = smem + QBM * QLS;
-  double* dsa = reinterpret_cast<double*>(smem + 2 * QBM * QLS);  // sqrt|delta_k|
-  double* dsb = dsa + kMaxCorr;                                     // sign(delta_k) sqrt|delta_k|
-  double* dco = dsb + kMaxCorr;                                     // 128 - c_k (byte -> centred q)
+  char* As = smem;                                   // 128 rows x QLS
+  char* Bs = smem + QBM * QLS;                       // 64 rows x QLS
+  double* sw = reinterpret_cast<double*>(smem + (QBM + QBN) * QLS);
+  double* wn_r = sw + kMaxSteps;                     // WN of the tile's 128 rows / 64 cols
+  double* wn_c = wn_r + QBM;
+  int32_t* n0_r = reinterpret_cast<int32_t*>(wn_c + QBN);
+  int32_t* n0_c = n0_r + QBM;
+  double* img = reinterpret_cast<double*>(smem + kStageBytes);  // per-wave 32x33 transpose images
 
+  const int64_t ntile = tiles * (tiles + 1) / 2;
+  const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
   int64_t tm, tn;
-  tri_tile(xcd_remap(blockIdx.x, tiles * (tiles + 1) / 2), tiles, tm, tn);
-  const int64_t bm = tm * QBM, bn = tn * QBM;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  tri_tile(wg >> 1, tiles, tm, tn);
+  const int64_t bm = tm * QBM, bn = tn * QBM + (wg & 1) * QBN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int main_step0 = main0 / 32;
+  if (EXTRA)
+    for (int k = t; k < main_step0; k += 256) sw[k] = step_w[k];
+  if (t < QBM) {
+    const int64_t gi = bm + t;
+    n0_r[t] = gi < n ? N0[gi] : 0;
+    if (EXTRA) wn_r[t] = gi < n ? WN[gi] : 0.0;
+  } else if (t < QBM + QBN) {
+    const int64_t gj = bn + (t - QBM);
+    n0_c[t - QBM] = gj < n ? N0[gj] : 0;
+    if (EXTRA) wn_c[t - QBM] = gj < n ? WN[gj] : 0.0;
+  }
 
-  // Both operands carry sqrt|delta| (B also the sign), so the (i, j) and (j, i) products of a
-  // diagonal tile are the same two rounded factors: the Gram comes out exactly symmetric.
-  if (CORR)
-    for (int k = t; k < kc; k += 256) {
-      const double sd = sqrt(fabs(delta[k]));
-      dsa[k] = sd;
-      dsb[k] = delta[k] < 0.0 ? -sd : sd;
-      dco[k] = 128.0 - cen[k];
-    }
-
-  // Staging: 128 rows x 64 B per operand = 512 x 16 B; thread t copies rows t>>2 and 64 + (t>>2),
-  // 16-byte column chunk t&3.
+  // Staging per 64-column stage: A 128 rows (2 x 16 B per thread), B 64 rows (1 x 16 B).
   const int srow = t >> 2, scol = (t & 3) * 16;
-  const int64_t ra0 = bm + srow, ra1 = bm + srow + 64, rb0 = bn + srow, rb1 = bn + srow + 64;
+  const int64_t ra0 = bm + srow, ra1 = bm + srow + 64, rb0 = bn + srow;
   const i32x4 zero4 = {0, 0, 0, 0};
-  i32x4 ga[2], gb[2];
+  i32x4 ga[2], gb;
   auto gload = [&](int k0) {
     ga[0] = ra0 < n ? *reinterpret_cast<const i32x4*>(Q + ra0 * kq + k0 + scol) : zero4;
     ga[1] = ra1 < n ? *reinterpret_cast<const i32x4*>(Q + ra1 * kq + k0 + scol) : zero4;
-    gb[0] = rb0 < n ? *reinterpret_cast<const i32x4*>(Q + rb0 * kq + k0 + scol) : zero4;
-    gb[1] = rb1 < n ? *reinterpret_cast<const i32x4*>(Q + rb1 * kq + k0 + scol) : zero4;
+    gb = rb0 < n ? *reinterpret_cast<const i32x4*>(Q + rb0 * kq + k0 + scol) : zero4;
   };
   gload(0);
 
-  i32x16 acc[2][2];
+  i32x16 acc[2];
+  double xacc[2][16];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
-  f64x4 cacc[4][4];
-  if (CORR) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cacc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
-  }
+    for (int r = 0; r < 16; ++r) {
+      acc[j][r] = 0;
+      if (EXTRA) xacc[j][r] = 0.0;
+    }
 
-  const int l32 = lane & 31, h = lane >> 5;
-  const int lr = lane & 15, lg = lane >> 4;
   for (int k0 = 0; k0 < kq; k0 += QBK) {
     __syncthreads();
     *reinterpret_cast<i32x4*>(As + srow * QLS + scol) = ga[0];
     *reinterpret_cast<i32x4*>(As + (srow + 64) * QLS + scol) = ga[1];
-    *reinterpret_cast<i32x4*>(Bs + srow * QLS + scol) = gb[0];
-    *reinterpret_cast<i32x4*>(Bs + (srow + 64) * QLS + scol) = gb[1];
+    *reinterpret_cast<i32x4*>(Bs + srow * QLS + scol) = gb;
     __syncthreads();
     if (k0 + QBK < kq) gload(k0 + QBK);
 
-    // int8 part: two 32-deep k-steps.  A and B fragments use the same (lane, byte) -> k map, so
-    // the product is independent of the hardware's k order inside a step.
+    // A and B fragments use the same (lane, byte) -> k map, so the product is independent of the
+    // hardware's k order inside a step.
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      i32x4 a[2], b[2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-        a[mi] = *reinterpret_cast<const i32x4*>(As + (wr * 64 + mi * 32 + l32) * QLS + ks * 32 + 16 * h);
+      const i32x4 a = *reinterpret_cast<const i32x4*>(As + (w * 32 + l32) * QLS + ks * 32 + 16 * h);
+      i32x4 b[2];
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj)
-        b[nj] = *reinterpret_cast<const i32x4*>(Bs + (wc * 64 + nj * 32 + l32) * QLS + ks * 32 + 16 * h);
+        b[nj] = *reinterpret_cast<const i32x4*>(Bs + (nj * 32 + l32) * QLS + ks * 32 + 16 * h);
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int nj = 0; nj < 2; ++nj) acc[nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[nj], acc[nj], 0, 0, 0);
+      if (EXTRA) {
+        const int step = k0 / 32 + ks;
+        if (step < main_step0) {
+          const double wgt = sw[step];
+          if (wgt != 0.0) {  // last k-step of an extra group: flush its exact cross term
 #pragma unroll
-        for (int nj = 0; nj < 2; ++nj)
-          acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
-    }
-
-    // FP64 correction columns: 16-column chunks of this stage below kc.  Lane group lg at
-    // sub-step s uses column 4*lg + s of the chunk (same map for A and B).
-    if (CORR) {
+            for (int nj = 0; nj < 2; ++nj)
 #pragma unroll
-      for (int c = 0; c < QBK / 16; ++c) {
-        const int kb = k0 + 16 * c;
-        if (kb >= kc) break;
-        uint32_t aw[4], bw[4];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          aw[mi] = *reinterpret_cast<const uint32_t*>(As + (wr * 64 + mi * 16 + lr) * QLS + 16 * c + 4 * lg);
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj)
-          bw[nj] = *reinterpret_cast<const uint32_t*>(Bs + (wc * 64 + nj * 16 + lr) * QLS + 16 * c + 4 * lg);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kk = kb + 4 * lg + s;
-          const double sa = dsa[kk], sb = dsb[kk], co = dco[kk];
-          double af[4], bf[4];
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) af[mi] = (sbyte(aw[mi], s) + co) * sa;
-#pragma unroll
-          for (int nj = 0; nj < 4; ++nj) bf[nj] = (sbyte(bw[nj], s) + co) * sb;
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int nj = 0; nj < 4; ++nj)
-              cacc[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mi], bf[nj], cacc[mi][nj], 0, 0, 0);
+              for (int r = 0; r < 16; ++r) {
+                xacc[nj][r] += wgt * double(acc[nj][r]);
+                acc[nj][r] = 0;
+              }
+          }
         }
       }
     }
   }
 
-  // ---- epilogue.  int32 32x32 C layout: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-  // f64 16x16 layout: col = lane & 15, row = (lane >> 4) + 4 * r.  Each int block goes through a
-  // per-wave LDS image so every lane picks up the integer for its f64-layout element.
-  __syncthreads();  // staging tiles fully consumed: reuse them as scratch
-  int32_t* iscr = reinterpret_cast<int32_t*>(smem) + w * (32 * 33);
-  double* tscr = reinterpret_cast<double*>(smem + 4 * 32 * 33 * 4) + w * (16 * 17);
+  // ---- epilogue in the 32x32 accumulator layout: col = lane & 31,
+  // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+  double* im = img + w * (32 * 33);
   const bool mirror = tm != tn;
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi) {
+  for (int bj = 0; bj < 2; ++bj) {
+    const int cl = bj * 32 + l32;
+    const int64_t gj = bn + cl;
+    const int32_t nbj = n0_c[cl];
+    const double wbj = EXTRA ? wn_c[cl] : 0.0;
 #pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) iscr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + l32] = acc[bi][bj][r];
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t gi = bm + w * 32 + rl;
+      const int32_t D0 = n0_r[w * 32 + rl] + nbj - 2 * acc[bj][r];  // exact
+      double dist = w0 * double(D0);
+      if (EXTRA) dist += (wn_r[w * 32 + rl] + wbj) - 2.0 * xacc[bj][r];
+      dist = dist > 0.0 ? dist : 0.0;
+      double kv = exp(neg_gamma * dist);
+      if (gi == gj) kv = 1.0;
+      if (gi < n && gj < n) __builtin_nontemporal_store(kv, K + gi * ldk + gj);
+      if (mirror) im[l32 * 33 + rl] = kv;  // im[col][row]
+    }
+    if (mirror) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // Mirrored rows = this tile's columns: 16 lanes per row, one 16-byte chunk each, so every
+      // store instruction writes 4 whole 256-byte row segments.
+      const int chunk = lane & 15;
+      const int64_t gcol = bm + w * 32 + 2 * chunk;
 #pragma unroll
-      for (int si = 0; si < 2; ++si) {
-#pragma unroll
-        for (int sj = 0; sj < 2; ++sj) {
-          const int mi = 2 * bi + si, nj = 2 * bj + sj;
-          const int64_t gj = bn + wc * 64 + nj * 16 + lr;
-          const int32_t nbj = gj < n ? Nq[gj] : 0;
-          const double cbj = (CORR && gj < n) ? cN[gj] : 0.0;
-          double kv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t gi = bm + wr * 64 + mi * 16 + lg + 4 * r;
-            const int32_t iv = iscr[(si * 16 + lg + 4 * r) * 33 + sj * 16 + lr];
-            const int32_t nai = gi < n ? Nq[gi] : 0;
-            const int32_t D = nai + nbj - 2 * iv;  // exact: sum_j (q_aj - q_bj)^2
-            double dist = w0 * double(D);
-            if (CORR) dist += (gi < n ? cN[gi] : 0.0) + cbj - 2.0 * cacc[mi][nj][r];
-            dist = dist > 0.0 ? dist : 0.0;
-            kv[r] = exp(neg_gamma * dist);
-            if (gi == gj) kv[r] = 1.0;
-            if (gi < n && gj < n) K[gi * ldk + gj] = kv[r];
-          }
-          if (mirror) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) tscr[lr * 17 + lg + 4 * r] = kv[r];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int row = lane >> 2, c0 = (lane & 3) * 4;
-            const int64_t grow = bn + wc * 64 + nj * 16 + row;
-            const int64_t gcol = bm + wr * 64 + mi * 16 + c0;
-            if (grow < n) {
-              double* dst = K + grow * ldk + gcol;
-              const double* sp = tscr + row * 17 + c0;
-              if (gcol + 3 < n) {
-                *reinterpret_cast<double2*>(dst) = double2{sp[0], sp[1]};
-                *reinterpret_cast<double2*>(dst + 2) = double2{sp[2], sp[3]};
-              } else {
-                for (int q = 0; q < 4; ++q)
-                  if (gcol + q < n) dst[q] = sp[q];
-              }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          }
+      for (int it = 0; it < 8; ++it) {
+        const int mrow = it * 4 + (lane >> 4);
+        const int64_t grow = bn + bj * 32 + mrow;
+        const double* sp = im + mrow * 33 + 2 * chunk;
+        if (grow < n) {
+          double* dst = K + grow * ldk + gcol;
+          if (gcol + 1 < n)
+            __builtin_nontemporal_store(f64x2{sp[0], sp[1]}, reinterpret_cast<f64x2*>(dst));
+          else if (gcol < n)
+            dst[0] = sp[0];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -291,65 +244,69 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 
 }  // namespace
 
-// Host-side column plan (from the training min/max): which weight is the integer base w0, which
-// columns need the FP64 correction, and the permuted column order.
+// Host-side column plan (from the training min/max): the main group (most common range) and the
+// extra groups, each padded to a 32-column k-step, with per-column centring offsets.
 bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P) {
   P->ok = false;
   if (!mn || !mx || d <= 0) return false;
-  std::vector<double> r(static_cast<size_t>(d), 0.0), wgt(static_cast<size_t>(d), 0.0);
-  std::map<double, int> freq;
-  std::vector<char> live(static_cast<size_t>(d), 0);
+  std::map<double, std::vector<int32_t>> groups;  // range -> columns
+  std::vector<double> r(static_cast<size_t>(d), 0.0);
   for (int64_t j = 0; j < d; ++j) {
     const double rng = mx[j] - mn[j];
     if (!(rng >= 1e-12)) continue;  // constant column: scaled to 0 everywhere, contributes nothing
-    if (rng > 255.0 + 1e-9) return false;
-    r[j] = rng;
-    wgt[j] = 1.0 / (rng * rng);
-    live[j] = 1;
-    ++freq[wgt[j]];
+    if (rng > 255.0 + 1e-9 || rng != std::floor(rng)) return false;  // integer data has integer ranges
+    r[size_t(j)] = rng;
+    groups[rng].push_back(int32_t(j));
   }
-  if (freq.empty()) return false;
-  double w0 = 0.0;
-  int best = -1;
-  for (const auto& kv : freq)
-    if (kv.second > best) {
-      best = kv.second;
-      w0 = kv.first;
+  if (groups.empty()) return false;
+  const std::vector<int32_t>* main = nullptr;
+  double rmain = 0.0;
+  for (const auto& kv : groups)
+    if (!main || kv.second.size() > main->size()) {
+      main = &kv.second;
+      rmain = kv.first;
     }
-  std::vector<int32_t> corr, main;
-  for (int64_t j = 0; j < d; ++j) {
-    if (!live[j]) continue;
-    (wgt[j] == w0 ? main : corr).push_back(int32_t(j));
+  P->w0 = 1.0 / (rmain * rmain);
+  P->perm.clear();
+  P->step_w.clear();
+  auto pad_to = [&](size_t m) {
+    while (P->perm.size() % m) P->perm.push_back(-1);
+  };
+  for (const auto& kv : groups) {
+    if (kv.first == rmain) continue;
+    const double wg = 1.0 / (kv.first * kv.first);
+    for (int32_t j : kv.second) P->perm.push_back(j);
+    pad_to(32);
+    const size_t steps = P->perm.size() / 32;
+    P->step_w.resize(steps, 0.0);
+    P->step_w[steps - 1] = wg;  // flush at the group's last k-step
   }
-  const int kc = int((corr.size() + 15) / 16 * 16);
-  if (kc > kMaxCorr || main.empty()) return false;
-  const int kq = int((size_t(kc) + main.size() + QBK - 1) / QBK * QBK);
-  P->w0 = w0;
-  P->kc = kc;
-  P->kq = kq;
-  P->perm.assign(size_t(kq), -1);
-  P->rmul.assign(size_t(kq), 0.0);
-  P->delta.assign(size_t(std::max(kc, 1)), 0.0);
-  P->cen.assign(size_t(std::max(kc, 1)), 0.0);
-  for (size_t i = 0; i < corr.size(); ++i) {
-    P->perm[i] = corr[i];
-    P->rmul[i] = r[size_t(corr[i])];
-    P->delta[i] = wgt[size_t(corr[i])] - w0;
-    P->cen[i] = std::floor(r[size_t(corr[i])] * 0.5);
+  P->main0 = int(P->perm.size());
+  for (int32_t j : *main) P->perm.push_back(j);
+  pad_to(64);
+  P->kq = int(P->perm.size());
+  if (P->kq / 32 > kMaxSteps) return false;
+  P->rmul.assign(P->perm.size(), 0.0);
+  P->off.assign(P->perm.size(), 0.0);
+  P->wx.assign(P->perm.size(), 0.0);
+  for (size_t k = 0; k < P->perm.size(); ++k) {
+    const int32_t j = P->perm[k];
+    if (j < 0) continue;
+    const double rj = r[size_t(j)];
+    P->rmul[k] = rj;
+    P->off[k] = std::ceil(rj * 0.5);  // q - ceil(r/2) in [-128, 127] for r <= 255
+    if (int(k) < P->main0) P->wx[k] = 1.0 / (rj * rj);
   }
-  for (size_t i = 0; i < main.size(); ++i) {
-    P->perm[size_t(kc) + i] = main[i];
-    P->rmul[size_t(kc) + i] = r[size_t(main[i])];
-  }
-  P->n_corr = int(corr.size());
+  if (P->step_w.empty()) P->step_w.push_back(0.0);
+  P->n_groups = int(groups.size());
   P->ok = true;
   return true;
 }
 
 size_t igram_workspace(int64_t n, const QuantPlan& P) {
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  return al(size_t(n) * size_t(P.kq)) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(size_t(P.kq) * 4) +
-         al(size_t(P.kq) * 8) + 2 * al(P.delta.size() * 8) + 256;
+  return al(size_t(n) * size_t(P.kq)) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.perm.size() * 4) +
+         3 * al(P.perm.size() * 8) + al(P.step_w.size() * 8) + 256;
 }
 
 // Quantise the (scaled) rows and, if every value is an integer multiple of 1/r_j in [0, 255/r_j],
@@ -365,45 +322,45 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
   }
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   char* p = static_cast<char*>(ws);
-  int8_t* Q = reinterpret_cast<int8_t*>(p);
-  p += al(size_t(n) * size_t(P.kq));
-  int32_t* Nq = reinterpret_cast<int32_t*>(p);
-  p += al(size_t(n) * 4);
-  double* cN = reinterpret_cast<double*>(p);
-  p += al(size_t(n) * 8);
-  int32_t* perm = reinterpret_cast<int32_t*>(p);
-  p += al(size_t(P.kq) * 4);
-  double* rmul = reinterpret_cast<double*>(p);
-  p += al(size_t(P.kq) * 8);
-  double* delta = reinterpret_cast<double*>(p);
-  p += al(P.delta.size() * 8);
-  double* cen = reinterpret_cast<double*>(p);
-  p += al(P.cen.size() * 8);
-  unsigned* fail = reinterpret_cast<unsigned*>(p);
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
+  auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
+  auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
+  auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
+  auto* perm = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
+  auto* rmul = reinterpret_cast<double*>(take(P.rmul.size() * 8));
+  auto* off = reinterpret_cast<double*>(take(P.off.size() * 8));
+  auto* wx = reinterpret_cast<double*>(take(P.wx.size() * 8));
+  auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
+  auto* fail = reinterpret_cast<unsigned*>(take(4));
   SVMD_CHECK(hipMemcpyAsync(perm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemcpyAsync(rmul, P.rmul.data(), P.rmul.size() * 8, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemcpyAsync(delta, P.delta.data(), P.delta.size() * 8, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemcpyAsync(cen, P.cen.data(), P.cen.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(off, P.off.data(), P.off.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(wx, P.wx.data(), P.wx.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemsetAsync(fail, 0, 4, s));
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3(unsigned((n + 3) / 4)), dim3(256), 0, s, X, n, ld, perm, rmul,
-                     delta, cen, P.kc, P.kq, Q, Nq, cN, fail);
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3(unsigned((n + 3) / 4)), dim3(256), 0, s, X, n, ld, perm, rmul, off,
+                     wx, P.main0, P.kq, Q, N0, WN, fail);
   SVMD_LAUNCH_CHECK();
   unsigned hfail = 1;
   SVMD_CHECK(hipMemcpyAsync(&hfail, fail, 4, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipStreamSynchronize(s));
   if (hfail) return SVM_OK;  // not integer-valued: caller uses the FP64 path
   const int64_t tiles = (n + QBM - 1) / QBM;
-  const int64_t nwg = tiles * (tiles + 1) / 2;
+  const int64_t nwg = tiles * (tiles + 1);  // two 128x64 halves per upper-triangular 128x128 tile
   if (nwg > 0x7FFFFFFF) {
     set_error("igram: problem too large for one launch");
     return SVM_ERR_ARG;
   }
-  if (P.kc > 0)
-    hipLaunchKernelGGL((igram_tri_kernel<true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.kc, Nq, cN,
-                       delta, cen, P.w0, -gamma, K, ldk, tiles);
+  if (P.main0 > 0)
+    hipLaunchKernelGGL((igram_tri_kernel<true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, WN,
+                       stw, P.w0, -gamma, K, ldk, tiles);
   else
-    hipLaunchKernelGGL((igram_tri_kernel<false>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.kc, Nq, cN,
-                       delta, cen, P.w0, -gamma, K, ldk, tiles);
+    hipLaunchKernelGGL((igram_tri_kernel<false>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, WN,
+                       stw, P.w0, -gamma, K, ldk, tiles);
   SVMD_LAUNCH_CHECK();
   *used = true;
   return SVM_OK;

@@ -42,6 +42,7 @@ class SVC:
         self.device = device
         self.scale = scale
         self.zero_is_positive = zero_is_positive
+        self._sv_host = None
         self.gram = gram  # "auto" | "fp64" | "int" (device backend Gram path, see ops.device.train)
         self._dev = None  # device-side model state (torch tensors)
 
@@ -125,8 +126,19 @@ class SVC:
             self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
         else:
             self.scaler_ = None
-        self.support_vectors_ = self._dev["Xs"][:, :d].cpu().numpy()
+        self._sv_host = None  # scaled SV rows stay on the device; copied to the host on first access
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
+
+    @property
+    def support_vectors_(self) -> np.ndarray:
+        """Scaled support-vector rows (host copy, fetched lazily from the device model)."""
+        if self._sv_host is None and self._dev is not None:
+            self._sv_host = self._dev["Xs"][:, : self._dev["d"]].cpu().numpy()
+        return self._sv_host
+
+    @support_vectors_.setter
+    def support_vectors_(self, value) -> None:
+        self._sv_host = value
 
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
