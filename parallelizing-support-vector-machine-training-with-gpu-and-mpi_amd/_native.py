@@ -119,6 +119,8 @@ _HIP_SIGS = {
     "svmd_train_q": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32,
                                POINTER(SvmParams), POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming),
                                _P, _P, c_int64, c_int32, POINTER(c_int32)]),
+    "svmd_train_rows": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32, POINTER(SvmParams),
+                                  POINTER(SvmResult), _P, _P, c_int32, c_int64, POINTER(c_int32), _P, c_int64]),
     "svmd_rbf_gram_q": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int64, c_double, _P,
                                   c_int64, c_int32, POINTER(c_int32)]),
     "svmd_decision": (c_int32, [c_void_p, _P, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,

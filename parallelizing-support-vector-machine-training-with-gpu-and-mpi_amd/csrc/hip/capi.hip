@@ -1,4 +1,5 @@
 // C ABI of the device library: context management and the end-to-end device training path.
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -321,6 +322,40 @@ SVM_API int svmd_train_q(void* h, const double* X_d, const double* sqn_d, int64_
   SVMD_CTX(h);
   return train_impl(ctx, X_d, sqn_d, n, ld, kdim, y_d, alpha_d, warm, resolve(p), r, K_d, ldk, timing, mn_h, mx_h,
                     d, gram_mode, gram_used);
+}
+
+SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t d,
+                            const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
+                            const double* mn_h, const double* mx_h, int32_t gram_mode, int64_t cache_bytes,
+                            int32_t* gram_used, int64_t* trace_host, int64_t trace_cap) {
+  SVMD_CTX(h);
+  const svm_params q = resolve(p);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  QuantPlan P;
+  if (gram_mode != 1 && mn_h && mx_h) plan_quant(mn_h, mx_h, d, &P);
+  if (cache_bytes <= 0) {
+    // Default: room for 16384 rows (an SMO touches a few thousand distinct rows at MNIST scale),
+    // capped at 60% of the free HBM.
+    size_t fr = 0, tot = 0;
+    SVMD_CHECK(hipMemGetInfo(&fr, &tot));
+    cache_bytes = std::min<int64_t>(int64_t(double(fr) * 0.6), int64_t(16384) * ((n + 1) / 2 * 2) * 8);
+  }
+  int32_t used = 0;
+  rc = run_smo_rowcache(ctx, X_d, sqn_d, n, ld, d, P, y_d, alpha_d, warm, q, r, size_t(cache_bytes), trace_host,
+                        trace_cap, &used);
+  if (rc) return rc;
+  if (gram_mode == 2 && !used) {
+    set_error("integer kernel rows requested but the rows are not integer-valued in [0, 255] after scaling");
+    return SVM_ERR_ARG;
+  }
+  if (gram_used) *gram_used = used;
+  if (r) {
+    std::vector<double> a(static_cast<size_t>(n));
+    SVMD_CHECK(hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost));
+    r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
+  }
+  return ctx->end();
 }
 
 SVM_API int svmd_rbf_gram_q(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,

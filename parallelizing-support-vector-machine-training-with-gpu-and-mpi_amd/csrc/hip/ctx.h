@@ -108,8 +108,14 @@ struct QuantPlan {
 };
 bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P);
 size_t igram_workspace(int64_t n, const QuantPlan& P);
+size_t quantize_aux_bytes(const QuantPlan& P);
+int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const QuantPlan& P, void* aux, int8_t* Q,
+                  int32_t* N0, double* WN, bool* ok);
 int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const QuantPlan& P, double gamma, double* K,
               int64_t ldk, void* ws, bool* used);
+int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t d,
+                     const QuantPlan& P, const int32_t* y, double* alpha, int32_t warm, const svm_params& p,
+                     svm_result* r, size_t cache_bytes, int64_t* trace, int64_t trace_cap, int32_t* used_int);
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
 

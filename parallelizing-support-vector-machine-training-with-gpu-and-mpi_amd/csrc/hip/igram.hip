@@ -303,10 +303,51 @@ bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P) {
   return true;
 }
 
+
+// Quantise n (scaled) rows into Q (n x P.kq int8), N0, WN.  *ok = false when some value is not an
+// integer multiple of 1/r_j in [0, 255/r_j] (nothing usable written).  aux: device scratch of
+// quantize_aux_bytes(P) bytes for the column tables.  Synchronises the stream (reads the flag).
+size_t quantize_aux_bytes(const QuantPlan& P) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  return al(P.perm.size() * 4) + 3 * al(P.perm.size() * 8) + 256;
+}
+
+int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const QuantPlan& P, void* aux, int8_t* Q,
+                  int32_t* N0, double* WN, bool* ok) {
+  *ok = false;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(aux);
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
+  auto* perm = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
+  auto* rmul = reinterpret_cast<double*>(take(P.rmul.size() * 8));
+  auto* off = reinterpret_cast<double*>(take(P.off.size() * 8));
+  auto* wx = reinterpret_cast<double*>(take(P.wx.size() * 8));
+  auto* fail = reinterpret_cast<unsigned*>(take(4));
+  SVMD_CHECK(hipMemcpyAsync(perm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(rmul, P.rmul.data(), P.rmul.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(off, P.off.data(), P.off.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(wx, P.wx.data(), P.wx.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemsetAsync(fail, 0, 4, s));
+  if (n > 0) {
+    hipLaunchKernelGGL(quantize_rows_kernel, dim3(unsigned((n + 3) / 4)), dim3(256), 0, s, X, n, ld, perm, rmul, off,
+                       wx, P.main0, P.kq, Q, N0, WN, fail);
+    SVMD_LAUNCH_CHECK();
+  }
+  unsigned hfail = 1;
+  SVMD_CHECK(hipMemcpyAsync(&hfail, fail, 4, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  *ok = hfail == 0;
+  return SVM_OK;
+}
+
 size_t igram_workspace(int64_t n, const QuantPlan& P) {
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  return al(size_t(n) * size_t(P.kq)) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.perm.size() * 4) +
-         3 * al(P.perm.size() * 8) + al(P.step_w.size() * 8) + 256;
+  return al(size_t(n) * size_t(P.kq)) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
+         quantize_aux_bytes(P);
 }
 
 // Quantise the (scaled) rows and, if every value is an integer multiple of 1/r_j in [0, 255/r_j],
@@ -330,25 +371,12 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
   auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
   auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
   auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
-  auto* perm = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
-  auto* rmul = reinterpret_cast<double*>(take(P.rmul.size() * 8));
-  auto* off = reinterpret_cast<double*>(take(P.off.size() * 8));
-  auto* wx = reinterpret_cast<double*>(take(P.wx.size() * 8));
   auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
-  auto* fail = reinterpret_cast<unsigned*>(take(4));
-  SVMD_CHECK(hipMemcpyAsync(perm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemcpyAsync(rmul, P.rmul.data(), P.rmul.size() * 8, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemcpyAsync(off, P.off.data(), P.off.size() * 8, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemcpyAsync(wx, P.wx.data(), P.wx.size() * 8, hipMemcpyHostToDevice, s));
+  bool ok = false;
+  int rc = quantize_rows(s, X, n, ld, P, p, Q, N0, WN, &ok);
+  if (rc) return rc;
+  if (!ok) return SVM_OK;  // not integer-valued: caller uses the FP64 path
   SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
-  SVMD_CHECK(hipMemsetAsync(fail, 0, 4, s));
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3(unsigned((n + 3) / 4)), dim3(256), 0, s, X, n, ld, perm, rmul, off,
-                     wx, P.main0, P.kq, Q, N0, WN, fail);
-  SVMD_LAUNCH_CHECK();
-  unsigned hfail = 1;
-  SVMD_CHECK(hipMemcpyAsync(&hfail, fail, 4, hipMemcpyDeviceToHost, s));
-  SVMD_CHECK(hipStreamSynchronize(s));
-  if (hfail) return SVM_OK;  // not integer-valued: caller uses the FP64 path
   const int64_t tiles = (n + QBM - 1) / QBM;
   const int64_t nwg = tiles * (tiles + 1);  // two 128x64 halves per upper-triangular 128x128 tile
   if (nwg > 0x7FFFFFFF) {

@@ -84,6 +84,17 @@ SVM_API int svmd_train_q(void* ctx, const double* X_d, const double* sqn_d, int6
                          svmd_timing* timing, const double* mn_h, const double* mx_h, int64_t d,
                          int32_t gram_mode, int32_t* gram_used);
 
+// SMO for problems whose Gram does not fit in HBM: kernel rows are computed on demand into a 2-way
+// set-associative LRU row cache of cache_bytes (<= 0: 16384 rows, at most 60% of the free HBM), filled by a grid-wide
+// kernel inside the replayed iteration graph (rowcache.hip).  With integer-valued rows the values
+// are bit-identical to the exact-integer Gram (same trajectory as svmd_train_q); otherwise FP64
+// rows (sqn_d required).  d = feature count (FP64 rows use the first d columns).
+SVM_API int svmd_train_rows(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
+                            int64_t d, const int32_t* y_d, double* alpha_d, int32_t warm,
+                            const svm_params* p, svm_result* r, const double* mn_h, const double* mx_h,
+                            int32_t gram_mode, int64_t cache_bytes, int32_t* gram_used,
+                            int64_t* trace_host, int64_t trace_cap);
+
 // Symmetric RBF Gram of n preprocessed rows with the same path selection as svmd_train_q.
 SVM_API int svmd_rbf_gram_q(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,
                             int64_t kdim, const double* mn_h, const double* mx_h, int64_t d,

@@ -36,7 +36,7 @@ def _resolve_device(device: str) -> str:
 class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 scale: bool = True, zero_is_positive: bool = False, gram: str = "auto"):
+                 scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto"):
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else (os.cpu_count() or 1))
         self.device = device
@@ -44,6 +44,7 @@ class SVC:
         self.zero_is_positive = zero_is_positive
         self._sv_host = None
         self.gram = gram  # "auto" | "fp64" | "int" (device backend Gram path, see ops.device.train)
+        self.kcache = kcache  # "auto" | "full" (resident Gram) | "rows" (on-demand HBM row cache)
         self._dev = None  # device-side model state (torch tensors)
 
     # ------------------------------------------------------------------ fit
@@ -109,7 +110,8 @@ class SVC:
             alpha = torch.zeros(X.shape[0], dtype=torch.float64, device=device)
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
-        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram)
+        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
+                          kcache=self.kcache)
         a = alpha.cpu().numpy()
         self._finish(a, y, res)
         idx = torch.from_numpy(self.support_).to(device)

@@ -195,31 +195,60 @@ def _host_stats(mn, mx):
     return a, b, int(a.shape[0])
 
 
+def gram_fits(n: int, device, fraction: float = 0.8) -> bool:
+    """Does the full n x n float64 Gram fit in `fraction` of the free device memory?"""
+    free, _ = torch.cuda.mem_get_info(torch.device(device))
+    return n * ((n + 1) // 2 * 2) * 8 <= fraction * (free + torch.cuda.memory_reserved(torch.device(device)))
+
+
 def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams,
           warm: bool = False, K: Optional[torch.Tensor] = None, mn=None, mx=None,
-          gram: str = "auto") -> Tuple[SMOResult, dict]:
-    """RBF Gram (into K, allocated by torch if None) + SMO.  Returns (result, timing dict in ms).
+          gram: str = "auto", kcache: str = "auto", cache_bytes: int = 0,
+          trace_cap: int = 0) -> Tuple[SMOResult, dict]:
+    """RBF kernel + SMO.  Returns (result, timing dict in ms).
 
     ``mn``/``mx`` are the min/max the rows were scaled with; with them the exact-integer Gram
-    (int8 MFMA + FP64 correction, igram.hip) runs when the rows are integer-valued pixels
-    (``gram="auto"``), ``gram="fp64"`` forces the FP64 MFMA Gram, ``gram="int"`` requires the
-    integer path."""
+    (int8 MFMA, igram.hip) runs when the rows are integer-valued pixels (``gram="auto"``),
+    ``gram="fp64"`` forces the FP64 MFMA Gram, ``gram="int"`` requires the integer path.
+    ``kcache="full"`` stores the whole Gram (into K, allocated by torch if None); ``"rows"`` uses
+    the on-demand HBM row cache (rowcache.hip) for problems whose Gram does not fit; ``"auto"``
+    picks "full" when the Gram fits in 80% of the free memory."""
     _check_rows(X)
     n = X.shape[0]
-    if K is None:
-        K = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+    if kcache == "auto":
+        kcache = "full" if (K is not None or gram_fits(n, X.device)) else "rows"
     ctx = _ctx_for(X)
     r = N.SvmResult()
-    tm = N.SvmdTiming()
     p = params.to_struct()
     a, b, d = _host_stats(mn, mx)
     used = ctypes.c_int32(0)
+    trace = np.zeros((max(trace_cap, 0), 2), dtype=np.int64) if trace_cap > 0 else None
+    if kcache == "rows":
+        import time as _t
+
+        t0 = _t.perf_counter()
+        N.check(ctx.lib.svmd_train_rows(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
+                                        X.shape[1], N.ptr(y), N.ptr(alpha), int(warm), ctypes.byref(p),
+                                        ctypes.byref(r), N.ptr(a), N.ptr(b), GRAM_MODES[gram], int(cache_bytes),
+                                        ctypes.byref(used), N.ptr(trace), max(trace_cap, 0)), "svmd_train_rows")
+        tms = (_t.perf_counter() - t0) * 1e3
+        res = SMOResult.from_struct(r)
+        out = {"gram_ms": 0.0, "smo_ms": tms, "total_ms": tms, "kcache": "rows",
+               "gram_path": "int8-exact" if used.value else "fp64"}
+        if trace is not None:
+            out["trace"] = trace[: max(0, min(trace_cap, res.iterations - 1))]
+        return res, out
+    if trace_cap > 0:
+        raise ValueError("trace_cap is supported by the row-cache path only (use smo() on a Gram)")
+    if K is None:
+        K = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+    tm = N.SvmdTiming()
     N.check(ctx.lib.svmd_train_q(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
                                  X.shape[1], N.ptr(y), N.ptr(alpha), int(warm), ctypes.byref(p), ctypes.byref(r),
                                  N.ptr(K), K.stride(0), ctypes.byref(tm), N.ptr(a), N.ptr(b), d,
                                  GRAM_MODES[gram], ctypes.byref(used)), "svmd_train_q")
     return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
-                                      "gram_path": "int8-exact" if used.value else "fp64"}
+                                      "kcache": "full", "gram_path": "int8-exact" if used.value else "fp64"}
 
 
 def rbf_gram_sym(X: torch.Tensor, sqn: Optional[torch.Tensor], gamma: float, mn=None, mx=None,

@@ -364,3 +364,60 @@ def test_svc_int_gram_matches_fp64_gram(dev, mn_data):
     assert abs(a.b_ - c.b_) <= 1e-7 * max(1.0, abs(c.b_))
     assert abs(a.b_ - b.b_) <= 1e-7 * max(1.0, abs(c.b_))
     np.testing.assert_array_equal(a.predict(te.X), c.predict(te.X))
+
+
+# ---------------------------------------------------------------- on-demand row cache (rowcache.hip)
+@pytest.mark.parametrize("cache_rows", [6, 64, 100000])
+def test_row_cache_smo_bit_identical_to_full_gram(dev, D, cache_rows):
+    """Row-cache SMO (tiny / small / unbounded cache) follows the full-Gram trajectory bit for bit."""
+    n = 2500
+    tr = synthetic_mnist(n, seed=21)
+    Xd = D.upload_rows(tr.X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    yd = torch.from_numpy(tr.y).to(dev)
+    K, path = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    assert path == "int8-exact"
+    a_full = torch.zeros(n, dtype=torch.float64, device=dev)
+    r_full, t_full = D.smo(K, yd, a_full, SVMParams(), n=n, trace_cap=100000)
+    a_rows = torch.zeros(n, dtype=torch.float64, device=dev)
+    ldc = (n + 1) // 2 * 2
+    r_rows, info = D.train(Xd, sqn, yd, a_rows, SVMParams(), mn=mn, mx=mx, kcache="rows",
+                           cache_bytes=cache_rows * ldc * 8, trace_cap=100000)
+    assert info["kcache"] == "rows" and info["gram_path"] == "int8-exact"
+    assert r_rows.iterations == r_full.iterations and r_rows.b == r_full.b
+    assert r_rows.stop_reason == "converged"
+    np.testing.assert_array_equal(info["trace"], t_full)
+    np.testing.assert_array_equal(a_rows.cpu().numpy(), a_full.cpu().numpy())
+
+
+def test_row_cache_warm_start_bit_identical(dev, D):
+    n = 1800
+    tr = synthetic_mnist(n, seed=22)
+    Xd = D.upload_rows(tr.X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    yd = torch.from_numpy(tr.y).to(dev)
+    K, _ = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    a0 = torch.zeros(n, dtype=torch.float64, device=dev)
+    D.smo(K, yd, a0, SVMParams(), n=n)
+    a0 = a0 * 0.5
+    a_full = a0.clone()
+    r_full, _ = D.smo(K, yd, a_full, SVMParams(), n=n, warm=True)
+    a_rows = a0.clone()
+    r_rows, _ = D.train(Xd, sqn, yd, a_rows, SVMParams(), warm=True, mn=mn, mx=mx, kcache="rows",
+                        cache_bytes=40 * n * 8)
+    assert r_rows.iterations == r_full.iterations and r_rows.b == r_full.b
+    np.testing.assert_array_equal(a_rows.cpu().numpy(), a_full.cpu().numpy())
+
+
+def test_row_cache_fp64_rows_match_oracle(dev, D):
+    """Real-valued features: FP64 kernel rows computed on demand; same optimum as the CPU oracle."""
+    rng = np.random.default_rng(5)
+    n = 1200
+    X = rng.normal(size=(n, 30))
+    y = np.where(X[:, 0] + 0.5 * X[:, 1] ** 2 + 0.3 * rng.normal(size=n) > 0.4, 1, -1).astype(np.int32)
+    c = SVC(device="cpu", gamma=0.05, C=2.0).fit(X, y)
+    g = SVC(device="cuda:0", gamma=0.05, C=2.0, kcache="rows").fit(X, y)
+    assert g.timings_["kcache"] == "rows" and g.timings_["gram_path"] == "fp64"
+    assert g.stop_reason_ == "converged"
+    assert set(g.support_.tolist()) == set(c.support_.tolist())
+    assert abs(g.b_ - c.b_) <= 1e-6 * max(1.0, abs(c.b_))
