@@ -10,6 +10,7 @@
 //   --model-dir D    write final_sv_{ids,labels,alphas}.txt and final_b.txt
 //   --json F         machine-readable summary
 //   --gram auto|fp64|int  (svm_gpu) RBF Gram path: exact-integer int8 MFMA for pixel data, or FP64 MFMA
+//   --warmup W       (svm_gpu) untimed training runs first (steady-state timings)
 #pragma once
 #include <chrono>
 #include <cstdio>
@@ -33,6 +34,7 @@ struct Options {
   svm_params p{};
   bool quiet = false;
   int gram_mode = 0;  // svm_gpu: 0 auto (exact-integer int8 MFMA Gram for pixel data), 1 fp64, 2 int
+  int warmup = 0;     // svm_gpu: untimed training runs before the timed one
 };
 
 inline void usage(const char* prog) {
@@ -40,7 +42,7 @@ inline void usage(const char* prog) {
           "usage: %s [--dataset P | --train F --test F | --synthetic N[,M] [--seed S]] [--n-limit N]\n"
           "          [--C 10] [--gamma 0.00125] [--tau 1e-5] [--eps 1e-12] [--sv-tol 1e-8]\n"
           "          [--max-iter 100000] [--positive-label 1] [--threads T] [--model-dir D] [--json F]\n"
-          "          [--gram auto|fp64|int]\n",
+          "          [--gram auto|fp64|int] [--warmup W]\n",
           prog);
 }
 
@@ -78,6 +80,7 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
     else if (a == "--model-dir") o.model_dir = next("--model-dir");
     else if (a == "--json") o.json = next("--json");
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--warmup") o.warmup = atoi(next("--warmup"));
     else if (a == "--gram") {
       const std::string g = next("--gram");
       o.gram_mode = g == "fp64" ? 1 : g == "int" ? 2 : 0;

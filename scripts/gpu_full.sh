@@ -12,4 +12,4 @@ run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench1 600 python bench.py --steps 5 --warmup 1 || exit 1
 run bench_nccl1_cascade 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 1 --steps 2 --warmup 1 --cascade || exit 1
 run bench_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29522 bench.py --gpus 2 --steps 2 --warmup 1 --backend gloo || exit 1
-run sweep 600 python -m svm355 sweep --synthetic 60000,10000 || exit 1
+run sweep 600 python -m svm355 sweep --synthetic 60000,10000 --warmup 1 || exit 1
