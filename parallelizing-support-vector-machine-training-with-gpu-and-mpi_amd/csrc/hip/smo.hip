@@ -403,17 +403,53 @@ constexpr uint32_t kStampFrom = 200, kStampCount = 2000;
 
 // NT threads per workgroup (NW = NT/64 waves), E register-resident elements per thread:
 // element e of thread t is training point lo + t + NT*e of the workgroup's slice.
-template <int NT, int E, bool STAMP>
+// XLOCAL: all participating workgroups run on ONE XCD (read from HW_REG_XCC_ID at start; the grid
+// is over-provisioned and the first `glocal` workgroups that land on XCD 0 take ranks 0..glocal-1,
+// the rest exit).  Records are then exchanged through that XCD's shared L2 (plain stores, L1-bypassing
+// sc1 loads) instead of the device-wide fabric.  If XCD 0 receives fewer than glocal workgroups the
+// registration times out before any state is touched (err = 2) and the host falls back.
+template <int NT, int E, bool STAMP, bool XLOCAL = false>
 __global__ __launch_bounds__(NT) void smo_persistent_kernel(
     const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
     double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
     SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
-    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps) {
+    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps,
+    int glocal = 0) {
   constexpr int NW = NT / 64;
   __shared__ PersistShared sh;
   unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = 0, rt0 = 0;
   bool stamping = false;
-  const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int G = gridDim.x, g = blockIdx.x;
+  if constexpr (XLOCAL) {
+    __shared__ int s_rank;
+    unsigned* reg = err + 2;
+    if (t == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      int rank = -1;
+      if ((xcc & 0xF) == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rank = tk < unsigned(glocal) ? int(tk) : -1;
+      }
+      if (rank >= 0) {  // wait until every participant has registered (bounded)
+        int64_t spins = 0;
+        while (__hip_atomic_load(reg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unsigned(glocal)) {
+          if (++spins > spin_limit) {
+            __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rank = -2;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      s_rank = rank;
+    }
+    __syncthreads();
+    if (s_rank < 0) return;  // not a participant (or registration timed out: nothing touched)
+    G = glocal;
+    g = s_rank;
+  }
   const int64_t lo = int64_t(g) * slice, hi_end = std::min<int64_t>(n, lo + slice);
   const double c_hi = C - eps, c_lo = 0.0 + eps;
   const double inf = __builtin_inf();
@@ -435,7 +471,7 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
 
   for (uint32_t epoch = 1;; ++epoch) {
     if (STAMP) {
-      const bool on = blockIdx.x == 0 && threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
+      const bool on = g == 0 && threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
       if (on && !stamping) rt0 = __builtin_amdgcn_s_memrealtime();
       if (!on && stamping) sacc[7] = __builtin_amdgcn_s_memrealtime() - rt0;
       stamping = on;
@@ -517,8 +553,12 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
         pay = lane == 7 ? b.i : pay;
         pay = lane == 8 ? lo32(ba) : pay;
         pay = lane == 9 ? hi32(ba) : pay;
-        __hip_atomic_store(rec + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (XLOCAL)  // stays in the XCD's L2, where every participant's sc1 loads look
+          __hip_atomic_store(rec + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          __hip_atomic_store(rec + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
       PSTAMP(2);
       // ---- 3. lane L polls workgroup L's record until its ten tags equal the epoch
@@ -857,10 +897,22 @@ namespace {
 template <int NT, int E>
 int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
                         double* f, int64_t n, unsigned long long* slots, SmoState* st, double C, double eps,
-                        double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
+                        double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err, bool xlocal) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(err) + 8;
   const int64_t slice = int64_t(NT) * E;
   const char* sv = getenv("SVM355_PSMO_STAMP");
+  if (xlocal) {
+    // Over-provisioned grid: ~2*G workgroups per XCD under round-robin dispatch; G of XCD 0's join.
+    const int grid = 16 * G;
+    if (sv && atoi(sv))
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha, f,
+                         n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G);
+    else
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha,
+                         f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G);
+    SVMD_LAUNCH_CHECK();
+    return SVM_OK;
+  }
   if (sv && atoi(sv))
     hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true>), dim3(G), dim3(NT), 0, s, K, ldk, y, alpha, f, n, slice,
                        slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
@@ -875,12 +927,16 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
 // {1, 2, 4, 8, 16} (capped per NT) with G = ceil(n / (NT*E)) <= target workgroups (SVM355_PSMO_WG,
 // default 64; all co-resident, one sweep pass).
 constexpr int kDefaultNT = 512;
-constexpr int64_t kSingleDefaultMax = 4096;  // auto mode: single workgroup up to this n (tuned on MI355X)
+constexpr int kXcdMaxG = 32;              // workgroups of the XCD-local solver (one XCD has 32 CUs)
+constexpr int64_t kXcdDefaultMax = 24000;  // default n limit of the XCD-local solver (tuned on MI355X)
+constexpr int64_t kSingleDefaultMax = 2048;  // auto mode: single workgroup up to this n (tuned on MI355X)
 constexpr int kSingleDefaultNT = 512;
-int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out) {
+int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out, int gcap) {
   int target = 64;
   if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
-  int nt = kDefaultNT;
+  if (gcap > 0) target = std::min(target, gcap);
+  // Measured on MI355X: 256-thread workgroups win for the XCD-local solver up to ~16k points.
+  int nt = (gcap > 0 && n <= 16000) ? 256 : kDefaultNT;
   if (const char* v = getenv("SVM355_PSMO_NT")) nt = atoi(v);
   if (nt != 256 && nt != 512 && nt != 1024) nt = kDefaultNT;
   const int emax = nt == 256 ? 16 : nt == 512 ? 8 : 4;
@@ -899,11 +955,12 @@ int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out) {
 
 int launch_persistent(hipStream_t s, int NT, int E, int G, const double* K, int64_t ldk, const int32_t* y,
                       double* alpha, double* f, int64_t n, unsigned long long* slots, SmoState* st, double C,
-                      double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err) {
+                      double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err,
+                      bool xlocal) {
 #define SVM_PSMO_CASE(nt, e)                                                                                 \
   if (NT == nt && E == e)                                                                                    \
     return launch_persistent_e<nt, e>(s, G, K, ldk, y, alpha, f, n, slots, st, C, eps, tau, max_iter, trace, \
-                                      tcap, err);
+                                      tcap, err, xlocal);
   SVM_PSMO_CASE(256, 1) SVM_PSMO_CASE(256, 2) SVM_PSMO_CASE(256, 4) SVM_PSMO_CASE(256, 8) SVM_PSMO_CASE(256, 16)
   SVM_PSMO_CASE(512, 1) SVM_PSMO_CASE(512, 2) SVM_PSMO_CASE(512, 4) SVM_PSMO_CASE(512, 8)
   SVM_PSMO_CASE(1024, 1) SVM_PSMO_CASE(1024, 2) SVM_PSMO_CASE(1024, 4)
@@ -1034,18 +1091,29 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
     return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
   }
   const bool want_persistent = !(mode && strcmp(mode, "graph") == 0);
-  if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT)) {
+  // XCD-local exchange (all workgroups on one XCD, records through its L2): SVM355_PSMO_XCD=1/0
+  // forces it on/off; the default enables it up to kXcdDefaultMax points.
+  bool xlocal = n <= kXcdDefaultMax;
+  if (const char* v = getenv("SVM355_PSMO_XCD")) xlocal = atoi(v) != 0;
+  if (want_persistent && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT, xlocal ? kXcdMaxG : 0)) {
     auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
     auto* err = reinterpret_cast<unsigned*>(ws + off_slots + size_t(2) * kMaxG * kRecStride * 8);
-    SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));  // epochs restart at 1 every launch
-    const int lrc = launch_persistent(s, NT, E, G, K, ldk, y, alpha, f, n, slots, st, p.C, p.eps, p.tau, p.max_iter,
-                                      dtrace, tcap, err);
-    if (lrc) return lrc;
     SmoState* hst = static_cast<SmoState*>(ctx->pinned);
     unsigned herr = 0;
-    SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
-    SVMD_CHECK(hipMemcpyAsync(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    SVMD_CHECK(hipStreamSynchronize(s));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));  // epochs restart at 1 every launch
+      const int lrc = launch_persistent(s, NT, E, G, K, ldk, y, alpha, f, n, slots, st, p.C, p.eps, p.tau,
+                                        p.max_iter, dtrace, tcap, err, xlocal);
+      if (lrc) return lrc;
+      SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
+      SVMD_CHECK(hipMemcpyAsync(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+      SVMD_CHECK(hipStreamSynchronize(s));
+      if (!(xlocal && herr == 2)) break;
+      // XCD 0 did not receive enough workgroups: nothing was touched, run the device-wide kernel.
+      xlocal = false;
+      if (!persistent_grid(n, &G, &E, &NT, 0)) break;
+      herr = 0;
+    }
     if (herr) {
       set_error("svmd_smo: persistent solver timed out waiting for a workgroup record (G=%d)", G);
       return SVM_ERR_DEVICE;

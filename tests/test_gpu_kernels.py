@@ -174,6 +174,27 @@ def test_single_workgroup_smo_matches_persistent(dev, D, monkeypatch, n):
     np.testing.assert_array_equal(a1, a2)
 
 
+@pytest.mark.parametrize("n", [5000, 20000])
+def test_xcd_local_persistent_smo_matches_graph(dev, D, monkeypatch, n):
+    """XCD-local persistent solver (records through one XCD's L2) follows the graph-replay trajectory."""
+    tr = synthetic_mnist(n, seed=13)
+    Xd = D.upload_rows(tr.X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    K, _ = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    yd = torch.from_numpy(tr.y).to(dev)
+    out = {}
+    for mode, xcd in (("persistent", "1"), ("graph", "0")):
+        monkeypatch.setenv("SVM355_SMO", mode)
+        monkeypatch.setenv("SVM355_PSMO_XCD", xcd)
+        a = torch.zeros(n, dtype=torch.float64, device=dev)
+        r, trc = D.smo(K, yd, a, SVMParams(), n=n, trace_cap=200000)
+        out[mode] = (r, trc, a.cpu().numpy())
+    (r1, t1, a1), (r2, t2, a2) = out["persistent"], out["graph"]
+    assert r1.iterations == r2.iterations and r1.b == r2.b and r1.stop_reason == "converged"
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(a1, a2)
+
+
 def test_device_smo_warm_start_bit_identical(dev, D, mn_data):
     tr, _ = mn_data
     X = MinMaxScaler().fit_transform(tr.X[:700])
