@@ -30,7 +30,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", "-pthread", "-Wall", "-Wextra",
             "-Wno-unused-parameter", f"-I{CSRC / 'include'}"]
-HIPFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
+HIPFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", f"-I{ROCM / 'include'}",
             "-Wall", "-Wno-unused-parameter", "-Wno-unused-result", f"-I{CSRC / 'include'}",
             f"-I{CSRC / 'hip'}"]
 
@@ -98,7 +98,8 @@ def build_hip(force=False, verbose=False) -> Path:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _stale(out, objs):
         _run([cc, "-shared", f"--offload-arch={ARCH}", *objs, f"-L{LIB}", "-lsvm355_core",
-              "-Wl,-rpath,$ORIGIN", "-o", out], verbose)
+              f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}",
+              "-o", out], verbose)
     return out
 
 
@@ -123,6 +124,22 @@ def build_apps(force=False, verbose=False):
     return outs
 
 
+SANITIZE = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-O1", "-g"]
+
+
+def build_sanitized(force=False, verbose=False) -> Path:
+    """Host-only ASan+UBSan build of the CPU core and the serial CLI: one static
+    executable ``bin_asan/svm_serial`` (sanitizers on host code only; no GPU code involved)."""
+    out_dir = PKG / "bin_asan"
+    out_dir.mkdir(exist_ok=True)
+    exe = out_dir / "svm_serial"
+    srcs = [*CORE_SRCS, CSRC / "apps" / "svm_serial.cpp"]
+    if force or _stale(exe, [*srcs, *CORE_HDRS, CSRC / "apps" / "cli_common.h"]):
+        flags = [f for f in CXXFLAGS if f != "-O3"] + SANITIZE
+        _run(["g++", *flags, *srcs, "-o", exe], verbose)
+    return exe
+
+
 def build_all(force=False, verbose=False, hip=True):
     outs = [build_core(force, verbose)]
     if hip:
@@ -135,10 +152,13 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-hip", action="store_true", help="build only the CPU core")
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan host oracle (bin_asan/)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     for p in build_all(a.force, a.verbose, hip=not a.no_hip):
         print(p)
+    if a.sanitize:
+        print(build_sanitized(a.force, a.verbose))
 
 
 if __name__ == "__main__":

@@ -7,6 +7,7 @@
 
 #include "ctx.h"
 #include "svm355_device.h"
+#include "trace.h"
 
 using namespace svm355;
 
@@ -165,6 +166,7 @@ SVM_API int svmd_minmax(void* h, const double* X_d, int64_t n, int64_t d, int64_
 SVM_API int svmd_preprocess(void* h, double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
                             double* mx_d, double* sqn_d, int32_t use_given) {
   SVMD_CTX(h);
+  TraceRange tr("svm355:preprocess");
   if (n <= 0 || d <= 0 || ld < d || !mn_d || !mx_d) {
     set_error("svmd_preprocess: bad arguments");
     return SVM_ERR_ARG;
@@ -207,6 +209,7 @@ SVM_API int svmd_smo(void* h, const double* K_d, int64_t ldk, const int32_t* y_d
                      double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
                      int64_t* trace_host, int64_t trace_cap) {
   SVMD_CTX(h);
+  TraceRange tr("svm355:smo");
   const svm_params q = resolve(p);
   int rc = ctx->begin();
   if (rc) return rc;
@@ -232,6 +235,7 @@ static int gram_any(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int6
       if (!strcmp(g, "int")) mode = 2;
     }
   }
+  TraceRange tr("svm355:gram");
   bool used = false;
   if (mode != 1 && mn_h && mx_h) {
     QuantPlan P;
@@ -283,7 +287,10 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
     }
   }
   const double t_gram = ms_since(t0);
-  if (!rc) rc = run_smo(ctx, K, ldk, y_d, n, alpha_d, warm, q, r, nullptr, 0);
+  if (!rc) {
+    TraceRange ts("svm355:smo");
+    rc = run_smo(ctx, K, ldk, y_d, n, alpha_d, warm, q, r, nullptr, 0);
+  }
   if (!rc && r) {
     std::vector<double> a(static_cast<size_t>(n));
     const hipError_t e = hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost);
@@ -342,6 +349,7 @@ SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int
     cache_bytes = std::min<int64_t>(int64_t(double(fr) * 0.6), int64_t(16384) * ((n + 1) / 2 * 2) * 8);
   }
   int32_t used = 0;
+  TraceRange tr("svm355:smo:rowcache");
   rc = run_smo_rowcache(ctx, X_d, sqn_d, n, ld, d, P, y_d, alpha_d, warm, q, r, size_t(cache_bytes), trace_host,
                         trace_cap, &used);
   if (rc) return rc;
@@ -383,6 +391,7 @@ SVM_API int svmd_decision(void* h, const double* Xs_d, const double* ns_d, const
     SVMD_CHECK(hipStreamSynchronize(ctx->stream));
     return ctx->end();
   }
+  TraceRange tr("svm355:decision");
   // Cross-kernel block K(Xq, Xs) in row chunks of <= 512 MB scratch, then a deterministic GEMV.
   const int64_t ldk = (nsv + 1) / 2 * 2;
   int64_t rows = std::max<int64_t>(128, (int64_t(512) << 20) / (ldk * 8) / 128 * 128);
@@ -410,5 +419,8 @@ SVM_API int svmd_gather_rows(void* h, const double* src_d, int64_t ld, const int
   if (rc) return rc;
   return ctx->end();
 }
+
+SVM_API void svmd_trace_push(const char* name) { roctxRangePushA(name ? name : "svm355"); }
+SVM_API void svmd_trace_pop(void) { roctxRangePop(); }
 
 }  // extern "C"

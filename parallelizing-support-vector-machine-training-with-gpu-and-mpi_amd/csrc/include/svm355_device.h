@@ -110,6 +110,11 @@ SVM_API int svmd_decision(void* ctx, const double* Xs_d, const double* ns_d, con
 SVM_API int svmd_gather_rows(void* ctx, const double* src_d, int64_t ld, const int64_t* idx_d,
                              int64_t k, double* dst_d);
 
+// roctx ranges (rocprofv3 --marker-trace); the library already brackets preprocess / gram / smo /
+// decision, these let callers mark their own phases (e.g. cascade rounds and exchanges).
+SVM_API void svmd_trace_push(const char* name);
+SVM_API void svmd_trace_pop(void);
+
 #ifdef __cplusplus
 }
 #endif

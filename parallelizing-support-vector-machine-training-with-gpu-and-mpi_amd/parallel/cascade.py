@@ -35,6 +35,7 @@ import numpy as np
 import torch
 
 from ..utils.config import SVMParams
+from ..utils.trace import trace_range
 from .transport import Transport
 
 
@@ -249,8 +250,9 @@ class CascadeSVM:
         return x if x.device == self.device else x.to(self.device)
 
     def _bcast_set(self, S: Optional[SVSet], width: int) -> SVSet:
-        payload = self._c(S.pack()) if self.t.rank == 0 else None
-        return SVSet.unpack(self._d(self.t.broadcast_rows(payload, width + 3)), width)
+        with trace_range("cascade:bcast_svs"):
+            payload = self._c(S.pack()) if self.t.rank == 0 else None
+            return SVSet.unpack(self._d(self.t.broadcast_rows(payload, width + 3)), width)
 
     def _allreduce(self, x: torch.Tensor, op: str) -> torch.Tensor:
         y = self._c(x.clone())
@@ -271,7 +273,8 @@ class CascadeSVM:
         if len(S) == 0:
             return S, 0.0
         t0 = time.perf_counter()
-        alpha, res = be.solve(S.X, S.y, S.alpha)
+        with trace_range(f"cascade:solve:{tag}"):
+            alpha, res = be.solve(S.X, S.y, S.alpha)
         dt = (time.perf_counter() - t0) * 1e3
         res_log.append({"round": rnd, "rank": self.t.rank, "layer": tag, "n": len(S), "iterations": res.iterations,
                         "b": res.b, "stop": res.stop_reason, "ms": dt})
@@ -350,13 +353,16 @@ class CascadeSVM:
         converged = False
         while rnd < self.max_rounds and not converged:
             shown = rnd if self.topology == "star" else rnd + 1
+            round_range = trace_range(f"cascade:round{shown}")
+            round_range.__enter__()
             self.log(f"=== Round {shown} ===")
             # Broadcast the global SV set (count + one packed buffer) from rank 0.
             G = self._bcast_set(G, be.width)
             if self.topology == "star":
                 S = merge_unseen(be, G, part)
                 local, _ = self._solve(be, S, "local", shown, solves)
-                gathered = t.gather_rows(self._c(local.pack()), dst=0)
+                with trace_range("cascade:gather_svs"):
+                    gathered = t.gather_rows(self._c(local.pack()), dst=0)
                 same = 0
                 if t.rank == 0:
                     merged = local
@@ -389,9 +395,11 @@ class CascadeSVM:
                             b = b_local
                     if step < t.world:
                         if t.rank % (2 * step) == step:
-                            t.send_rows(self._c(cur.pack()), t.rank - step)
+                            with trace_range(f"cascade:send_svs:step{step}"):
+                                t.send_rows(self._c(cur.pack()), t.rank - step)
                         elif t.rank % (2 * step) == 0:
-                            recv = SVSet.unpack(self._d(t.recv_rows(t.rank + step, be.width + 3)), be.width)
+                            with trace_range(f"cascade:recv_svs:step{step}"):
+                                recv = SVSet.unpack(self._d(t.recv_rows(t.rank + step, be.width + 3)), be.width)
                     step *= 2
                 same = 0
                 if t.rank == 0:
@@ -410,6 +418,7 @@ class CascadeSVM:
                     self.log(f"[rank 0] Not converged yet. New SV count = {len(G)}")
                 self._checkpoint(rnd + 1, G, b, global_ids)
             converged = bool(t.broadcast_int(same))
+            round_range.__exit__(None, None, None)
             rnd += 1
 
         # Share the final model with every rank (the reference keeps it on rank 0 only).
