@@ -5,6 +5,7 @@ Capabilities of guaijiacc/Parallelizing-Support-Vector-Machine-Training-with-GPU
 re-designed for gfx950:
 
 * ``svm355.models.SVC``              RBF SVM, first-order SMO (reference semantics), CPU oracle or GPU
+* ``svm355.models.OneVsRestSVC``     all digits one-vs-rest over ONE resident Gram (10 SMO solves)
 * ``svm355.parallel.CascadeSVM``     classical tree and modified two-layer star Cascade SVM over
                                      ``torch.distributed`` (RCCL on GPUs, gloo on CPUs) or threads
 * ``svm355.utils.data``              CSV I/O, one-vs-rest labels, min-max scaling, synthetic MNIST
@@ -13,10 +14,11 @@ re-designed for gfx950:
 """
 from .utils.config import SVMParams
 from .utils.data import Dataset, MinMaxScaler, load_csv, one_vs_rest, synthetic_mnist, write_csv
+from .models.multiclass import OneVsRestSVC
 from .models.svc import SVC
 
 __all__ = ["SVMParams", "Dataset", "MinMaxScaler", "load_csv", "one_vs_rest", "synthetic_mnist", "write_csv",
-           "SVC", "CascadeSVM"]
+           "SVC", "OneVsRestSVC", "CascadeSVM"]
 __version__ = "0.1.0"
 
 

@@ -1,4 +1,5 @@
 """Estimators and model persistence."""
+from .multiclass import OneVsRestSVC
 from .svc import SVC
 
-__all__ = ["SVC"]
+__all__ = ["SVC", "OneVsRestSVC"]

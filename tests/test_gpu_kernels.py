@@ -442,3 +442,17 @@ def test_row_cache_fp64_rows_match_oracle(dev, D):
     assert g.stop_reason_ == "converged"
     assert set(g.support_.tolist()) == set(c.support_.tolist())
     assert abs(g.b_ - c.b_) <= 1e-6 * max(1.0, abs(c.b_))
+
+
+def test_ovr_multiclass_gpu_matches_cpu(dev):
+    from svm355 import OneVsRestSVC
+
+    tr = synthetic_mnist(1500, seed=31)
+    te = synthetic_mnist(400, seed=31, offset=1500)
+    g = OneVsRestSVC(device="cuda:0").fit(tr.X, tr.labels)
+    c = OneVsRestSVC(device="cpu").fit(tr.X, tr.labels)
+    assert g.timings_["gram_path"] == "int8-exact"
+    assert all(s == "converged" for s in g.stop_reasons_)
+    np.testing.assert_array_equal(g.support_, c.support_)
+    np.testing.assert_allclose(g.intercepts_b_, c.intercepts_b_, rtol=0, atol=1e-7)
+    np.testing.assert_array_equal(g.predict(te.X), c.predict(te.X))
