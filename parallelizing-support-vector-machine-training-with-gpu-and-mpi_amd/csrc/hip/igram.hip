@@ -37,14 +37,21 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int QBM = 128;        // tile rows / cols
-constexpr int QBK = 64;         // int8 columns per LDS stage (two 32-deep MFMA k-steps)
-constexpr int QLS = QBK + 16;   // LDS row stride in bytes (80: conflict-free ds_read_b128 rows)
+constexpr int QBM = 128;        // tile rows
 constexpr int QBN = 64;         // columns per workgroup (half of a 128x128 tile)
 constexpr int kMaxSteps = 128;  // 32-column k-steps (kq <= 4096)
-// staging tiles + step weights + row/col norms of the tile, then the per-wave transpose images
-constexpr int kStageBytes = (QBM + QBN) * QLS + kMaxSteps * 8 + (QBM + QBN) * 12;
-constexpr int kSmemBytes = kStageBytes + 4 * 32 * 33 * 8;
+constexpr int kColAlign = 128;  // kq is a multiple of this (host plan): 128-column LDS stages
+// LDS: per-tile tables (step weights, row/col norms) first, then a union of the int8 staging tiles
+// (k-loop) and the per-wave 32x33 f64 transpose images (epilogue).
+constexpr int kTableBytes = kMaxSteps * 8 + (QBM + QBN) * 12;
+constexpr int kImgBytes = 4 * 32 * 33 * 8;
+template <int BK>
+struct IgramCfg {
+  static constexpr int LS = BK + 16;  // row stride in bytes: conflict-free ds_read_b128 for BK = 64 / 128
+  static constexpr int kStage = (QBM + QBN) * LS;
+  static constexpr int kUnion = kStage > kImgBytes ? kStage : kImgBytes;
+  static constexpr int kSmem = kTableBytes + kUnion;
+};
 
 // ---- quantisation: one wave per row.  Writes the permuted centred int8 row q'_k = q_k - off_k,
 // N0 = sum_{main} q'^2 (exact int) and WN = sum_{extra} w_k q'^2; flags any value that is not an
@@ -94,23 +101,28 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
 
 // Upper-triangular 128x128 tiles of K = exp(-gamma * dist), each split into two 128x64 halves
 // (one workgroup each: 4 waves x 32 rows x 64 columns, 2 MFMA 32x32 tiles per wave), each
-// off-diagonal tile also stored transposed.  kq = int8 columns (multiple of QBK); columns
+// off-diagonal tile also stored transposed.  kq = int8 columns (multiple of BK); columns
 // [0, main0) are the extra groups (main0 a multiple of 32), step_w[s] = weight of k-step s's group
-// if s is the LAST k-step of its group (flush), else 0.
-template <bool EXTRA>
+// if s is the LAST k-step of its group (flush), else 0.  BK = int8 columns per LDS stage.
+template <bool EXTRA, int BK>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
     double* __restrict__ K, int64_t ldk, int64_t tiles) {
-  __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
-  char* As = smem;                                   // 128 rows x QLS
-  char* Bs = smem + QBM * QLS;                       // 64 rows x QLS
-  double* sw = reinterpret_cast<double*>(smem + (QBM + QBN) * QLS);
+  using Cfg = IgramCfg<BK>;
+  constexpr int QLS = Cfg::LS;
+  constexpr int CPR = BK / 16;            // 16-byte chunks per staged row
+  constexpr int RPP = 256 / CPR;          // rows per staging pass
+  constexpr int APASS = QBM / RPP, BPASS = QBN / RPP;
+  __shared__ __attribute__((aligned(16))) char smem[Cfg::kSmem];
+  double* sw = reinterpret_cast<double*>(smem);
   double* wn_r = sw + kMaxSteps;                     // WN of the tile's 128 rows / 64 cols
   double* wn_c = wn_r + QBM;
   int32_t* n0_r = reinterpret_cast<int32_t*>(wn_c + QBN);
   int32_t* n0_c = n0_r + QBM;
-  double* img = reinterpret_cast<double*>(smem + kStageBytes);  // per-wave 32x33 transpose images
+  char* As = smem + kTableBytes;                     // 128 rows x QLS
+  char* Bs = As + QBM * QLS;                         // 64 rows x QLS
+  double* img = reinterpret_cast<double*>(smem + kTableBytes);  // epilogue: per-wave 32x33 images
 
   const int64_t ntile = tiles * (tiles + 1) / 2;
   const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
@@ -132,15 +144,21 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     if (EXTRA) wn_c[t - QBM] = gj < n ? WN[gj] : 0.0;
   }
 
-  // Staging per 64-column stage: A 128 rows (2 x 16 B per thread), B 64 rows (1 x 16 B).
-  const int srow = t >> 2, scol = (t & 3) * 16;
-  const int64_t ra0 = bm + srow, ra1 = bm + srow + 64, rb0 = bn + srow;
+  // Staging per BK-column stage: thread t copies 16-byte chunk t % CPR of rows t / CPR + RPP * p.
+  const int srow = t / CPR, scol = (t % CPR) * 16;
   const i32x4 zero4 = {0, 0, 0, 0};
-  i32x4 ga[2], gb;
+  i32x4 ga[APASS], gb[BPASS];
   auto gload = [&](int k0) {
-    ga[0] = ra0 < n ? *reinterpret_cast<const i32x4*>(Q + ra0 * kq + k0 + scol) : zero4;
-    ga[1] = ra1 < n ? *reinterpret_cast<const i32x4*>(Q + ra1 * kq + k0 + scol) : zero4;
-    gb = rb0 < n ? *reinterpret_cast<const i32x4*>(Q + rb0 * kq + k0 + scol) : zero4;
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+      const int64_t r = bm + srow + RPP * p;
+      ga[p] = r < n ? *reinterpret_cast<const i32x4*>(Q + r * kq + k0 + scol) : zero4;
+    }
+#pragma unroll
+    for (int p = 0; p < BPASS; ++p) {
+      const int64_t r = bn + srow + RPP * p;
+      gb[p] = r < n ? *reinterpret_cast<const i32x4*>(Q + r * kq + k0 + scol) : zero4;
+    }
   };
   gload(0);
 
@@ -154,18 +172,19 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       if (EXTRA) xacc[j][r] = 0.0;
     }
 
-  for (int k0 = 0; k0 < kq; k0 += QBK) {
+  for (int k0 = 0; k0 < kq; k0 += BK) {
     __syncthreads();
-    *reinterpret_cast<i32x4*>(As + srow * QLS + scol) = ga[0];
-    *reinterpret_cast<i32x4*>(As + (srow + 64) * QLS + scol) = ga[1];
-    *reinterpret_cast<i32x4*>(Bs + srow * QLS + scol) = gb;
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) *reinterpret_cast<i32x4*>(As + (srow + RPP * p) * QLS + scol) = ga[p];
+#pragma unroll
+    for (int p = 0; p < BPASS; ++p) *reinterpret_cast<i32x4*>(Bs + (srow + RPP * p) * QLS + scol) = gb[p];
     __syncthreads();
-    if (k0 + QBK < kq) gload(k0 + QBK);
+    if (k0 + BK < kq) gload(k0 + BK);
 
     // A and B fragments use the same (lane, byte) -> k map, so the product is independent of the
     // hardware's k order inside a step.
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       const i32x4 a = *reinterpret_cast<const i32x4*>(As + (w * 32 + l32) * QLS + ks * 32 + 16 * h);
       i32x4 b[2];
 #pragma unroll
@@ -191,6 +210,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     }
   }
 
+  __syncthreads();  // staging tiles fully consumed: the union becomes the transpose images
   // ---- epilogue in the 32x32 accumulator layout: col = lane & 31,
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
   double* im = img + w * (32 * 33);
@@ -283,7 +303,7 @@ bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P) {
   }
   P->main0 = int(P->perm.size());
   for (int32_t j : *main) P->perm.push_back(j);
-  pad_to(64);
+  pad_to(kColAlign);
   P->kq = int(P->perm.size());
   if (P->kq / 32 > kMaxSteps) return false;
   P->rmul.assign(P->perm.size(), 0.0);
@@ -383,12 +403,17 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
     set_error("igram: problem too large for one launch");
     return SVM_ERR_ARG;
   }
-  if (P.main0 > 0)
-    hipLaunchKernelGGL((igram_tri_kernel<true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, WN,
-                       stw, P.w0, -gamma, K, ldk, tiles);
-  else
-    hipLaunchKernelGGL((igram_tri_kernel<false>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, WN,
-                       stw, P.w0, -gamma, K, ldk, tiles);
+  int bk = P.kq % 128 == 0 ? 128 : 64;  // fewer, deeper stages when the column count allows
+  if (const char* v = getenv("SVM355_IGRAM_BK")) bk = atoi(v) == 64 || P.kq % 128 ? 64 : 128;
+#define SVM_IGRAM(EX, B)                                                                                    \
+  hipLaunchKernelGGL((igram_tri_kernel<EX, B>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, \
+                     WN, stw, P.w0, -gamma, K, ldk, tiles)
+  if (P.main0 > 0) {
+    if (bk == 128) SVM_IGRAM(true, 128); else SVM_IGRAM(true, 64);
+  } else {
+    if (bk == 128) SVM_IGRAM(false, 128); else SVM_IGRAM(false, 64);
+  }
+#undef SVM_IGRAM
   SVMD_LAUNCH_CHECK();
   *used = true;
   return SVM_OK;
