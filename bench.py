@@ -8,8 +8,11 @@ One "step" is one complete training run on the fixed synthetic 60k x 784 MNIST-s
 shape and value domain because MNIST itself is not available offline):
 
 * N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's
-  GPU "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram
-  on MFMA f64, device SMO to convergence.
+  GPU "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram,
+  device SMO to convergence.
+* The pixel rows are held as uint8 (what MNIST is) and cross PCIe as bytes; they are widened to
+  FP64 on the device, where every value is exact, so all results are identical to an FP64 upload.
+  ``--input f64`` ships FP64 rows like the reference does (+~6 ms of H2D at 60k).
 * N > 1: one rank per GPU (torchrun, RCCL over xGMI), the modified two-layer Cascade SVM
   (mpi_svm_main2.cpp, default) or the classical tree (--topology tree).  Timed scope = a whole
   cascade fit of each rank's partition (H2D, global scaling, all rounds to convergence).
@@ -45,6 +48,8 @@ def main(argv=None):
     ap.add_argument("--m", type=int, default=10000, help="test rows for the parity fields")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
+    ap.add_argument("--input", choices=["u8", "f64"], default="u8",
+                    help="host row format: uint8 pixels (default) or FP64 as in the reference")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--cascade", action="store_true",
                     help="run the cascade path even on one rank (rehearsal of the RCCL code path)")
@@ -90,6 +95,9 @@ def main(argv=None):
         lo, hi = partition_bounds(a.n, world, rank)
         tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo)
     te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
+    if a.input == "u8":
+        tr = tr.compact()
+        te = te.compact() if te is not None else None
 
     def barrier_sync():
         torch.cuda.synchronize(dev)
@@ -162,6 +170,7 @@ def main(argv=None):
                 "seq_len": 784,
                 "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{world}",
             },
+            "host_rows": "uint8 (widened to fp64 on device)" if a.input == "u8" else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
             **extra,

@@ -107,6 +107,7 @@ _HIP_SIGS = {
     "svmd_set_stream": (c_int32, [c_void_p, c_void_p]),
     "svmd_synchronize": (c_int32, [c_void_p]),
     "svmd_upload_rows": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, c_int64]),
+    "svmd_upload_rows_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, c_int64]),
     "svmd_minmax": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P]),
     "svmd_preprocess":(c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int32]),
     "svmd_row_norms": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P]),

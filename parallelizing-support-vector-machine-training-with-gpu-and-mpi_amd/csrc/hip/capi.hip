@@ -146,6 +146,27 @@ SVM_API int svmd_upload_rows(void* h, const double* X_host, int64_t n, int64_t d
   return ctx->end();
 }
 
+SVM_API int svmd_upload_rows_u8(void* h, const uint8_t* X_host, int64_t n, int64_t d, double* X_d,
+                                int64_t ld) {
+  SVMD_CTX(h);
+  if (ld < d || n < 0 || d <= 0) {
+    set_error("svmd_upload_rows_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  if (n > 0) {
+    rc = ctx->ensure_ws(size_t(n) * size_t(d));
+    if (rc) return rc;
+    uint8_t* stage = static_cast<uint8_t*>(ctx->ws);
+    SVMD_CHECK(hipMemcpyAsync(stage, X_host, size_t(n) * size_t(d), hipMemcpyHostToDevice, ctx->stream));
+    rc = launch_widen_u8(ctx->stream, stage, n, d, ld, X_d);
+    if (rc) return rc;
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));  // the host buffer may be released on return
+  }
+  return ctx->end();
+}
+
 SVM_API int svmd_minmax(void* h, const double* X_d, int64_t n, int64_t d, int64_t ld, double* mn_d,
                         double* mx_d) {
   SVMD_CTX(h);

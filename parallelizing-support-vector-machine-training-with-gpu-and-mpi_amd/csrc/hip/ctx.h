@@ -82,6 +82,7 @@ struct DeviceCtx {
   }
 
 // Kernel launchers implemented in the .hip translation units (all enqueue on `s`).
+int launch_widen_u8(hipStream_t s, const uint8_t* src, int64_t n, int64_t d, int64_t ld, double* dst);
 int launch_minmax(hipStream_t s, const double* X, int64_t n, int64_t d, int64_t ld, double* mn,
                   double* mx, double* scratch, size_t scratch_doubles);
 int launch_scale_norms(hipStream_t s, double* X, int64_t n, int64_t d, int64_t ld, const double* mn,

@@ -93,7 +93,27 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const double* __restri
   }
 }
 
+// Compact uint8 pixel rows (n x d, contiguous) -> zero-padded FP64 rows (n x ld).  Pixel data are
+// uploaded as bytes (8x less PCIe traffic) and widened on the device; every value is exact in FP64.
+__global__ __launch_bounds__(256) void widen_u8_kernel(const uint8_t* __restrict__ src, int64_t n, int64_t d,
+                                                       int64_t ld, double* __restrict__ dst) {
+  const int64_t total = n * ld;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = i / ld, c = i - r * ld;
+    dst[i] = c < d ? double(src[r * d + c]) : 0.0;
+  }
+}
+
 }  // namespace
+
+int launch_widen_u8(hipStream_t s, const uint8_t* src, int64_t n, int64_t d, int64_t ld, double* dst) {
+  if (n <= 0) return SVM_OK;
+  const int64_t blocks = std::min<int64_t>((n * ld + 255) / 256, 256 * 64);
+  hipLaunchKernelGGL(widen_u8_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, src, n, d, ld, dst);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
 
 int launch_minmax(hipStream_t s, const double* X, int64_t n, int64_t d, int64_t ld, double* mn,
                   double* mx, double* scratch, size_t scratch_doubles) {

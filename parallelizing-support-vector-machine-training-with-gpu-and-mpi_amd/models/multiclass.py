@@ -40,11 +40,12 @@ class OneVsRestSVC:
 
     # ------------------------------------------------------------------ fit
     def fit(self, X: np.ndarray, labels: np.ndarray, classes: Optional[List[int]] = None) -> "OneVsRestSVC":
-        X = np.ascontiguousarray(X, dtype=np.float64)
+        cuda = self._dev() != "cpu"
+        X = np.ascontiguousarray(X, dtype=np.uint8 if (cuda and X.dtype == np.uint8) else np.float64)
         labels = np.asarray(labels)
         self.classes_ = np.array(sorted(set(labels.tolist())) if classes is None else classes)
         t0 = time.perf_counter()
-        if self._dev() == "cpu":
+        if not cuda:
             self._fit_cpu(X, labels)
         else:
             self._fit_cuda(X, labels)
@@ -122,7 +123,8 @@ class OneVsRestSVC:
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
         """(m, classes) decision values sum_k coef_kc K(x, sv_k) - b_c."""
-        X = np.ascontiguousarray(X, dtype=np.float64)
+        X = np.ascontiguousarray(X, dtype=np.uint8 if (self._dev_model is not None and X.dtype == np.uint8)
+                                 else np.float64)
         if self._dev_model is not None:
             import torch
 

@@ -99,7 +99,19 @@ def available() -> bool:
 
 
 def upload_rows(X: np.ndarray, device, ld: Optional[int] = None) -> torch.Tensor:
-    """Host (n, d) float64 -> device (n, ld) zero-padded rows (hipMemcpy2DAsync)."""
+    """Host (n, d) rows -> device (n, ld) zero-padded FP64 rows.
+
+    float rows go over PCIe as FP64 (hipMemcpy2DAsync).  uint8 rows (pixel data, see
+    ``utils.data.compact_pixels``) go over as bytes, 8x less H2D traffic, and are widened to FP64 on
+    the device (every value is exact), so everything downstream is identical."""
+    if isinstance(X, np.ndarray) and X.dtype == np.uint8:
+        X = np.ascontiguousarray(X)
+        n, d = X.shape
+        ld = padded_dim(d) if ld is None else ld
+        out = torch.empty((n, ld), dtype=torch.float64, device=device)
+        ctx = DeviceContext.get(out.device)
+        N.check(ctx.lib.svmd_upload_rows_u8(ctx.bind(), N.ptr(X), n, d, N.ptr(out), ld), "svmd_upload_rows_u8")
+        return out
     X = np.ascontiguousarray(X, dtype=np.float64)
     n, d = X.shape
     ld = padded_dim(d) if ld is None else ld

@@ -317,7 +317,8 @@ class CascadeSVM:
             ) -> CascadeResult:
         """Train on this rank's partition (raw, unscaled rows) with global sample ids."""
         t = self.t
-        X_part = np.ascontiguousarray(X_part, dtype=np.float64)
+        # uint8 pixel rows stay compact up to the device (widened to FP64 there)
+        X_part = np.ascontiguousarray(X_part, dtype=np.uint8 if X_part.dtype == np.uint8 else np.float64)
         d = t.broadcast_int(X_part.shape[1] if t.rank == 0 else 0)
         if X_part.shape[1] != d:
             raise ValueError(f"rank {t.rank}: partition has {X_part.shape[1]} features, rank 0 has {d}")
@@ -438,7 +439,8 @@ class CascadeSVM:
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
         r, be = self.result, self._be
-        Xq = be.to_rows(np.ascontiguousarray(X, dtype=np.float64), self.device)
+        X = np.ascontiguousarray(X, dtype=np.uint8 if X.dtype == np.uint8 else np.float64)
+        Xq = be.to_rows(X, self.device)
         be.scale_(Xq, r.mn, r.mx)
         if len(r.sv) == 0:
             return np.full(X.shape[0], -r.b)

@@ -22,7 +22,7 @@ MNIST_D = 784
 
 @dataclass
 class Dataset:
-    X: np.ndarray  # (n, d) float64, C-contiguous
+    X: np.ndarray  # (n, d) float64 (or uint8 after compact()), C-contiguous
     y: np.ndarray  # (n,) int32 in {+1, -1}
     labels: np.ndarray  # (n,) int32 raw labels
 
@@ -36,6 +36,26 @@ class Dataset:
 
     def subset(self, start: int, stop: int) -> "Dataset":
         return Dataset(self.X[start:stop], self.y[start:stop], self.labels[start:stop])
+
+    def compact(self) -> "Dataset":
+        """The same dataset with uint8 rows when every feature is an integer in [0, 255] (pixels)."""
+        Xc = compact_pixels(self.X)
+        return self if (Xc is None or Xc is self.X) else Dataset(Xc, self.y, self.labels)
+
+
+def compact_pixels(X: np.ndarray) -> Optional[np.ndarray]:
+    """uint8 copy of X if every value is an integer in [0, 255], else None.
+
+    MNIST-style pixel data are bytes; the reference holds them as FP64 (read_CSV, main3.cpp:13-54)
+    and ships 8 bytes per pixel to the GPU.  The device path accepts the uint8 rows directly and
+    widens them to FP64 on the device, where every value is exact, so results are unchanged."""
+    X = np.asarray(X)
+    if X.dtype == np.uint8:
+        return X
+    if X.size == 0:
+        return None
+    Xc = X.astype(np.uint8)
+    return Xc if np.array_equal(Xc, X) else None
 
 
 def one_vs_rest(labels: np.ndarray, positive_label: int = 1) -> np.ndarray:

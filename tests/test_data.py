@@ -3,7 +3,7 @@ labels, min-max scaling (main3.cpp:57-89) and the synthetic MNIST-shaped generat
 import numpy as np
 import pytest
 
-from svm355.utils.data import MinMaxScaler, load_csv, one_vs_rest, synthetic_mnist, write_csv
+from svm355.utils.data import MinMaxScaler, compact_pixels, load_csv, one_vs_rest, synthetic_mnist, write_csv
 
 
 def _write(path, text):
@@ -83,3 +83,13 @@ def test_synthetic_mnist_shape_and_determinism():
     assert 0.1 < np.mean(a.X > 0) < 0.35  # MNIST-like sparsity (~19% ink)
     c = synthetic_mnist(300, seed=4)
     assert not np.array_equal(a.X, c.X)
+
+
+def test_compact_pixels_exact_bytes_only():
+    a = synthetic_mnist(50, seed=5)
+    c = a.compact()
+    assert c.X.dtype == np.uint8 and np.array_equal(c.X.astype(np.float64), a.X)
+    assert c.y is a.y and compact_pixels(c.X) is c.X
+    for bad in (np.array([[0.5, 1.0]]), np.array([[256.0]]), np.array([[-1.0]]), np.array([[np.nan]])):
+        assert compact_pixels(bad) is None
+    assert c.compact() is c and (c.n, c.d) == (a.n, a.d)

@@ -387,6 +387,26 @@ def test_svc_int_gram_matches_fp64_gram(dev, mn_data):
     np.testing.assert_array_equal(a.predict(te.X), c.predict(te.X))
 
 
+def test_upload_u8_rows_equal_fp64_upload(dev, D, mn_data):
+    tr, _ = mn_data
+    Xc = tr.compact().X
+    assert Xc.dtype == np.uint8
+    for ld in (None, 800):
+        a = D.upload_rows(Xc[:517], dev, ld)
+        b = D.upload_rows(tr.X[:517], dev, ld)
+        assert a.dtype == torch.float64 and a.shape == b.shape == (517, ld or 784)
+        assert torch.equal(a, b)  # includes the zero padding columns
+
+
+def test_svc_u8_rows_bit_identical_to_fp64_rows(dev, mn_data):
+    tr, te = mn_data
+    a = SVC(device="cuda:0").fit(tr.compact().X, tr.y)
+    b = SVC(device="cuda:0").fit(tr.X, tr.y)
+    assert a.b_ == b.b_ and a.n_iter_ == b.n_iter_
+    np.testing.assert_array_equal(a.alpha_, b.alpha_)
+    np.testing.assert_array_equal(a.decision_function(te.compact().X), b.decision_function(te.X))
+
+
 # ---------------------------------------------------------------- on-demand row cache (rowcache.hip)
 @pytest.mark.parametrize("cache_rows", [6, 64, 100000])
 def test_row_cache_smo_bit_identical_to_full_gram(dev, D, cache_rows):
