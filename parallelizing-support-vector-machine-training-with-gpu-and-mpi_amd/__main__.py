@@ -110,7 +110,7 @@ def _cascade(argv) -> int:
 
     from .parallel.cascade import CascadeSVM, partition_bounds
     from .parallel.transport import TorchDistTransport
-    from .utils.config import SVMParams
+    from .utils.config import SVMParams, default_threads
     from .utils.data import load_csv, synthetic_mnist
 
     if "RANK" not in os.environ:  # single process: a world of one
@@ -147,7 +147,7 @@ def _cascade(argv) -> int:
         tr = full.subset(lo, hi)
         te = load_csv(a.test or f"{a.dataset}_test_data.csv", positive_label=a.positive_label) if rank == 0 else None
 
-    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=os.cpu_count() or 1)
+    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=default_threads())
     model = CascadeSVM(TorchDistTransport(comm_dev), params, topology=a.topology, max_rounds=a.max_rounds,
                        verbose=a.verbose, checkpoint_dir=a.checkpoint_dir, resume=a.resume, device=dev)
     t0 = time.perf_counter()

@@ -30,9 +30,9 @@ struct XRows {
   const double* X;
   int64_t d;
   double gamma;
-  void fill(int64_t i, double* row, int64_t n, int32_t nt) const {
+  void fill(int64_t i, double* row, int64_t n, WorkerTeam& team) const {
     const double* xi = X + i * d;
-    parallel_for(n, nt, [&](int64_t lo, int64_t hi) {
+    team.parallel_for(n, [&](int64_t lo, int64_t hi) {
       for (int64_t j = lo; j < hi; ++j) row[j] = rbf_direct(xi, X + j * d, d, gamma);
     });
   }
@@ -43,7 +43,7 @@ struct XRows {
 struct GramRows {
   const double* K;
   int64_t ldk;
-  void fill(int64_t i, double* row, int64_t n, int32_t) const {
+  void fill(int64_t i, double* row, int64_t n, WorkerTeam&) const {
     const double* src = K + i * ldk;
     for (int64_t j = 0; j < n; ++j) row[j] = src[j];
   }
@@ -63,7 +63,12 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
     return SVM_ERR_EMPTY;
   }
   const auto t0 = std::chrono::steady_clock::now();
-  const int32_t nt = std::max(1, p.n_threads);
+  // Worker count: the requested threads, but at least kMinPerThread elements each (the passes are
+  // a few ns per element; below that the fork/join of a pass costs more than it saves).  The
+  // result does not depend on the count (static chunks, serial tie-break in the merge).
+  constexpr int64_t kMinPerThread = 256;
+  const int32_t nt = int32_t(std::max<int64_t>(1, std::min<int64_t>(std::max(1, p.n_threads), n / kMinPerThread)));
+  WorkerTeam team(nt);
   const double C = p.C, eps = p.eps, tau = p.tau;
   std::vector<double> f(size_t(n), 0.0);
 
@@ -75,7 +80,7 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
     std::vector<int64_t> nz;
     for (int64_t j = 0; j < n; ++j)
       if (alpha[j] != 0.0) nz.push_back(j);
-    parallel_for(n, nt, [&](int64_t lo, int64_t hi) {
+    team.parallel_for(n, [&](int64_t lo, int64_t hi) {
       for (int64_t i = lo; i < hi; ++i) {
         double sum = 0.0;
         for (int64_t j : nz) sum += alpha[j] * y[j] * rows.k(j, i);
@@ -114,7 +119,7 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
     if (nchunks == 1) {
       scan(0);
     } else {
-      parallel_for(nchunks, nt, [&](int64_t lo, int64_t hi) {
+      team.parallel_for(nchunks, [&](int64_t lo, int64_t hi) {
         for (int64_t c = lo; c < hi; ++c) scan(c);
       });
     }
@@ -137,11 +142,11 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
     // --- kernel rows on change
     if (i_high != i_high_prev) {
       i_high_prev = i_high;
-      rows.fill(i_high, Kh.data(), n, nt);
+      rows.fill(i_high, Kh.data(), n, team);
     }
     if (i_low != i_low_prev) {
       i_low_prev = i_low;
-      rows.fill(i_low, Kl.data(), n, nt);
+      rows.fill(i_low, Kl.data(), n, team);
     }
     // --- two-variable update (main3.cpp:235-266)
     const int s = y[i_high] * y[i_low];
@@ -173,7 +178,7 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
     // --- f update (main3.cpp:268-275): f_i += (dh*y_h)*Kh_i + (dl*y_l)*Kl_i
     const double dh = ah_new - ah, dl = al_new - al;
     const int32_t yh = y[i_high], yl = y[i_low];
-    parallel_for(n, nt, [&](int64_t lo, int64_t hi) {
+    team.parallel_for(n, [&](int64_t lo, int64_t hi) {
       for (int64_t i = lo; i < hi; ++i) f[size_t(i)] += dh * yh * Kh[size_t(i)] + dl * yl * Kl[size_t(i)];
     });
     alpha[i_high] = ah_new;

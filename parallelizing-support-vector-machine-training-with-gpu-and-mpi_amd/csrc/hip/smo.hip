@@ -292,89 +292,86 @@ __device__ __forceinline__ double mk64(uint32_t lo, uint32_t hi) {
   return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
 }
 
-// ---- wave64 arg-reductions on (double value, uint32 index) without LDS traffic, in two cheap
-// stages: (1) the wave-wide min (max) VALUE with one v_min_f64 (v_max_f64) per step, (2) the
-// smallest index among the lanes holding that value with one v_min_u32 per step.  The result is
-// the lexicographic (value, lowest index) winner — the serial tie rule — identical in every lane
-// and independent of the schedule.  Steps: DPP quad_perm xor1, xor2, row_half_mirror (8),
-// row_mirror (16), then the gfx950 v_permlane16_swap / v_permlane32_swap for the 32/64-lane halves.
+// ---- wave64 arg-reductions on (double value, uint32 index) without LDS traffic, with the serial
+// tie rule (smallest value -- largest for MAX -- then the lowest index): the result is identical in
+// every lane and independent of the schedule.  Values are compared through an order-preserving
+// 64-bit key (sign-folded bits, -0 folded onto +0).  Its HIGH word is reduced with one DPP move and
+// one v_min/max_u32 per step (quad_perm xor1, xor2, row_half_mirror (8), row_mirror (16), then the
+// gfx950 v_permlane16_swap / v_permlane32_swap for the 32/64-lane halves); a ballot then finds the
+// lanes holding the winning high word -- almost always exactly one, whose value, index and lane are
+// read directly.  Only a tie of the high words costs a second 32-bit pass over the low words, and
+// only an exact value tie a third pass for the lowest index.  (Replaces a 64-bit value pass plus an
+// index pass on every reduction: about half the DPP steps.)
 struct VI {
   double v;
   uint32_t i;
+};
+struct VIL {  // winner: value, index and the lane that holds it (read its other fields with readlane)
+  double v;
+  uint32_t i;
+  int lane;
 };
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
   return uint32_t(__builtin_amdgcn_mov_dpp(int(x), CTRL, 0xF, 0xF, false));
 }
-template <int CTRL>
-__device__ __forceinline__ double dpp64(double x) {
-  return mk64(dpp32<CTRL>(lo32(x)), dpp32<CTRL>(hi32(x)));
+__device__ __forceinline__ uint64_t order_key(double v) {
+  const uint64_t u = uint64_t(__double_as_longlong(v == 0.0 ? 0.0 : v));
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 template <bool MIN>
-__device__ __forceinline__ double vbest(double a, double b) {
-  return MIN ? fmin(a, b) : fmax(a, b);
+__device__ __forceinline__ uint32_t pick32(uint32_t a, uint32_t b) {
+  return MIN ? min(a, b) : max(a, b);
 }
 // v_permlane{16,32}_swap with both operands = x returns, in every lane, its own value and its
 // partner's (in an order that depends on the row): combine both.
 template <bool MIN, bool S32>
-__device__ __forceinline__ double swap_best64(double x) {
-  const uint32_t l = lo32(x), h = hi32(x);
-  if constexpr (S32) {
-    const auto L = __builtin_amdgcn_permlane32_swap(l, l, false, false);
-    const auto H = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-    return vbest<MIN>(mk64(L[0], H[0]), mk64(L[1], H[1]));
-  } else {
-    const auto L = __builtin_amdgcn_permlane16_swap(l, l, false, false);
-    const auto H = __builtin_amdgcn_permlane16_swap(h, h, false, false);
-    return vbest<MIN>(mk64(L[0], H[0]), mk64(L[1], H[1]));
-  }
-}
-template <bool S32>
-__device__ __forceinline__ uint32_t swap_min32(uint32_t x) {
+__device__ __forceinline__ uint32_t swap_pick32(uint32_t x) {
   if constexpr (S32) {
     const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return min(r[0], r[1]);
+    return pick32<MIN>(r[0], r[1]);
   } else {
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return min(r[0], r[1]);
+    return pick32<MIN>(r[0], r[1]);
   }
 }
-// L = number of leading lanes that may hold candidates (1..64, power of two): reductions over the
-// NW per-wave results of one workgroup need only log2(NW) steps.
+// Butterfly over aligned groups of L lanes (L = 1..64, power of two); returns lane 0's group result
+// (wave-uniform).
+template <bool MIN, int L>
+__device__ __forceinline__ uint32_t group_pick32(uint32_t x) {
+  if (L > 1) x = pick32<MIN>(x, dpp32<0xB1>(x));   // quad_perm [1,0,3,2]
+  if (L > 2) x = pick32<MIN>(x, dpp32<0x4E>(x));   // quad_perm [2,3,0,1]
+  if (L > 4) x = pick32<MIN>(x, dpp32<0x141>(x));  // row_half_mirror
+  if (L > 8) x = pick32<MIN>(x, dpp32<0x140>(x));  // row_mirror
+  if (L > 16) x = swap_pick32<MIN, false>(x);
+  if (L > 32) x = swap_pick32<MIN, true>(x);
+  return uint32_t(__builtin_amdgcn_readfirstlane(int(x)));
+}
+__device__ __forceinline__ double read_lane64(double x, int src) {
+  return mk64(uint32_t(__builtin_amdgcn_readlane(int(lo32(x)), src)),
+              uint32_t(__builtin_amdgcn_readlane(int(hi32(x)), src)));
+}
+// Requires a full wave (EXEC = all 64 lanes).  L = number of leading lanes that may hold candidates;
+// lanes >= L must hold "no candidate" sentinels (value +inf for MIN / -inf for MAX, index
+// kSentinel), which never beat a real candidate.
 template <bool MIN, int L = 64>
-__device__ __forceinline__ VI wave_arg(VI a) {  // requires a full wave (EXEC = all 64 lanes)
-  double m = a.v;
-  if (L > 1) m = vbest<MIN>(m, dpp64<0xB1>(m));   // quad_perm [1,0,3,2]
-  if (L > 2) m = vbest<MIN>(m, dpp64<0x4E>(m));   // quad_perm [2,3,0,1]
-  if (L > 4) m = vbest<MIN>(m, dpp64<0x141>(m));  // row_half_mirror
-  if (L > 8) m = vbest<MIN>(m, dpp64<0x140>(m));  // row_mirror
-  if (L > 16) m = swap_best64<MIN, false>(m);
-  if (L > 32) m = swap_best64<MIN, true>(m);
-  uint32_t i = a.v == m ? a.i : 0xFFFFFFFFu;
-  if (L > 1) i = min(i, dpp32<0xB1>(i));
-  if (L > 2) i = min(i, dpp32<0x4E>(i));
-  if (L > 4) i = min(i, dpp32<0x141>(i));
-  if (L > 8) i = min(i, dpp32<0x140>(i));
-  if (L > 16) i = swap_min32<false>(i);
-  if (L > 32) i = swap_min32<true>(i);
-  return VI{m, i};
-}
-template <bool MIN>
-__device__ __forceinline__ bool better(VI a, VI b) {  // does b replace a?
-  return MIN ? (b.v < a.v || (b.v == a.v && b.i < a.i)) : (b.v > a.v || (b.v == a.v && b.i < a.i));
-}
-__device__ __forceinline__ double first_lane(double x) {
-  return mk64(uint32_t(__builtin_amdgcn_readfirstlane(int(lo32(x)))),
-              uint32_t(__builtin_amdgcn_readfirstlane(int(hi32(x)))));
-}
-// Value held by the lane whose index is the (uniform) winner index; 0 if it is the sentinel.
-__device__ __forceinline__ double winner_alpha(uint32_t my_i, double my_a, uint32_t win) {
-  const unsigned long long m = __ballot(my_i == win && win != kSentinel);
-  if (!m) return 0.0;
-  const int src = __builtin_ctzll(m);
-  return mk64(uint32_t(__builtin_amdgcn_readlane(int(lo32(my_a)), src)),
-              uint32_t(__builtin_amdgcn_readlane(int(hi32(my_a)), src)));
+__device__ __forceinline__ VIL wave_arg(VI a) {
+  const uint64_t k = order_key(a.v);
+  const uint32_t kh = uint32_t(k >> 32), kl = uint32_t(k);
+  const uint32_t bh = group_pick32<MIN, L>(kh);
+  unsigned long long tie = __ballot(kh == bh);
+  if (__popcll(tie) != 1) {  // equal high words: compare the low words
+    const uint32_t bl = group_pick32<MIN, L>(kh == bh ? kl : (MIN ? 0xFFFFFFFFu : 0u));
+    const bool same = kh == bh && kl == bl;
+    tie = __ballot(same);
+    if (__popcll(tie) != 1) {  // exact value tie (e.g. the first iteration, f = -y): lowest index
+      const uint32_t bi = group_pick32<true, L>(same ? a.i : 0xFFFFFFFFu);
+      tie = __ballot(same && a.i == bi);
+    }
+  }
+  const int src = __builtin_ctzll(tie);
+  return VIL{read_lane64(a.v, src), uint32_t(__builtin_amdgcn_readlane(int(a.i), src)), src};
 }
 
 struct PersistShared {
@@ -497,8 +494,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
       }
     }
     {
-      const VI wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
-      const double awmn = winner_alpha(mn.i, amn, wmn.i), awmx = winner_alpha(mx.i, amx, wmx.i);
+      const VIL wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
+      const double awmn = read_lane64(amn, wmn.lane), awmx = read_lane64(amx, wmx.lane);
       PSTAMP(0);
       if (lane == 0) {
         sh.wv[0][w] = wmn.v;
@@ -530,16 +527,13 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
           caa = sh.wa[0][lane];
           cba = sh.wa[1][lane];
         }
-        // Lanes 0..NW-1 hold the wave results: log2(NW) steps leave the merge in lane 0, which is
-        // broadcast (readfirstlane) so every publishing lane sees the same record.
-        a = wave_arg<true, NW>(ca);
-        b = wave_arg<false, NW>(cb);
-        aa = winner_alpha(ca.i, caa, a.i);
-        ba = winner_alpha(cb.i, cba, b.i);
-        a = VI{first_lane(a.v), uint32_t(__builtin_amdgcn_readfirstlane(int(a.i)))};
-        b = VI{first_lane(b.v), uint32_t(__builtin_amdgcn_readfirstlane(int(b.i)))};
-        aa = first_lane(aa);
-        ba = first_lane(ba);
+        // Lanes 0..NW-1 hold the wave results (sentinels above): log2(NW) steps; the winner is read
+        // from its lane, so every publishing lane sees the same record.
+        const VIL ra = wave_arg<true, NW>(ca), rb = wave_arg<false, NW>(cb);
+        a = VI{ra.v, ra.i};
+        b = VI{rb.v, rb.i};
+        aa = read_lane64(caa, ra.lane);
+        ba = read_lane64(cba, rb.lane);
       }
       if (lane < kGranules) {
         // Branch-free payload selection (no divergent switch).
@@ -592,8 +586,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
       }
       const bool any_to = __any(timed_out);
       PSTAMP(3);
-      const VI wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
-      const double awgm = winner_alpha(gm.i, agm, wgm.i), awgx = winner_alpha(gx.i, agx, wgx.i);
+      const VIL wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
+      const double awgm = read_lane64(agm, wgm.lane), awgx = read_lane64(agx, wgx.lane);
       if (lane == 0) {
         sh.gv[0] = wgm.v;
         sh.gi[0] = wgm.i;
@@ -774,8 +768,8 @@ __global__ __launch_bounds__(kSingleNT) void smo_single_kernel(
       }
     }
     {
-      const VI wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
-      const double awmn = winner_alpha(mn.i, amn, wmn.i), awmx = winner_alpha(mx.i, amx, wmx.i);
+      const VIL wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
+      const double awmn = read_lane64(amn, wmn.lane), awmx = read_lane64(amx, wmx.lane);
       PSTAMP(0);
       if (lane == 0) {
         sh.wv[par][0][w] = wmn.v;
@@ -796,17 +790,16 @@ __global__ __launch_bounds__(kSingleNT) void smo_single_kernel(
       caa = sh.wa[par][0][lane];
       cba = sh.wa[par][1][lane];
     }
-    const VI ga = wave_arg<true, NW>(ca), gb = wave_arg<false, NW>(cb);
-    const double aga = first_lane(winner_alpha(ca.i, caa, ga.i)), agb = first_lane(winner_alpha(cb.i, cba, gb.i));
-    const uint32_t uih = uint32_t(__builtin_amdgcn_readfirstlane(int(ga.i)));
-    const uint32_t uil = uint32_t(__builtin_amdgcn_readfirstlane(int(gb.i)));
+    const VIL ga = wave_arg<true, NW>(ca), gb = wave_arg<false, NW>(cb);
+    const double aga = read_lane64(caa, ga.lane), agb = read_lane64(cba, gb.lane);
+    const uint32_t uih = ga.i, uil = gb.i;
     if (uih == kSentinel || uil == kSentinel) {
       stop = SVM_STOP_NO_CANDIDATE;
       break;
     }
     PSTAMP(2);
     const int64_t ih = uih, il = uil;
-    const double bh = first_lane(ga.v), bl = first_lane(gb.v);
+    const double bh = ga.v, bl = gb.v;
     b_high = bh;
     b_low = bl;
     if (bl <= bh + 2.0 * tau) {

@@ -16,7 +16,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from ..utils.config import SVMParams
+from ..utils.config import SVMParams, default_threads
 from ..utils.data import MinMaxScaler
 
 
@@ -24,10 +24,8 @@ class OneVsRestSVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  gram: str = "auto"):
-        import os
-
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
-                                n_threads=n_threads if n_threads > 0 else (os.cpu_count() or 1))
+                                n_threads=n_threads if n_threads > 0 else default_threads())
         self.device = device
         self.gram = gram
 

@@ -21,7 +21,7 @@ from typing import Optional
 
 import numpy as np
 
-from ..utils.config import SVMParams
+from ..utils.config import SVMParams, default_threads
 from ..utils.data import MinMaxScaler
 
 
@@ -42,7 +42,7 @@ class SVC:
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto"):
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
-                                n_threads=n_threads if n_threads > 0 else (os.cpu_count() or 1))
+                                n_threads=n_threads if n_threads > 0 else default_threads())
         self.device = device
         self.scale = scale
         self.zero_is_positive = zero_is_positive

@@ -13,9 +13,22 @@
 from __future__ import annotations
 
 import dataclasses
+import os
 from dataclasses import dataclass
 
 from .._native import params_struct
+
+
+def default_threads(cap: int = 16) -> int:
+    """CPU workers for the native oracle: the CPUs this process may run on, capped at ``cap``.
+
+    ``os.cpu_count()`` reports the whole machine (hundreds of CPUs on a GPU node) even when the
+    process is confined to a few; the O(n) SMO passes gain nothing past ~16 workers."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))
 
 
 @dataclass
