@@ -25,6 +25,7 @@ Accuracy, #SV, b and iterations of the last run are reported alongside (parity f
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -34,8 +35,12 @@ import numpy as np
 
 REF_GPU_S = 58.570  # GPU SMO training time, 60k
 REF_SERIAL_S = 3285.662  # serial SMO training time, 60k
+REF_GPU_PRED_S = 38.297  # GPU prediction time, 60k train / 10k test
 REF_STAR_S = {4: 886.733, 8: 649.773, 16: 440.705, 32: 333.696, 64: 301.263}
 REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
+# A rank that dies leaves the others blocked in a collective: RCCL's watchdog aborts the job after
+# this long instead of hanging it (the reference has no failure handling).
+COLLECTIVE_TIMEOUT = datetime.timedelta(minutes=10)
 METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
 
 
@@ -83,9 +88,9 @@ def main(argv=None):
         import torch.distributed as dist
 
         if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=COLLECTIVE_TIMEOUT)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=COLLECTIVE_TIMEOUT)
     comm_dev = dev if a.backend == "nccl" else torch.device("cpu")
     params = SVMParams()
 
@@ -126,10 +131,13 @@ def main(argv=None):
         step()
     barrier_sync()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(a.steps):
         step()
+        marks.append(time.perf_counter())  # host-side step boundaries (diagnostic only)
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    step_ms = [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + marks[:-1], marks)]
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -139,9 +147,18 @@ def main(argv=None):
     value = ms / 1e3
     extra = {}
     if not use_cascade:
+        # Prediction on the 10k test rows (outside the timed region): H2D, scaling with the training
+        # statistics, MFMA cross-kernel against the SVs, decision values back to the host.  The
+        # reference's GPU "prediction" (38.3 s at 60k) also parses the test CSV.
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        model.decision_function(te.X)
+        torch.cuda.synchronize(dev)
+        pred_ms = (time.perf_counter() - tp) * 1e3
         acc = model.score(te.X, te.y)
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
-                 "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_}
+                 "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
+                 "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S}
     else:
         acc = model.score(te.X, te.y) if rank == 0 else None
         s = model.summary()
@@ -173,6 +190,7 @@ def main(argv=None):
             "host_rows": "uint8 (widened to fp64 on device)" if a.input == "u8" else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
+            "step_ms": step_ms,
             **extra,
         }
         s = json.dumps(line)

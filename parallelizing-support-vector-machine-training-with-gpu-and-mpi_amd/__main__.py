@@ -17,6 +17,7 @@ The native CLIs take the options listed in ``csrc/apps/cli_common.h`` (``--datas
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import subprocess
@@ -25,6 +26,9 @@ import time
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
+# A rank that dies leaves the others blocked in a collective: the process group's watchdog aborts
+# the job after this long instead of hanging it.
+COLLECTIVE_TIMEOUT = datetime.timedelta(minutes=10)
 
 
 def _native(name: str, args) -> int:
@@ -126,9 +130,9 @@ def _cascade(argv) -> int:
         dev = torch.device("cpu")
     backend = a.backend if use_gpu else "gloo"
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, timeout=COLLECTIVE_TIMEOUT)
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=COLLECTIVE_TIMEOUT)
     comm_dev = dev if backend == "nccl" else torch.device("cpu")
 
     if a.synthetic:
