@@ -10,6 +10,7 @@ Targets
                                  and the device-resident SMO driver (hipGraph replay)
   bin/svm_serial          g++   main3.cpp-equivalent CLI
   bin/svm_gpu             hipcc gpu_svm_main3/4-equivalent CLI (--n-limit sweep)
+  bin/svm_cascade         hipcc mpi_svm_main2/3-equivalent: one process, a thread per GPU, RCCL
 """
 from __future__ import annotations
 
@@ -125,6 +126,17 @@ def build_apps(force=False, verbose=False):
         _run(["g++", *CXXFLAGS, src, f"-L{LIB}", "-lsvm355_hip", "-lsvm355_core", rpath,
               "-o", gpu], verbose)
     outs.append(gpu)
+    # Native cascade (one process, one thread per GPU, RCCL): hipcc for the HIP runtime + RCCL headers.
+    casc = BIN / "svm_cascade"
+    srcs = [CSRC / "apps" / "svm_cascade.cpp", *sorted((CSRC / "cascade").glob("*.cpp"))]
+    deps = [*srcs, *sorted((CSRC / "cascade").glob("*.h")), LIB / "libsvm355_core.so", LIB / "libsvm355_hip.so",
+            *HIP_HDRS, CSRC / "apps" / "cli_common.h"]
+    if force or _stale(casc, deps):
+        _run([hipcc(), "-std=c++17", "-O2", "-fPIC", "-pthread", "-Wall", "-Wno-unused-parameter",
+              f"-I{CSRC / 'include'}", f"-I{CSRC / 'cascade'}", f"-I{ROCM / 'include'}", *srcs, f"-L{LIB}",
+              "-lsvm355_hip", "-lsvm355_core", f"-L{ROCM / 'lib'}", "-lrccl", rpath, f"-Wl,-rpath,{ROCM / 'lib'}",
+              "-o", casc], verbose)
+    outs.append(casc)
     return outs
 
 

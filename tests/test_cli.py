@@ -52,3 +52,13 @@ def test_cli_cascade_two_ranks_gloo(tmp_path):
     assert "[rank 0] Running modified CascadeSVM with 2 processes" in out
     s = json.loads(js.read_text())
     assert s["converged"] and s["world"] == 2
+
+
+def test_native_cascade_rejects_non_power_of_two_tree():
+    """bin/svm_cascade aborts a classical cascade on a non-power-of-2 world (mpi_svm_main3.cpp:420-428)
+    before touching a GPU, so this runs on a CPU-only host too."""
+    exe = Path(__file__).resolve().parents[1] / "svm355" / "bin" / "svm_cascade"
+    r = subprocess.run([str(exe), "--topology", "tree", "--gpus", "3", "--synthetic", "100,10"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
+    assert "power-of-2" in r.stderr
