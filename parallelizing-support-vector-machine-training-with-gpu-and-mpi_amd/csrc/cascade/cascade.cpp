@@ -30,6 +30,14 @@ namespace {
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// roctx range through the device library (visible with rocprofv3 --marker-trace), SURVEY §5.1.
+struct Trace {
+  explicit Trace(const std::string& name) { svmd_trace_push(name.c_str()); }
+  ~Trace() { svmd_trace_pop(); }
+  Trace(const Trace&) = delete;
+  Trace& operator=(const Trace&) = delete;
+};
+
 using Clock = std::chrono::steady_clock;
 double ms_between(Clock::time_point a, Clock::time_point b) {
   return std::chrono::duration<double, std::milli>(b - a).count();
@@ -245,6 +253,7 @@ class Rank {
 
   // ---- exchanges
   SvSet bcast_set(const SvSet& G) {  // G meaningful on rank 0
+    Trace tr("cascade:bcast_svs");
     const int64_t k = t_.bcast_i64(t_.rank() == 0 ? G.k : 0, 0);
     if (t_.rank() == 0)
       pack_into(G, pack_, k);
@@ -255,6 +264,7 @@ class Rank {
   }
   // Star: local SV sets to rank 0 (counts all-gathered, max-count-padded gather, source order).
   std::vector<SvSet> gather_sets(const SvSet& local) {
+    Trace tr("cascade:gather_svs");
     const std::vector<int64_t> counts = t_.allgather_i64(local.k);
     const int64_t kmax = *std::max_element(counts.begin(), counts.end());
     std::vector<SvSet> out;
@@ -274,6 +284,7 @@ class Rank {
   }
   // Tree: count, then one packed buffer (M3 :689-716).
   void send_set(const SvSet& S, int peer) {
+    Trace tr("cascade:send_svs");
     cnt_.ensure(8);
     SVMC(svmd_memcpy_h2d(ctx_, cnt_.p, &S.k, 8));
     t_.send(cnt_.p, 8, peer);
@@ -283,6 +294,7 @@ class Rank {
     }
   }
   SvSet recv_set(int peer) {
+    Trace tr("cascade:recv_svs");
     cnt_.ensure(8);
     t_.recv(cnt_.p, 8, peer);
     int64_t k = 0;
@@ -295,6 +307,7 @@ class Rank {
   // Warm-start SMO on S (SMO_train(..., init=false)); returns (its SVs with alpha > sv_tol, b).
   std::pair<SvSet, double> solve(const SvSet& S) {
     if (S.k == 0) return {empty(), 0.0};
+    Trace tr("cascade:solve");
     const int64_t k = S.k, ldk = (k + 1) / 2 * 2;
     sqn_.ensure(k * 8);
     yd_.ensure(k * 4);
@@ -368,6 +381,7 @@ CascadeOutput run_cascade(Transport& t, void* ctx, const double* X_host, const i
   bool converged = false;
   while (rnd < cfg.max_rounds && !converged) {
     const int shown = cfg.tree ? rnd + 1 : rnd;
+    Trace round_range("cascade:round" + std::to_string(shown));
     if (log) {
       printf("=== Round %d ===\n", shown);
       fflush(stdout);
