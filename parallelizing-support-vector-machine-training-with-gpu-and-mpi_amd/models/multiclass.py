@@ -3,7 +3,9 @@
 The reference trains a single one-vs-rest classifier (digit "1" vs the rest, main3.cpp:49-52).
 Training all ten digits the same way is ten SMO solves on the same rows: the RBF Gram does not
 depend on the labels, so on the device it is computed once (exact-integer int8 MFMA path for
-pixel data), kept resident in HBM and reused by every class's SMO.  Prediction evaluates one
+pixel data), kept resident in HBM and reused by every class's SMO.  The solves are independent and
+each persistent SMO kernel is latency-bound on at most 64 workgroups, so ``concurrent_solves`` of
+them run at once on separate streams and fill the 256 CUs.  Prediction evaluates one
 cross-kernel block against the union of all classes' support vectors and applies every class's
 dual coefficients with one FP64 matrix product; the predicted label is the arg-max decision value.
 
@@ -23,7 +25,10 @@ from ..utils.data import MinMaxScaler
 class OneVsRestSVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 gram: str = "auto"):
+                 gram: str = "auto", concurrent_solves: int = 8):
+        """``concurrent_solves``: class solves run at once on the GPU (each persistent SMO occupies at
+        most 64 of the MI355X's 256 CUs; results do not depend on it)."""
+        self.concurrent_solves = concurrent_solves
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else default_threads())
         self.device = device
@@ -88,13 +93,30 @@ class OneVsRestSVC:
         t2 = time.perf_counter()
         n = X.shape[0]
         alphas = torch.zeros((len(self.classes_), n), dtype=torch.float64, device=device)
-        bs, iters, stops = [], [], []
         ys = self._ys(labels)
-        for k, y in enumerate(ys):
-            r, _ = D.smo(K, torch.from_numpy(y).to(device), alphas[k], self.params, n=n)
-            bs.append(r.b)
-            iters.append(r.iterations)
-            stops.append(r.stop_reason)
+        ys_d = [torch.from_numpy(y).to(device) for y in ys]
+        torch.cuda.synchronize(device)
+
+        def solve(k):
+            # Each class solve on its own stream (and, per host thread, its own device context):
+            # the SMO is latency-bound on <= 64 workgroups, so several classes share the 256 CUs.
+            s = torch.cuda.Stream(device)
+            with torch.cuda.stream(s):
+                r, _ = D.smo(K, ys_d[k], alphas[k], self.params, n=n)
+            s.synchronize()
+            return r
+
+        workers = max(1, min(self.concurrent_solves, len(ys)))
+        if workers > 1:
+            from concurrent.futures import ThreadPoolExecutor
+
+            with ThreadPoolExecutor(max_workers=workers) as ex:  # the native calls release the GIL
+                results = list(ex.map(solve, range(len(ys))))
+        else:
+            results = [solve(k) for k in range(len(ys))]
+        bs = [r.b for r in results]
+        iters = [r.iterations for r in results]
+        stops = [r.stop_reason for r in results]
         torch.cuda.synchronize(device)
         t3 = time.perf_counter()
         del K
