@@ -386,6 +386,11 @@ struct PersistShared {
 // s_memtime deltas per phase over epochs [kStampFrom, kStampFrom + kStampCount) into stamps[0..7]
 // (stamps[7] = s_memrealtime delta, 100 MHz, for the clock).  Never used in timed runs.
 constexpr uint32_t kStampFrom = 200, kStampCount = 2000;
+// Exchange-skew diagnostic (same STAMP builds): s_memrealtime (100 MHz, one clock for the whole chip)
+// of every workgroup's record publication and of workgroup 0's sweep completion, for kSkewEpochs
+// epochs from kStampFrom, at stamps[kSkewBase + g * kSkewEpochs + e] / [... + kMaxG * kSkewEpochs + e].
+constexpr uint32_t kSkewEpochs = 64;
+constexpr int kSkewBase = 16;
 #define PSTAMP(k)                                                                   \
   do {                                                                              \
     if (STAMP && stamping) {                                                        \
@@ -555,6 +560,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
                              __HIP_MEMORY_SCOPE_AGENT);
       }
       PSTAMP(2);
+      if (STAMP && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
+        stamps[kSkewBase + g * kSkewEpochs + (epoch - kStampFrom)] = __builtin_amdgcn_s_memrealtime();
       // ---- 3. lane L polls workgroup L's record until its ten tags equal the epoch
       VI gm{inf, kSentinel}, gx{-inf, kSentinel};
       double agm = 0.0, agx = 0.0;
@@ -585,6 +592,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
         }
       }
       const bool any_to = __any(timed_out);
+      if (STAMP && g == 0 && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
+        stamps[kSkewBase + kMaxG * kSkewEpochs + (epoch - kStampFrom)] = __builtin_amdgcn_s_memrealtime();
       PSTAMP(3);
       const VIL wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
       const double awgm = read_lane64(agm, wgm.lane), awgx = read_lane64(agx, wgx.lane);
@@ -1007,7 +1016,8 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   const size_t off_cnt = off_idx + al(size_t(n) * 8);
   const size_t off_trace = off_cnt + al(8);
   const size_t off_slots = off_trace + al(size_t(tcap) * 16);
-  const size_t slot_bytes = size_t(2) * kMaxG * kRecStride * 8 + 256;  // records + error word + stamps
+  // records + error word + phase stamps + exchange-skew stamps
+  const size_t slot_bytes = size_t(2) * kMaxG * kRecStride * 8 + 256 + (size_t(kMaxG) + 1) * kSkewEpochs * 8;
   const size_t total = off_slots + al(slot_bytes);
   int rc = ctx->ensure_ws(total);
   if (rc) return rc;
@@ -1119,6 +1129,35 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
               "globalred+barrier2 %.0f | loads %.0f | update %.0f | clock %.0f MHz | us/iter %.3f\n", NT, G, E,
               hs[0] / cnt, hs[1] / cnt, hs[2] / cnt, hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, hs[6] / cnt, mhz,
               double(hs[7]) / 100.0 / cnt);
+      if (atoi(sv) == 2) {  // exchange skew: spread of the record publications, and WG 0's wait past the last
+        std::vector<unsigned long long> sk(size_t(kMaxG + 1) * kSkewEpochs);
+        SVMD_CHECK(hipMemcpy(sk.data(), reinterpret_cast<unsigned long long*>(err) + 8 + kSkewBase,
+                             sk.size() * 8, hipMemcpyDeviceToHost));
+        double spread = 0.0, tail = 0.0;
+        std::vector<double> late(size_t(G), 0.0);  // mean lateness of each workgroup behind the first
+        int used = 0;
+        for (uint32_t e = 0; e < kSkewEpochs; ++e) {
+          unsigned long long lo = ~0ull, hi = 0;
+          for (int q = 0; q < G; ++q) {
+            const unsigned long long v = sk[size_t(q) * kSkewEpochs + e];
+            lo = std::min(lo, v);
+            hi = std::max(hi, v);
+          }
+          const unsigned long long done = sk[size_t(kMaxG) * kSkewEpochs + e];
+          if (!lo || !done || done < hi) continue;
+          ++used;
+          spread += double(hi - lo) * 10.0;
+          tail += double(done - hi) * 10.0;
+          for (int q = 0; q < G; ++q) late[size_t(q)] += double(sk[size_t(q) * kSkewEpochs + e] - lo) * 10.0;
+        }
+        if (used) {
+          fprintf(stderr, "[psmo skew G=%d, %d epochs] publication spread %.0f ns | last publication -> WG0 sweep done %.0f ns\n",
+                  G, used, spread / used, tail / used);
+          fprintf(stderr, "[psmo skew] mean lateness per workgroup (ns):");
+          for (int q = 0; q < G; ++q) fprintf(stderr, " %.0f", late[size_t(q)] / used);
+          fprintf(stderr, "\n");
+        }
+      }
     }
     return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
   }
