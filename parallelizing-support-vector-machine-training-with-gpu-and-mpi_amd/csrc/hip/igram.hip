@@ -269,16 +269,41 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 bool plan_quant(const double* mn, const double* mx, int64_t d, QuantPlan* P) {
   P->ok = false;
   if (!mn || !mx || d <= 0) return false;
-  std::map<double, std::vector<int32_t>> groups;  // range -> columns
-  std::vector<double> r(static_cast<size_t>(d), 0.0);
+  std::map<double, std::vector<int32_t>> by_range;  // range -> columns
   for (int64_t j = 0; j < d; ++j) {
     const double rng = mx[j] - mn[j];
     if (!(rng >= 1e-12)) continue;  // constant column: scaled to 0 everywhere, contributes nothing
     if (rng > 255.0 + 1e-9 || rng != std::floor(rng)) return false;  // integer data has integer ranges
-    r[size_t(j)] = rng;
-    groups[rng].push_back(int32_t(j));
+    by_range[rng].push_back(int32_t(j));
   }
-  if (groups.empty()) return false;
+  if (by_range.empty()) return false;
+  // Exact group merging: a column of range r joins a group of range R when r divides R -- its
+  // integers q in [0, r] become q * R / r in [0, R], and (dq)^2 / r^2 = (dq * R / r)^2 / R^2 -- so pixel
+  // columns whose maxima divide 255 (1, 3, 5, 15, 17, 51, 85) join the main group, and small ranges
+  // join any larger group they divide, each merge saving a padded k-step and an FP64 flush per tile.
+  // Ranges are placed from the most populated down; the first group each one divides takes it.
+  std::vector<std::pair<double, size_t>> order;
+  for (const auto& kv : by_range) order.emplace_back(kv.first, kv.second.size());
+  std::stable_sort(order.begin(), order.end(), [](const auto& a, const auto& b) {
+    return a.second != b.second ? a.second > b.second : a.first > b.first;
+  });
+  std::vector<double> targets;                    // group ranges in creation order
+  std::map<double, std::vector<int32_t>> groups;  // group range -> columns
+  std::vector<double> r(static_cast<size_t>(d), 0.0);  // per column: its group's range
+  for (const auto& [rng, cnt] : order) {
+    double to = rng;
+    for (double T : targets)
+      if (std::fmod(T, rng) == 0.0) {
+        to = T;
+        break;
+      }
+    if (to == rng) targets.push_back(rng);
+    for (int32_t j : by_range[rng]) {
+      r[size_t(j)] = to;
+      groups[to].push_back(j);
+    }
+  }
+  for (auto& kv : groups) std::sort(kv.second.begin(), kv.second.end());
   const std::vector<int32_t>* main = nullptr;
   double rmain = 0.0;
   for (const auto& kv : groups)

@@ -344,6 +344,7 @@ def _int_data(n, d, seed, ranges):
     (1031, 784, [255] * 9 + [254, 200], 2),  # ~18% correction columns
     (300, 100, [255] * 6 + [17, 3, 1], 3),  # several distinct ranges, small d
     (129, 40, [100], 4),                   # base range != 255
+    (777, 300, [255] * 8 + [254, 127, 2, 85, 253], 5),  # ranges merged into 255 / 254 (divisors), 253 apart
 ])
 def test_int_gram_matches_exact(dev, D, n, d, ranges, seed):
     P = _int_data(n, d, seed, ranges)
