@@ -257,10 +257,15 @@ __global__ __launch_bounds__(kNT) void kc_step_kernel(const KcPartial* __restric
   wave_argmin(hv, hi);
   wave_argmax(lv, li);
   __shared__ KcPartial sp[kNT / kWave];
+  __shared__ int32_t sdot[128];  // exact int32 cross term of each 32-column k-step of (i_high, i_low)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) sp[w] = KcPartial{hv, hi, lv, li};
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  // Every thread merges the per-wave partials (same inputs, same order -> the same pair everywhere).
+  hv = sp[0].vmin;
+  hi = sp[0].imin;
+  lv = sp[0].vmax;
+  li = sp[0].imax;
   for (int k = 1; k < kNT / kWave; ++k) {
     if (better_min(hv, hi, sp[k].vmin, sp[k].imin)) {
       hv = sp[k].vmin;
@@ -271,6 +276,30 @@ __global__ __launch_bounds__(kNT) void kc_step_kernel(const KcPartial* __restric
       li = sp[k].imax;
     }
   }
+  // K12 of the exact-integer path: one k-step per thread (the integer sums are exact, so the
+  // group-ordered FP64 flushes below reproduce kval() bit for bit) instead of one thread walking
+  // all kq columns -- that serial dot product was most of this kernel's ~15 us.
+  const bool need_k12 = INT && hi < n && li < n && hi != li && !(lv <= hv + 2.0 * tau);  // block-uniform
+  if (need_k12) {
+    const int nsteps = q.kq / 32;
+    if (int(threadIdx.x) < nsteps) {
+      const int4* pa = reinterpret_cast<const int4*>(q.Q + hi * int64_t(q.kq)) + 2 * threadIdx.x;
+      const int4* pb = reinterpret_cast<const int4*>(q.Q + li * int64_t(q.kq)) + 2 * threadIdx.x;
+      const int4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+      int32_t acc = 0;
+      acc = __builtin_amdgcn_sdot4(a0.x, b0.x, acc, false);
+      acc = __builtin_amdgcn_sdot4(a0.y, b0.y, acc, false);
+      acc = __builtin_amdgcn_sdot4(a0.z, b0.z, acc, false);
+      acc = __builtin_amdgcn_sdot4(a0.w, b0.w, acc, false);
+      acc = __builtin_amdgcn_sdot4(a1.x, b1.x, acc, false);
+      acc = __builtin_amdgcn_sdot4(a1.y, b1.y, acc, false);
+      acc = __builtin_amdgcn_sdot4(a1.z, b1.z, acc, false);
+      acc = __builtin_amdgcn_sdot4(a1.w, b1.w, acc, false);
+      sdot[threadIdx.x] = acc;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
   st->miss_h = st->miss_l = 0;
   if (hi >= n || li >= n) {  // main3.cpp:205-209
     st->pending = 0;
@@ -287,7 +316,28 @@ __global__ __launch_bounds__(kNT) void kc_step_kernel(const KcPartial* __restric
   }
   const int32_t yh = y[hi], yl = y[li];
   const double K11 = kval<INT>(q, hi, hi, neg_gamma), K22 = kval<INT>(q, li, li, neg_gamma);
-  const double K12 = kval<INT>(q, hi, li, neg_gamma);
+  double K12;
+  if (need_k12) {  // kval<true>(q, hi, li) from the per-step sums, same operation order
+    int32_t acc = 0;
+    double x = 0.0;
+    for (int st_k = 0; st_k < q.kq / 32; ++st_k) {
+      acc += sdot[st_k];
+      if (st_k < q.main_step0) {
+        const double wg = q.step_w[st_k];
+        if (wg != 0.0) {
+          x += wg * double(acc);
+          acc = 0;
+        }
+      }
+    }
+    const int32_t D0 = q.N0[hi] + q.N0[li] - 2 * acc;
+    double dist = q.w0 * double(D0);
+    if (q.main_step0 > 0) dist += (q.WN[hi] + q.WN[li]) - 2.0 * x;
+    dist = dist > 0.0 ? dist : 0.0;
+    K12 = exp(neg_gamma * dist);
+  } else {
+    K12 = kval<INT>(q, hi, li, neg_gamma);
+  }
   const double ah = alpha[hi], al = alpha[li];
   const int s = yh * yl;
   const double eta = K11 + K22 - 2.0 * K12;

@@ -1,11 +1,12 @@
 """Beyond the resident-Gram limit: train on n synthetic MNIST rows whose n x n FP64 Gram does not fit
 in one MI355X's HBM (n = 250k -> 500 GB), via the on-demand HBM row cache (rowcache.hip)."""
+import os
 import sys
 import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from svm355 import SVC  # noqa: E402
 from svm355.ops import device as D  # noqa: E402
 from svm355.utils.data import synthetic_mnist  # noqa: E402
