@@ -9,7 +9,8 @@ cascade  the MPI Cascade programs (code/mpi_svm_main2.cpp ``--topology star`` = 
          code/mpi_svm_main3.cpp ``--topology tree`` = classical), one process per GPU over
          torch.distributed (RCCL/xGMI; ``--backend gloo`` for CPU ranks).  Run it under
          ``torchrun --nproc-per-node P`` or pass ``--gpus P`` and it launches torchrun itself.
-         stdout follows the reference's ``[rank 0] ...`` lines.
+         stdout follows the reference's ``[rank 0] ...`` lines.  ``--native`` runs
+         the C++ driver bin/svm_cascade instead (one process, a thread per GPU, RCCL from C++).
 
 The native CLIs take the options listed in ``csrc/apps/cli_common.h`` (``--dataset``,
 ``--synthetic N[,M]``, ``--C``, ``--gamma``, ``--tau``, ``--model-dir``, ``--json`` ...).
@@ -91,7 +92,25 @@ def _cascade(argv) -> int:
     ap.add_argument("--checkpoint-dir", default=None, help="per-round cascade state (resume with --resume)")
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("-v", "--verbose", type=int, default=1)
+    ap.add_argument("--native", action="store_true",
+                    help="run bin/svm_cascade instead: one process, a thread per GPU, RCCL driven from C++")
+    ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
+                    help="--native only: RCCL (one GPU per rank) or loopback (ranks share GPUs)")
     a = ap.parse_args(argv)
+
+    if a.native:
+        args = ["--topology", a.topology, "--gpus", str(max(1, a.gpus)), "--transport", a.transport,
+                "--max-rounds", str(a.max_rounds), "--C", str(a.C), "--gamma", str(a.gamma), "--tau", str(a.tau),
+                "--positive-label", str(a.positive_label), "--seed", str(a.seed)]
+        if a.synthetic:
+            args += ["--synthetic", a.synthetic]
+        else:
+            args += ["--train", a.train or f"{a.dataset}_train_data.csv", "--test", a.test or f"{a.dataset}_test_data.csv"]
+        if a.json:
+            args += ["--json", a.json]
+        if a.model_dir:
+            args += ["--model-dir", a.model_dir]
+        return _native("svm_cascade", args)
 
     if "RANK" not in os.environ and a.gpus > 0:
         # Not under a launcher: start one (a child process — never exec from here).
