@@ -1,4 +1,4 @@
-"""Command-line entry points: ``python -m svm355 {serial,gpu,sweep,cascade} [options]``.
+"""Command-line entry points: ``python -m svm355 {serial,gpu,sweep,cascade,multiclass} [options]``.
 
 serial   the reference's serial program (code/main3.cpp) -> native ``bin/svm_serial``
 gpu      the single-GPU program (code/gpu_svm_main3.cu; ``--n-limit N`` = gpu_svm_main4.cu) ->
@@ -11,6 +11,9 @@ cascade  the MPI Cascade programs (code/mpi_svm_main2.cpp ``--topology star`` = 
          ``torchrun --nproc-per-node P`` or pass ``--gpus P`` and it launches torchrun itself.
          stdout follows the reference's ``[rank 0] ...`` lines.  ``--native`` runs
          the C++ driver bin/svm_cascade instead (one process, a thread per GPU, RCCL from C++).
+
+multiclass  all-digit one-vs-rest (models/multiclass.py): one shared Gram per GPU, class solves
+         concurrent on streams; ``--gpus P`` deals the classes over P ranks (torchrun, RCCL).
 
 The native CLIs take the options listed in ``csrc/apps/cli_common.h`` (``--dataset``,
 ``--synthetic N[,M]``, ``--C``, ``--gamma``, ``--tau``, ``--model-dir``, ``--json`` ...).
@@ -114,18 +117,7 @@ def _cascade(argv) -> int:
 
     if "RANK" not in os.environ and a.gpus > 0:
         # Not under a launcher: start one (a child process — never exec from here).
-        fwd, skip = [], False
-        for x in argv:
-            if skip:
-                skip = False
-            elif x == "--gpus":
-                skip = True
-            elif not x.startswith("--gpus="):
-                fwd.append(x)
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
-               "-m", "svm355", "cascade", *fwd]
-        return subprocess.call(cmd, cwd=str(PKG.parent))
+        return _launch_self("cascade", argv, a.gpus)
 
     import numpy as np
     import torch
@@ -203,6 +195,94 @@ def _cascade(argv) -> int:
     return 0
 
 
+def _launch_self(cmd: str, argv, gpus: int) -> int:
+    """Start torchrun with ``gpus`` ranks running ``python -m svm355 <cmd>`` (a child process)."""
+    fwd, skip = [], False
+    for x in argv:
+        if skip:
+            skip = False
+        elif x == "--gpus":
+            skip = True
+        elif not x.startswith("--gpus="):
+            fwd.append(x)
+    run = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
+           "-m", "svm355", cmd, *fwd]
+    return subprocess.call(run, cwd=str(PKG.parent))
+
+
+def _multiclass(argv) -> int:
+    ap = argparse.ArgumentParser(prog="svm355 multiclass")
+    ap.add_argument("--dataset", default="mnist3")
+    ap.add_argument("--train", default=None)
+    ap.add_argument("--test", default=None)
+    ap.add_argument("--synthetic", default=None, help="N[,M]: MNIST-shaped synthetic data")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--C", type=float, default=10.0)
+    ap.add_argument("--gamma", type=float, default=0.00125)
+    ap.add_argument("--tau", type=float, default=1e-5)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--gpus", type=int, default=0, help="launch torchrun with this many ranks (classes dealt over them)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args(argv)
+    if "RANK" not in os.environ and a.gpus > 1:
+        return _launch_self("multiclass", argv, a.gpus)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from .models.multiclass import OneVsRestSVC
+    from .parallel.transport import TorchDistTransport
+    from .utils.data import load_csv, synthetic_mnist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    use_gpu = not a.cpu and torch.cuda.is_available()
+    dev = "cpu"
+    if use_gpu:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+        dev = f"cuda:{torch.cuda.current_device()}"
+    transport = None
+    if world > 1:
+        backend = a.backend if use_gpu else "gloo"
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(dev), timeout=COLLECTIVE_TIMEOUT)
+        else:
+            dist.init_process_group("gloo", timeout=COLLECTIVE_TIMEOUT)
+        transport = TorchDistTransport(torch.device(dev) if backend == "nccl" else torch.device("cpu"))
+    if a.synthetic:
+        parts = a.synthetic.split(",")
+        n, m = int(parts[0]), int(parts[1]) if len(parts) > 1 else 10000
+        tr, te = synthetic_mnist(n, seed=a.seed), synthetic_mnist(m, seed=a.seed, offset=n)
+    else:
+        tr = load_csv(a.train or f"{a.dataset}_train_data.csv")
+        te = load_csv(a.test or f"{a.dataset}_test_data.csv")
+    model = OneVsRestSVC(C=a.C, gamma=a.gamma, tol=a.tau, device=dev)
+    t0 = time.perf_counter()
+    model.fit(tr.X, tr.labels, transport=transport)
+    if use_gpu:
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    acc = model.score(te.X, te.labels) if te.n else None
+    t2 = time.perf_counter()
+    if rank == 0:
+        print(f"[rank 0] one-vs-rest over {len(model.classes_)} classes on {world} rank(s), n = {tr.n}")
+        print(f"[rank 0] union SV count = {len(model.support_)}, iterations per class = {model.n_iter_.tolist()}")
+        print(f"[rank 0] Test accuracy = {acc}")
+        print(f"[rank 0] training time = {int((t1 - t0) * 1e3)} ms, prediction time = {int((t2 - t1) * 1e3)} ms")
+        if a.json:
+            Path(a.json).write_text(json.dumps({
+                "program": "svm355 multiclass", "world": world, "n": tr.n, "classes": model.classes_.tolist(),
+                "n_sv_union": int(len(model.support_)), "n_iter": model.n_iter_.tolist(),
+                "b": model.intercepts_b_.tolist(), "stop_reasons": model.stop_reasons_, "accuracy": acc,
+                "training_ms": (t1 - t0) * 1e3, "prediction_ms": (t2 - t1) * 1e3}) + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] in ("-h", "--help"):
@@ -217,6 +297,8 @@ def main(argv=None) -> int:
         return _sweep(rest)
     if cmd == "cascade":
         return _cascade(rest)
+    if cmd == "multiclass":
+        return _multiclass(rest)
     print(f"unknown command {cmd!r}\n\n{__doc__}", file=sys.stderr)
     return 2
 

@@ -10,6 +10,12 @@ cross-kernel block against the union of all classes' support vectors and applies
 dual coefficients with one FP64 matrix product; the predicted label is the arg-max decision value.
 
 On the CPU (``device="cpu"``) each class is the native oracle (bit-exact reference arithmetic).
+
+Across GPUs (``fit(..., transport=t)``, one rank per GPU over RCCL): the classes are dealt
+round-robin to the ranks, each rank builds the Gram on its own GPU and solves its classes, and one
+all-reduce of the (classes x n) alpha matrix plus per-class b/iterations gives every rank the whole
+model — the one-vs-rest analogue of the reference's data-parallel cascade, with no cross-rank
+dependency inside a solve.
 """
 from __future__ import annotations
 
@@ -29,6 +35,7 @@ class OneVsRestSVC:
         """``concurrent_solves``: class solves run at once on the GPU (each persistent SMO occupies at
         most 64 of the MI355X's 256 CUs; results do not depend on it)."""
         self.concurrent_solves = concurrent_solves
+        self._transport = None
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else default_threads())
         self.device = device
@@ -42,7 +49,13 @@ class OneVsRestSVC:
         return self.device
 
     # ------------------------------------------------------------------ fit
-    def fit(self, X: np.ndarray, labels: np.ndarray, classes: Optional[List[int]] = None) -> "OneVsRestSVC":
+    def fit(self, X: np.ndarray, labels: np.ndarray, classes: Optional[List[int]] = None,
+            transport=None) -> "OneVsRestSVC":
+        """With a ``transport`` (svm355.parallel.transport, e.g. one rank per GPU over RCCL) every rank
+        passes the same rows, solves the classes k with k % world == rank on its own Gram, and the
+        per-class alphas, b and iteration counts are all-reduced, so every rank ends with the whole
+        model (identical to a single-rank fit)."""
+        self._transport = transport
         cuda = self._dev() != "cpu"
         X = np.ascontiguousarray(X, dtype=np.uint8 if (cuda and X.dtype == np.uint8) else np.float64)
         labels = np.asarray(labels)
@@ -58,21 +71,49 @@ class OneVsRestSVC:
     def _ys(self, labels):
         return [np.where(labels == c, 1, -1).astype(np.int32) for c in self.classes_]
 
+    def _mine(self, k: int) -> bool:
+        t = self._transport
+        return t is None or k % t.world == t.rank
+
+    def _combine(self, alphas, bs, iters, stops):
+        """All-reduce the per-class results of a distributed fit (zeros for other ranks' classes)."""
+        t = self._transport
+        if t is None:
+            return alphas, bs, iters, stops
+        import torch
+
+        from .. import _native as N
+
+        codes = {v: k for k, v in N.STOP_NAMES.items()}
+        a = alphas if isinstance(alphas, torch.Tensor) else torch.from_numpy(alphas)
+        meta = torch.tensor([[b, it, codes.get(st, 0)] for b, it, st in zip(bs, iters, stops)], dtype=torch.float64)
+        a_c, m_c = a.to(t.device), meta.to(t.device)
+        t.allreduce_(a_c, "sum")
+        t.allreduce_(m_c, "sum")
+        a = a_c.to(a.device)
+        m = m_c.cpu().numpy()
+        out_a = a if isinstance(alphas, torch.Tensor) else a.numpy()
+        return (out_a, [float(x) for x in m[:, 0]], [int(x) for x in m[:, 1]],
+                [N.STOP_NAMES.get(int(x), str(int(x))) for x in m[:, 2]])
+
     def _fit_cpu(self, X, labels):
         from ..ops import cpu as C
 
         self.scaler_ = MinMaxScaler().fit(X)
         Xs = self.scaler_.transform(X)
         K = C.rbf_matrix(Xs, Xs, self.params.gamma, self.params.n_threads)
-        coefs, bs, iters, stops, sup = [], [], [], [], set()
-        for y in self._ys(labels):
+        ys = self._ys(labels)
+        alphas = np.zeros((len(ys), X.shape[0]))
+        bs, iters, stops = [0.0] * len(ys), [0] * len(ys), [""] * len(ys)
+        for k, y in enumerate(ys):
+            if not self._mine(k):
+                continue
             a, r, _ = C.smo_train_gram(K, y, self.params)
-            coefs.append(a * y)
-            bs.append(r.b)
-            iters.append(r.iterations)
-            stops.append(r.stop_reason)
-            sup.update(np.flatnonzero(a > self.params.sv_tol).tolist())
-        self._finish(np.array(sorted(sup), dtype=np.int64), np.stack(coefs, 1), bs, iters, stops)
+            alphas[k], bs[k], iters[k], stops[k] = a, r.b, r.iterations, r.stop_reason
+        alphas, bs, iters, stops = self._combine(alphas, bs, iters, stops)
+        Y = np.stack(ys, 0)
+        sup = np.flatnonzero((alphas > self.params.sv_tol).any(0)).astype(np.int64)
+        self._finish(sup, (alphas * Y).T, bs, iters, stops)
         self.support_vectors_ = Xs[self.support_]
         self._dev_model = None
 
@@ -106,18 +147,20 @@ class OneVsRestSVC:
             s.synchronize()
             return r
 
-        workers = max(1, min(self.concurrent_solves, len(ys)))
+        mine = [k for k in range(len(ys)) if self._mine(k)]
+        workers = max(1, min(self.concurrent_solves, len(mine)))
         if workers > 1:
             from concurrent.futures import ThreadPoolExecutor
 
             with ThreadPoolExecutor(max_workers=workers) as ex:  # the native calls release the GIL
-                results = list(ex.map(solve, range(len(ys))))
+                results = dict(zip(mine, ex.map(solve, mine)))
         else:
-            results = [solve(k) for k in range(len(ys))]
-        bs = [r.b for r in results]
-        iters = [r.iterations for r in results]
-        stops = [r.stop_reason for r in results]
+            results = {k: solve(k) for k in mine}
+        bs = [results[k].b if k in results else 0.0 for k in range(len(ys))]
+        iters = [results[k].iterations if k in results else 0 for k in range(len(ys))]
+        stops = [results[k].stop_reason if k in results else "" for k in range(len(ys))]
         torch.cuda.synchronize(device)
+        alphas, bs, iters, stops = self._combine(alphas, bs, iters, stops)
         t3 = time.perf_counter()
         del K
         a = alphas.cpu().numpy()  # (classes, n)

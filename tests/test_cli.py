@@ -62,3 +62,12 @@ def test_native_cascade_rejects_non_power_of_two_tree():
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1
     assert "power-of-2" in r.stderr
+
+
+def test_cli_multiclass_two_ranks_gloo(tmp_path):
+    js = tmp_path / "mc.json"
+    out = _run(["multiclass", "--synthetic", "500,200", "--cpu", "--gpus", "2", "--backend", "gloo",
+                "--json", str(js)], tmp_path, timeout=600)
+    assert "[rank 0] one-vs-rest over 10 classes on 2 rank(s)" in out
+    s = json.loads(js.read_text())
+    assert s["world"] == 2 and all(r == "converged" for r in s["stop_reasons"]) and s["accuracy"] > 0.8

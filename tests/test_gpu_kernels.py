@@ -477,3 +477,23 @@ def test_ovr_multiclass_gpu_matches_cpu(dev):
     np.testing.assert_array_equal(g.support_, c.support_)
     np.testing.assert_allclose(g.intercepts_b_, c.intercepts_b_, rtol=0, atol=1e-7)
     np.testing.assert_array_equal(g.predict(te.X), c.predict(te.X))
+
+
+def test_ovr_distributed_threads_gpu_equals_single_rank(dev):
+    """Two ranks on the one GPU (thread transport): each solves its classes on its own Gram; the
+    all-reduced model equals the single-rank device fit exactly."""
+    from svm355 import OneVsRestSVC
+    from svm355.parallel.transport import run_threads
+
+    tr = synthetic_mnist(1200, seed=32)
+    one = OneVsRestSVC(device="cuda:0").fit(tr.X, tr.labels)
+
+    def fn(t):
+        m = OneVsRestSVC(device="cuda:0").fit(tr.X, tr.labels, transport=t)
+        return m.support_, m.dual_coef_, m.intercepts_b_, m.n_iter_
+
+    for sup, coef, b, it in run_threads(2, fn, device_for_rank=lambda r: torch.device("cuda:0")):
+        np.testing.assert_array_equal(sup, one.support_)
+        np.testing.assert_array_equal(coef, one.dual_coef_)
+        np.testing.assert_array_equal(b, one.intercepts_b_)
+        np.testing.assert_array_equal(it, one.n_iter_)

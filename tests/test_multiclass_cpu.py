@@ -18,3 +18,66 @@ def test_ovr_cpu_matches_per_class_svc():
     np.testing.assert_allclose(m.decision_function(te.X)[:, k], s.decision_function(te.X), rtol=0, atol=1e-12)
     acc = m.score(te.X, te.labels)
     assert acc > 0.8, acc
+
+
+def _ovr_rank(t, tr):
+    m = OneVsRestSVC(device="cpu", n_threads=2).fit(tr.X, tr.labels, transport=t)
+    return m.support_, m.dual_coef_, m.intercepts_b_, m.n_iter_, m.stop_reasons_
+
+
+def test_ovr_distributed_over_threads_equals_single_rank():
+    """Classes split over 3 ranks (k % world == rank), results all-reduced: every rank holds the
+    same model as a single-rank fit, bit for bit (each class is solved by exactly one rank)."""
+    from svm355.parallel.transport import run_threads
+
+    tr = synthetic_mnist(400, seed=5)
+    one = OneVsRestSVC(device="cpu", n_threads=2).fit(tr.X, tr.labels)
+    for sup, coef, b, it, st in run_threads(3, lambda t: _ovr_rank(t, tr)):
+        np.testing.assert_array_equal(sup, one.support_)
+        np.testing.assert_array_equal(coef, one.dual_coef_)
+        np.testing.assert_array_equal(b, one.intercepts_b_)
+        np.testing.assert_array_equal(it, one.n_iter_)
+        assert st == one.stop_reasons_
+
+
+def _gloo_ovr_worker(rank, world, port, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from svm355.parallel.transport import TorchDistTransport
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = synthetic_mnist(400, seed=5)
+        q.put((rank, *_ovr_rank(TorchDistTransport(torch.device("cpu")), tr)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ovr_distributed_gloo_two_processes():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_ovr_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tr = synthetic_mnist(400, seed=5)
+    one = OneVsRestSVC(device="cpu", n_threads=2).fit(tr.X, tr.labels)
+    for _, sup, coef, b, it, st in res:
+        np.testing.assert_array_equal(sup, one.support_)
+        np.testing.assert_array_equal(coef, one.dual_coef_)
+        np.testing.assert_array_equal(b, one.intercepts_b_)
+        assert st == one.stop_reasons_
