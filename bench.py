@@ -131,10 +131,14 @@ def main(argv=None):
         step()
     barrier_sync()
     t0 = time.perf_counter()
-    marks = []
+    marks, parts = [], []
     for _ in range(a.steps):
         step()
         marks.append(time.perf_counter())  # host-side step boundaries (diagnostic only)
+        if not use_cascade:  # per-step upload / Gram / SMO split (diagnostic only)
+            parts.append([round(model.timings_.get(k, 0.0), 2) for k in ("upload_preprocess_ms", "gram_alloc_ms",
+                                                                           "gram_ms", "smo_ms")]
+                         + [round(model.fit_time_ * 1e3, 2)])
     barrier_sync()
     elapsed = time.perf_counter() - t0
     step_ms = [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + marks[:-1], marks)]
@@ -196,6 +200,7 @@ def main(argv=None):
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
             "step_ms": step_ms,
+            "step_upload_alloc_gram_smo_fit_ms": parts,
             **extra,
         }
         s = json.dumps(line)

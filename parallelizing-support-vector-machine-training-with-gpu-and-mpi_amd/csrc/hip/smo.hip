@@ -403,6 +403,9 @@ constexpr int kSkewBase = 16;
     }                                                                               \
   } while (0)
 
+// XCD-local registration window (s_memrealtime ticks, 100 MHz): 2 ms, then the host falls back.
+constexpr unsigned long long kRegisterTicks = 200000;
+
 // NT threads per workgroup (NW = NT/64 waves), E register-resident elements per thread:
 // element e of thread t is training point lo + t + NT*e of the workgroup's slice.
 // XLOCAL: all participating workgroups run on ONE XCD (read from HW_REG_XCC_ID at start; the grid
@@ -434,15 +437,27 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
         const unsigned tk = __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rank = tk < unsigned(glocal) ? int(tk) : -1;
       }
-      if (rank >= 0) {  // wait until every participant has registered (bounded)
-        int64_t spins = 0;
-        while (__hip_atomic_load(reg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unsigned(glocal)) {
-          if (++spins > spin_limit) {
-            __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rank = -2;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
+      if (rank >= 0) {
+        // Wait until every participant has registered, for at most kRegisterTicks.  The outcome is
+        // one compare-and-swap on the decision word (reg[1]: 0 forming, 1 go, 2 abandoned), so all
+        // participants agree even when the last one registers just as another gives up.
+        unsigned* decision = reg + 1;
+        const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+        unsigned d;
+        while ((d = __hip_atomic_load(decision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+          unsigned want = 0u;
+          if (__hip_atomic_load(reg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(glocal))
+            __hip_atomic_compare_exchange_strong(decision, &want, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+          else if (__builtin_amdgcn_s_memrealtime() - t_start > kRegisterTicks)
+            __hip_atomic_compare_exchange_strong(decision, &want, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (d != 1u) {
+          __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          rank = -2;
         }
       }
       s_rank = rank;
@@ -930,15 +945,20 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
 // default 64; all co-resident, one sweep pass).
 constexpr int kDefaultNT = 512;
 constexpr int kXcdMaxG = 32;              // workgroups of the XCD-local solver (one XCD has 32 CUs)
-constexpr int64_t kXcdDefaultMax = 24000;  // default n limit of the XCD-local solver (tuned on MI355X)
+constexpr int64_t kXcdDefaultMax = 65536;  // default n limit of the XCD-local solver (tuned on MI355X)
+constexpr int64_t kXcdWideFrom = 24000;    // above this the XCD-local solver uses 1024-thread workgroups
 constexpr int64_t kSingleDefaultMax = 2048;  // auto mode: single workgroup up to this n (tuned on MI355X)
 constexpr int kSingleDefaultNT = 512;
 int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out, int gcap) {
   int target = 64;
   if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
   if (gcap > 0) target = std::min(target, gcap);
-  // Measured on MI355X: 256-thread workgroups win for the XCD-local solver up to ~16k points.
-  int nt = (gcap > 0 && n <= 16000) ? 256 : kDefaultNT;
+  // Measured on MI355X (profiles/r1_smo_launch_shape.txt): the XCD-local solver wants 256-thread
+  // workgroups up to ~16k points and 1024-thread ones (E <= 2, <= 30 workgroups) from 24k to 64k,
+  // where it beats the device-wide exchange by 3-7 % per iteration.
+  int nt = kDefaultNT;
+  if (gcap > 0 && n <= 16000) nt = 256;
+  if (gcap > 0 && n > kXcdWideFrom) nt = 1024;
   if (const char* v = getenv("SVM355_PSMO_NT")) nt = atoi(v);
   if (nt != 256 && nt != 512 && nt != 1024) nt = kDefaultNT;
   const int emax = nt == 256 ? 16 : nt == 512 ? 8 : 4;
@@ -1113,6 +1133,8 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
       SVMD_CHECK(hipStreamSynchronize(s));
       if (!(xlocal && herr == 2)) break;
       // XCD 0 did not receive enough workgroups: nothing was touched, run the device-wide kernel.
+      fprintf(stderr, "[svm355] XCD-local SMO: fewer than %d workgroups registered on XCD 0; "
+              "running the device-wide solver\n", G);
       xlocal = false;
       if (!persistent_grid(n, &G, &E, &NT, 0)) break;
       herr = 0;

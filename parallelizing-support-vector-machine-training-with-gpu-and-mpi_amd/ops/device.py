@@ -252,15 +252,19 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
         return res, out
     if trace_cap > 0:
         raise ValueError("trace_cap is supported by the row-cache path only (use smo() on a Gram)")
+    import time as _t
+
+    ta = _t.perf_counter()
     if K is None:
         K = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+    alloc_ms = (_t.perf_counter() - ta) * 1e3
     tm = N.SvmdTiming()
     N.check(ctx.lib.svmd_train_q(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
                                  X.shape[1], N.ptr(y), N.ptr(alpha), int(warm), ctypes.byref(p), ctypes.byref(r),
                                  N.ptr(K), K.stride(0), ctypes.byref(tm), N.ptr(a), N.ptr(b), d,
                                  GRAM_MODES[gram], ctypes.byref(used)), "svmd_train_q")
     return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
-                                      "kcache": "full", "gram_path": "int8-exact" if used.value else "fp64"}
+                                      "gram_alloc_ms": alloc_ms, "kcache": "full", "gram_path": "int8-exact" if used.value else "fp64"}
 
 
 def rbf_gram_sym(X: torch.Tensor, sqn: Optional[torch.Tensor], gamma: float, mn=None, mx=None,
