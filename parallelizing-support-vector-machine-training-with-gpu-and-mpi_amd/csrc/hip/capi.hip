@@ -244,6 +244,23 @@ SVM_API int svmd_smo(void* h, const double* K_d, int64_t ldk, const int32_t* y_d
   return ctx->end();
 }
 
+SVM_API int svmd_smo_multi(void* h, const double* K_d, int64_t ldk, const int32_t* Y_d, int64_t n, int32_t nclass,
+                           double* A_d, const svm_params* p, svm_result* r, int32_t* batched) {
+  SVMD_CTX(h);
+  TraceRange tr("svm355:smo_multi");
+  const svm_params q = resolve(p);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = run_smo_multi(ctx, K_d, ldk, Y_d, n, nclass, A_d, q, r, batched);
+  if (rc) return rc;
+  if (r) {
+    std::vector<double> a(static_cast<size_t>(n) * size_t(nclass));
+    SVMD_CHECK(hipMemcpy(a.data(), A_d, a.size() * 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < nclass; ++k) r[k].n_sv = svm_sv_indices(a.data() + size_t(k) * size_t(n), n, q.sv_tol, nullptr);
+  }
+  return ctx->end();
+}
+
 // Gram selection: mode 0 = auto (exact-integer path when the scaled rows are integer multiples of
 // 1/r_j, else FP64), 1 = FP64 only, 2 = integer path required.  SVM355_GRAM=fp64|int overrides
 // the auto mode.  mn/mx (host, d values) are the min-max statistics the rows were scaled with.

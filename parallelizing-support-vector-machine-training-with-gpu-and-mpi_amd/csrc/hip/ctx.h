@@ -119,5 +119,8 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
                      svm_result* r, size_t cache_bytes, int64_t* trace, int64_t trace_cap, int32_t* used_int);
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
+// nclass cold-start solves on one Gram (Y, A: nclass x n, class-major): XCD teams (smo.hip).
+int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y, int64_t n, int nclass, double* A,
+                  const svm_params& p, svm_result* r, int32_t* batched);
 
 }  // namespace svm355

@@ -19,6 +19,7 @@
 // (gram_mfma.hip), so K11/K22/K12 are plain loads.  Arithmetic replicates main3.cpp:235-275
 // operation by operation (built with -ffp-contract=off), so on an identical kernel matrix the
 // trajectory is bit-identical to the CPU oracle.
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -406,67 +407,21 @@ constexpr int kSkewBase = 16;
 // XCD-local registration window (s_memrealtime ticks, 100 MHz): 2 ms, then the host falls back.
 constexpr unsigned long long kRegisterTicks = 200000;
 
-// NT threads per workgroup (NW = NT/64 waves), E register-resident elements per thread:
-// element e of thread t is training point lo + t + NT*e of the workgroup's slice.
-// XLOCAL: all participating workgroups run on ONE XCD (read from HW_REG_XCC_ID at start; the grid
-// is over-provisioned and the first `glocal` workgroups that land on XCD 0 take ranks 0..glocal-1,
-// the rest exit).  Records are then exchanged through that XCD's shared L2 (plain stores, L1-bypassing
-// sc1 loads) instead of the device-wide fabric.  If XCD 0 receives fewer than glocal workgroups the
-// registration times out before any state is touched (err = 2) and the host falls back.
-template <int NT, int E, bool STAMP, bool XLOCAL = false>
-__global__ __launch_bounds__(NT) void smo_persistent_kernel(
-    const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
-    double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
-    SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
-    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps,
-    int glocal = 0) {
+// One solve of the persistent SMO by G co-resident workgroups (this one is g), NT threads per
+// workgroup (NW = NT/64 waves), E register-resident elements per thread: element e of thread t is
+// training point lo + t + NT*e of the workgroup's slice.  Epochs continue from epoch0 (record tags
+// must never repeat on a slot array); returns the last epoch used.
+template <int NT, int E, bool STAMP, bool XLOCAL>
+__device__ __forceinline__ uint32_t persist_solve(
+    PersistShared& sh, int G, int g, uint32_t epoch0, const double* __restrict__ K, int64_t ldk,
+    const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice,
+    unsigned long long* __restrict__ slots, SmoState* __restrict__ st, double C, double eps, double tau,
+    int64_t max_iter, int64_t* __restrict__ trace, int64_t trace_cap, unsigned* __restrict__ err,
+    int64_t spin_limit, unsigned long long* __restrict__ stamps) {
   constexpr int NW = NT / 64;
-  __shared__ PersistShared sh;
   unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = 0, rt0 = 0;
   bool stamping = false;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int G = gridDim.x, g = blockIdx.x;
-  if constexpr (XLOCAL) {
-    __shared__ int s_rank;
-    unsigned* reg = err + 2;
-    if (t == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      int rank = -1;
-      if ((xcc & 0xF) == 0) {
-        const unsigned tk = __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rank = tk < unsigned(glocal) ? int(tk) : -1;
-      }
-      if (rank >= 0) {
-        // Wait until every participant has registered, for at most kRegisterTicks.  The outcome is
-        // one compare-and-swap on the decision word (reg[1]: 0 forming, 1 go, 2 abandoned), so all
-        // participants agree even when the last one registers just as another gives up.
-        unsigned* decision = reg + 1;
-        const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-        unsigned d;
-        while ((d = __hip_atomic_load(decision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-          unsigned want = 0u;
-          if (__hip_atomic_load(reg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(glocal))
-            __hip_atomic_compare_exchange_strong(decision, &want, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-          else if (__builtin_amdgcn_s_memrealtime() - t_start > kRegisterTicks)
-            __hip_atomic_compare_exchange_strong(decision, &want, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (d != 1u) {
-          __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          rank = -2;
-        }
-      }
-      s_rank = rank;
-    }
-    __syncthreads();
-    if (s_rank < 0) return;  // not a participant (or registration timed out: nothing touched)
-    G = glocal;
-    g = s_rank;
-  }
   const int64_t lo = int64_t(g) * slice, hi_end = std::min<int64_t>(n, lo + slice);
   const double c_hi = C - eps, c_lo = 0.0 + eps;
   const double inf = __builtin_inf();
@@ -486,7 +441,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
   double b_high = st->b_high, b_low = st->b_low;
   int32_t stop = SVM_STOP_RUNNING;
 
-  for (uint32_t epoch = 1;; ++epoch) {
+  uint32_t epoch = epoch0 + 1;
+  for (;; ++epoch) {
     if (STAMP) {
       const bool on = g == 0 && threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
       if (on && !stamping) rt0 = __builtin_amdgcn_s_memrealtime();
@@ -721,6 +677,146 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
     st->pending = 0;
     st->stop = stop < 0 ? SVM_STOP_RUNNING : stop;
   }
+  return epoch;
+}
+
+
+// XCD-local team registration (thread 0 of a workgroup running on XCD `xcc`).  reg[0] counts the
+// workgroups that landed on the team's XCD: the first glocal take ranks 0..glocal-1 and wait until
+// all have registered, for at most kRegisterTicks.  The outcome is one compare-and-swap on the
+// decision word reg[1] (0 forming, 1 go, 2 abandoned), so all participants agree even when the last
+// one registers just as another gives up.  Returns the rank, -1 (not a participant) or -2
+// (abandoned: *err = 2, nothing touched).
+__device__ int xcd_register(unsigned* reg, unsigned* err, int glocal, unsigned long long ticks) {
+  const unsigned tk = __hip_atomic_fetch_add(reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tk >= unsigned(glocal)) return -1;
+  unsigned* decision = reg + 1;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  unsigned d;
+  while ((d = __hip_atomic_load(decision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+    unsigned want = 0u;
+    if (__hip_atomic_load(reg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(glocal))
+      __hip_atomic_compare_exchange_strong(decision, &want, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    else if (__builtin_amdgcn_s_memrealtime() - t_start > ticks)
+      __hip_atomic_compare_exchange_strong(decision, &want, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __builtin_amdgcn_s_sleep(2);
+  }
+  if (d != 1u) {
+    __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return -2;
+  }
+  return int(tk);
+}
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return xcc & 0xF;
+}
+
+// XLOCAL: all participating workgroups run on ONE XCD (XCD 0; the grid is over-provisioned, see
+// xcd_register, the rest exit).  Records are then exchanged through that XCD's shared L2 (plain
+// stores, L1-bypassing sc1 loads) instead of the device-wide fabric.  If XCD 0 receives fewer than
+// glocal workgroups the registration is abandoned before any state is touched (err = 2) and the
+// host falls back to the device-wide kernel.
+template <int NT, int E, bool STAMP, bool XLOCAL = false>
+__global__ __launch_bounds__(NT) void smo_persistent_kernel(
+    const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
+    double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
+    SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
+    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps,
+    int glocal = 0, unsigned long long reg_ticks = kRegisterTicks) {
+  __shared__ PersistShared sh;
+  int G = gridDim.x, g = blockIdx.x;
+  if constexpr (XLOCAL) {
+    __shared__ int s_rank;
+    if (threadIdx.x == 0) s_rank = xcc_id() == 0 ? xcd_register(err + 2, err, glocal, reg_ticks) : -1;
+    __syncthreads();
+    if (s_rank < 0) return;  // not a participant (or registration abandoned: nothing touched)
+    G = glocal;
+    g = s_rank;
+  }
+  persist_solve<NT, E, STAMP, XLOCAL>(sh, G, g, 0, K, ldk, y, alpha, f, n, slice, slots, st, C, eps, tau, max_iter,
+                                      trace, trace_cap, err, spin_limit, stamps);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Batched solves (one-vs-rest: one SMO per class on the same resident Gram).  Every XCD forms its
+// own team of glocal workgroups (xcd_register on its own registration words) and runs whole solves
+// with the XCD-local exchange; teams pull class indices from one queue, so the eight XCDs work on
+// eight classes at once and a team that finishes early takes the next class.  Team rank 0 takes
+// the class and posts it in the team's mailbox ((round << 10) | class); the other members poll it.
+// A team that cannot form leaves its classes to the others; the host re-runs any class no team
+// took (st[k].stop still RUNNING).  ctl layout (u32): team x at [4x .. 4x+3] = {count, decision,
+// mailbox, -}, queue at [kMultiQueue], error word at [kMultiErr].
+constexpr int kMultiTeams = 8;
+constexpr int kMultiQueue = 4 * kMultiTeams, kMultiErr = kMultiQueue + 1, kMultiCtlWords = 64;
+constexpr unsigned long long kMailTicks = 10000000ull;  // 100 ms: a team member gives up waiting for a class
+
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void smo_multi_kernel(
+    const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ Y, double* __restrict__ A,
+    double* __restrict__ F, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
+    SmoState* __restrict__ st, int nclass, double C, double eps, double tau, int64_t max_iter,
+    unsigned* __restrict__ ctl, int64_t spin_limit, int glocal, unsigned long long reg_ticks) {
+  __shared__ PersistShared sh;
+  __shared__ int s_rank, s_cls;
+  const unsigned team = xcc_id();
+  unsigned* err = ctl + kMultiErr;
+  if (threadIdx.x == 0)
+    s_rank = team < unsigned(kMultiTeams) ? xcd_register(ctl + 4 * team, err, glocal, reg_ticks) : -1;
+  __syncthreads();
+  const int g = s_rank;
+  if (g < 0) return;
+  unsigned* mail = ctl + 4 * team + 2;
+  unsigned long long* tslots = slots + size_t(team) * 2 * kMaxG * kRecStride;
+  uint32_t epoch = 0;
+  for (unsigned round = 1;; ++round) {
+    if (threadIdx.x == 0) {
+      int cls = nclass;
+      if (g == 0) {
+        const unsigned c = __hip_atomic_fetch_add(ctl + kMultiQueue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cls = c < unsigned(nclass) ? int(c) : nclass;
+        __hip_atomic_store(mail, (round << 10) | unsigned(cls), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const unsigned v = __hip_atomic_load(mail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((v >> 10) == round) {
+            cls = int(v & 1023u);
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kMailTicks) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      s_cls = cls;
+    }
+    __syncthreads();
+    const int cls = s_cls;
+    if (cls >= nclass) break;
+    epoch = persist_solve<NT, E, false, true>(sh, glocal, g, epoch, K, ldk, Y + int64_t(cls) * n, A + int64_t(cls) * n,
+                                              F + int64_t(cls) * n, n, slice, tslots, st + cls, C, eps, tau, max_iter,
+                                              nullptr, 0, err, spin_limit, nullptr);
+    if (sh.timeout) break;
+  }
+}
+
+// Cold start of nclass problems: alpha = 0, f = -y, fresh state.
+__global__ void smo_multi_init_kernel(const int32_t* __restrict__ Y, double* __restrict__ A, double* __restrict__ F,
+                                      int64_t total, SmoState* st, int nclass) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < total) {
+    A[i] = 0.0;
+    F[i] = -static_cast<double>(Y[i]);
+  }
+  if (i < nclass) st[i] = SmoState{0, 0, 0.0, 0.0, 0.0, 0.0, 1, 0, SVM_STOP_RUNNING};
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -910,6 +1006,12 @@ __global__ __launch_bounds__(kSingleNT) void smo_single_kernel(
 
 namespace {
 
+// XCD-local registration window (SVM355_PSMO_REG_US overrides, microseconds).
+unsigned long long register_ticks() {
+  if (const char* v = getenv("SVM355_PSMO_REG_US")) return std::max(1ull, strtoull(v, nullptr, 10)) * 100ull;
+  return kRegisterTicks;
+}
+
 // Launch the persistent solver for a (threads per workgroup NT, elements per thread E) shape.
 template <int NT, int E>
 int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
@@ -923,10 +1025,12 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
     const int grid = 16 * G;
     if (sv && atoi(sv))
       hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha, f,
-                         n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G);
+                         n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G,
+                         register_ticks());
     else
       hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha,
-                         f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G);
+                         f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G,
+                         register_ticks());
     SVMD_LAUNCH_CHECK();
     return SVM_OK;
   }
@@ -1133,8 +1237,13 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
       SVMD_CHECK(hipStreamSynchronize(s));
       if (!(xlocal && herr == 2)) break;
       // XCD 0 did not receive enough workgroups: nothing was touched, run the device-wide kernel.
-      fprintf(stderr, "[svm355] XCD-local SMO: fewer than %d workgroups registered on XCD 0; "
-              "running the device-wide solver\n", G);
+      unsigned reg[2] = {0, 0};
+      SVMD_CHECK(hipMemcpy(reg, err + 2, sizeof(reg), hipMemcpyDeviceToHost));
+      static std::atomic<int> reported{0};
+      if (reported.fetch_add(1) == 0)
+        fprintf(stderr, "[svm355] XCD-local SMO: fewer than %d workgroups registered on XCD 0 within %.0f us "
+                "(%u landed there in all, grid %d; another XCD-local solve running concurrently?); running the "
+                "device-wide solver (reported once)\n", G, double(register_ticks()) / 100.0, reg[0], 16 * G);
       xlocal = false;
       if (!persistent_grid(n, &G, &E, &NT, 0)) break;
       herr = 0;
@@ -1248,6 +1357,91 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   }
   SVMD_CHECK(hipMemcpy(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost));
   return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
+}
+
+namespace {
+template <int NT, int E>
+void launch_multi_e(hipStream_t s, int grid, const double* K, int64_t ldk, const int32_t* Y, double* A, double* F,
+                    int64_t n, unsigned long long* slots, SmoState* st, int nclass, const svm_params& p, unsigned* ctl,
+                    int G) {
+  hipLaunchKernelGGL((smo_multi_kernel<NT, E>), dim3(grid), dim3(NT), 0, s, K, ldk, Y, A, F, n, int64_t(NT) * E, slots,
+                     st, nclass, p.C, p.eps, p.tau, p.max_iter, ctl, int64_t(1) << 22, G, register_ticks());
+}
+}  // namespace
+
+int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y, int64_t n, int nclass, double* A,
+                  const svm_params& p, svm_result* r, int32_t* batched) {
+  if (n <= 0 || nclass <= 0) {
+    set_error("svmd_smo_multi: empty problem");
+    return SVM_ERR_EMPTY;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t s = ctx->stream;
+  std::vector<SmoState> fin(static_cast<size_t>(nclass));
+  int G = 0, E = 0, NT = 0;
+  bool ok = nclass < 1000 && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT, kXcdMaxG);
+  ok = ok && ((NT == 256 && E <= 2) || (NT == 512 && E <= 2) || (NT == 1024 && E <= 4));
+  if (const char* v = getenv("SVM355_SMO_MULTI"); v && atoi(v) == 0) ok = false;
+  if (batched) *batched = 0;
+  if (ok) {
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t total = size_t(nclass) * size_t(n);
+    const size_t off_f = 0;
+    const size_t off_st = off_f + al(total * 8);
+    const size_t off_slots = off_st + al(size_t(nclass) * sizeof(SmoState));
+    const size_t slot_bytes = size_t(kMultiTeams) * 2 * kMaxG * kRecStride * 8;
+    const size_t off_ctl = off_slots + al(slot_bytes);
+    int rc = ctx->ensure_ws(off_ctl + al(kMultiCtlWords * 4));
+    if (rc) return rc;
+    char* ws = static_cast<char*>(ctx->ws);
+    double* F = reinterpret_cast<double*>(ws + off_f);
+    SmoState* st = reinterpret_cast<SmoState*>(ws + off_st);
+    auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
+    auto* ctl = reinterpret_cast<unsigned*>(ws + off_ctl);
+    const int64_t init_n = std::max<int64_t>(int64_t(total), nclass);
+    hipLaunchKernelGGL(smo_multi_init_kernel, dim3(unsigned((init_n + 255) / 256)), dim3(256), 0, s, Y, A, F,
+                       int64_t(total), st, nclass);
+    SVMD_LAUNCH_CHECK();
+    SVMD_CHECK(hipMemsetAsync(ws + off_slots, 0, al(slot_bytes) + al(kMultiCtlWords * 4), s));
+    // Over-provisioned grid as for the single XCD-local solve: ~2*G workgroups per XCD.
+    const int grid = 16 * G;
+#define SVM_MULTI_CASE(nt, e) \
+  else if (NT == nt && E == e) launch_multi_e<nt, e>(s, grid, K, ldk, Y, A, F, n, slots, st, nclass, p, ctl, G);
+    if (false) {
+    }
+    SVM_MULTI_CASE(256, 1) SVM_MULTI_CASE(256, 2) SVM_MULTI_CASE(512, 1) SVM_MULTI_CASE(512, 2)
+    SVM_MULTI_CASE(1024, 1) SVM_MULTI_CASE(1024, 2) SVM_MULTI_CASE(1024, 4)
+#undef SVM_MULTI_CASE
+    SVMD_LAUNCH_CHECK();
+    unsigned herr = 0;
+    SVMD_CHECK(hipMemcpyAsync(fin.data(), st, size_t(nclass) * sizeof(SmoState), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipMemcpyAsync(&herr, ctl + kMultiErr, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipStreamSynchronize(s));
+    if (const char* v = getenv("SVM355_SMO_MULTI_DEBUG"); v && atoi(v)) {
+      unsigned hc[kMultiCtlWords];
+      SVMD_CHECK(hipMemcpy(hc, ctl, sizeof(hc), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[smo_multi G=%d NT=%d E=%d] per XCD landed/decision:", G, NT, E);
+      for (int x = 0; x < kMultiTeams; ++x) fprintf(stderr, " %u/%u", hc[4 * x], hc[4 * x + 1]);
+      fprintf(stderr, " | queue %u err %u\n", hc[kMultiQueue], hc[kMultiErr]);
+    }
+    if (herr == 1) {
+      set_error("svmd_smo_multi: a team timed out waiting for a workgroup record or its mailbox");
+      return SVM_ERR_DEVICE;
+    }
+    if (batched) *batched = 1;
+  }
+  // Classes no team solved (batched path off or unavailable, or teams that could not form): one by one.
+  for (int k = 0; k < nclass; ++k) {
+    if (ok && fin[size_t(k)].stop != SVM_STOP_RUNNING) {
+      const int rc = finish_smo(fin[size_t(k)], r ? &r[k] : nullptr, nullptr, nullptr, 0, t0);
+      if (rc) return rc;
+      continue;
+    }
+    const int rc = run_smo(ctx, K, ldk, Y + int64_t(k) * n, n, A + int64_t(k) * n, 0, p, r ? &r[k] : nullptr,
+                           nullptr, 0);
+    if (rc) return rc;
+  }
+  return SVM_OK;
 }
 
 }  // namespace svm355

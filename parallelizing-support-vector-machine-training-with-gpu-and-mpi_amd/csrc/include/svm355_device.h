@@ -69,6 +69,14 @@ SVM_API int svmd_smo(void* ctx, const double* K_d, int64_t ldk, const int32_t* y
                      double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
                      int64_t* trace_host, int64_t trace_cap);
 
+// nclass independent cold-start SMO solves on one device kernel matrix (one-vs-rest): Y_d and A_d
+// are nclass x n, class-major (row k = class k's +-1 labels / alphas).  The classes run
+// concurrently, one XCD-local team of workgroups per XCD pulling classes from a queue; r receives
+// nclass results.  *batched (optional) = 1 when the batched kernel ran (else the solves ran one by
+// one, e.g. SVM355_SMO_MULTI=0 or a shape it does not cover).
+SVM_API int svmd_smo_multi(void* ctx, const double* K_d, int64_t ldk, const int32_t* Y_d, int64_t n, int32_t nclass,
+                           double* A_d, const svm_params* p, svm_result* r, int32_t* batched);
+
 // End-to-end training on preprocessed device rows: RBF Gram (allocated internally, or K_d if
 // non-NULL with ldk >= n) + SMO.  timing may be NULL.
 SVM_API int svmd_train(void* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld,

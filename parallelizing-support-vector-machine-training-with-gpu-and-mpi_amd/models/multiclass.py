@@ -4,8 +4,11 @@ The reference trains a single one-vs-rest classifier (digit "1" vs the rest, mai
 Training all ten digits the same way is ten SMO solves on the same rows: the RBF Gram does not
 depend on the labels, so on the device it is computed once (exact-integer int8 MFMA path for
 pixel data), kept resident in HBM and reused by every class's SMO.  The solves are independent and
-each persistent SMO kernel is latency-bound on at most 64 workgroups, so ``concurrent_solves`` of
-them run at once on separate streams and fill the 256 CUs.  Prediction evaluates one
+each is latency-bound on one XCD's worth of workgroups, so they run in ONE launch
+(smo.hip smo_multi_kernel): every XCD forms a team of workgroups that exchanges its per-iteration
+candidates through that XCD's L2 and pulls classes from a shared queue — eight classes at once, and
+a team that finishes early takes the next class.  (``solver="streams"``: one persistent solve per
+class on ``concurrent_solves`` streams instead.)  Prediction evaluates one
 cross-kernel block against the union of all classes' support vectors and applies every class's
 dual coefficients with one FP64 matrix product; the predicted label is the arg-max decision value.
 
@@ -31,9 +34,13 @@ from ..utils.data import MinMaxScaler
 class OneVsRestSVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 gram: str = "auto", concurrent_solves: int = 8):
-        """``concurrent_solves``: class solves run at once on the GPU (each persistent SMO occupies at
-        most 64 of the MI355X's 256 CUs; results do not depend on it)."""
+                 gram: str = "auto", concurrent_solves: int = 8, solver: str = "auto"):
+        """``solver``: "batched" (default via "auto") runs all class solves in ONE kernel launch, a team
+        of workgroups per XCD pulling classes from a queue; "streams" runs one persistent solve per
+        class on ``concurrent_solves`` streams.  Results are identical either way."""
+        if solver not in ("auto", "batched", "streams"):
+            raise ValueError("solver must be auto, batched or streams")
+        self.solver = solver
         self.concurrent_solves = concurrent_solves
         self._transport = None
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
@@ -148,8 +155,19 @@ class OneVsRestSVC:
             return r
 
         mine = [k for k in range(len(ys)) if self._mine(k)]
+        results = {}
+        self.batched_ = False
+        if self.solver in ("auto", "batched") and mine:
+            # One launch: an XCD-local team per XCD, classes pulled from a queue (smo_multi_kernel).
+            Yb = torch.stack([ys_d[k] for k in mine]).contiguous()
+            Ab = torch.zeros((len(mine), n), dtype=torch.float64, device=device)
+            rs, self.batched_ = D.smo_multi(K, Yb, Ab, self.params, n=n)
+            alphas[mine] = Ab
+            results = dict(zip(mine, rs))
         workers = max(1, min(self.concurrent_solves, len(mine)))
-        if workers > 1:
+        if results:
+            pass
+        elif workers > 1:
             from concurrent.futures import ThreadPoolExecutor
 
             with ThreadPoolExecutor(max_workers=workers) as ex:  # the native calls release the GIL
@@ -174,7 +192,8 @@ class OneVsRestSVC:
                            "mn": mn, "mx": mx, "d": d, "device": device}
         self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, "gram_ms": (t2 - t1) * 1e3,
-                         "smo_ms_all_classes": (t3 - t2) * 1e3, "gram_path": path}
+                         "smo_ms_all_classes": (t3 - t2) * 1e3, "gram_path": path,
+                         "smo_solver": "batched" if self.batched_ else "streams"}
 
     def _finish(self, sup, coef_full, bs, iters, stops):
         self.support_ = sup

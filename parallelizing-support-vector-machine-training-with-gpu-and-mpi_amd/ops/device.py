@@ -15,7 +15,7 @@ from __future__ import annotations
 import ctypes
 import threading
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -194,6 +194,27 @@ def smo(K: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams
     if trace is not None:
         trace = trace[: max(0, min(trace_cap, res.iterations - 1))]
     return res, trace
+
+
+def smo_multi(K: torch.Tensor, Y: torch.Tensor, A: torch.Tensor, params: SVMParams,
+              n: Optional[int] = None) -> Tuple[List[SMOResult], bool]:
+    """``nclass`` cold-start SMO solves on one resident Gram (one-vs-rest): Y (nclass, n) int32 +-1,
+    A (nclass, n) float64 receives the alphas.  The classes run concurrently, one XCD-local team per
+    XCD (smo.hip, smo_multi_kernel); each result equals the single solve's bit for bit.
+    Returns (results, batched) — batched False when the solves ran one by one."""
+    n = K.shape[0] if n is None else n
+    if Y.dtype != torch.int32 or A.dtype != torch.float64 or Y.shape != A.shape or Y.shape[1] != n:
+        raise ValueError("Y must be (nclass, n) int32 and A (nclass, n) float64")
+    if not (Y.is_contiguous() and A.is_contiguous()):
+        raise ValueError("Y and A must be contiguous (class-major)")
+    nclass = Y.shape[0]
+    ctx = _ctx_for(K)
+    rs = (N.SvmResult * nclass)()
+    batched = ctypes.c_int32(0)
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_smo_multi(ctx.bind(), N.ptr(K), K.stride(0), N.ptr(Y), n, nclass, N.ptr(A),
+                                   ctypes.byref(p), rs, ctypes.byref(batched)), "svmd_smo_multi")
+    return [SMOResult.from_struct(r) for r in rs], bool(batched.value)
 
 
 GRAM_MODES = {"auto": 0, "fp64": 1, "int": 2}

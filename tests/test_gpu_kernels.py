@@ -497,3 +497,20 @@ def test_ovr_distributed_threads_gpu_equals_single_rank(dev):
         np.testing.assert_array_equal(coef, one.dual_coef_)
         np.testing.assert_array_equal(b, one.intercepts_b_)
         np.testing.assert_array_equal(it, one.n_iter_)
+
+
+@pytest.mark.parametrize("n", [1500, 5000, 26000])
+def test_ovr_batched_xcd_teams_equal_per_class_solves(dev, n):
+    """All classes in one launch (an XCD-local team per XCD pulling classes from a queue) gives the
+    per-class persistent solves' results bit for bit; shapes cover 256-, 512- and 1024-thread teams."""
+    from svm355 import OneVsRestSVC
+
+    tr = synthetic_mnist(n, seed=33)
+    b = OneVsRestSVC(device="cuda:0", solver="batched").fit(tr.X, tr.labels)
+    s = OneVsRestSVC(device="cuda:0", solver="streams").fit(tr.X, tr.labels)
+    assert b.timings_["smo_solver"] == "batched" and s.timings_["smo_solver"] == "streams"
+    assert all(r == "converged" for r in b.stop_reasons_)
+    np.testing.assert_array_equal(b.n_iter_, s.n_iter_)
+    np.testing.assert_array_equal(b.intercepts_b_, s.intercepts_b_)
+    np.testing.assert_array_equal(b.support_, s.support_)
+    np.testing.assert_array_equal(b.dual_coef_, s.dual_coef_)
