@@ -79,6 +79,14 @@ SVM_API int svmd_memcpy_d2h(void* h, void* dst_h, const void* src_d, int64_t byt
   return ctx->end();
 }
 
+SVM_API void svmd_destroy(void* h);
+
+namespace {
+__global__ void module_warm_kernel(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
+}
+}  // namespace
+
 SVM_API void* svmd_create(int32_t device) {
   if (hipSetDevice(device) != hipSuccess) {
     set_error("svmd_create: hipSetDevice(%d) failed", device);
@@ -93,6 +101,15 @@ SVM_API void* svmd_create(int32_t device) {
     delete ctx;
     return nullptr;
   }
+  // Pay the one-time costs here, not inside the first solve: load this library's code object (one
+  // launch), and allocate the pinned state block and a small solver workspace (grown on demand).
+  hipLaunchKernelGGL(module_warm_kernel, dim3(1), dim3(64), 0, ctx->stream, nullptr);
+  if (hipGetLastError() != hipSuccess || ctx->ensure_pinned(size_t(1) << 16) != SVM_OK ||
+      ctx->ensure_ws(size_t(16) << 20) != SVM_OK || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    set_error("svmd_create: warm-up on device %d failed", device);
+    svmd_destroy(ctx);
+    return nullptr;
+  }
   return ctx;
 }
 
@@ -104,10 +121,24 @@ SVM_API void svmd_destroy(void* h) {
   ctx->release_graph();
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->gram) (void)hipFree(ctx->gram);
+  if (ctx->count_d) (void)hipFree(ctx->count_d);
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
   if (ctx->ev_out) (void)hipEventDestroy(ctx->ev_out);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+SVM_API int svmd_release_cache(void* h) {
+  SVMD_CTX(h);
+  if (ctx->gram) {
+    SVMD_CHECK(hipSetDevice(ctx->device));
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+    SVMD_CHECK(hipFree(ctx->gram));
+    ctx->gram = nullptr;
+    ctx->gram_bytes = 0;
+  }
+  return SVM_OK;
 }
 
 SVM_API int svmd_set_stream(void* h, void* stream) {
@@ -237,9 +268,10 @@ SVM_API int svmd_smo(void* h, const double* K_d, int64_t ldk, const int32_t* y_d
   rc = run_smo(ctx, K_d, ldk, y_d, n, alpha_d, warm, q, r, trace_host, trace_cap);
   if (rc) return rc;
   if (r) {
-    std::vector<double> a(static_cast<size_t>(n));
-    SVMD_CHECK(hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost));
-    r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
+    int64_t c = 0;
+    rc = count_sv(ctx, alpha_d, n, 1, q.sv_tol, &c);
+    if (rc) return rc;
+    r->n_sv = c;
   }
   return ctx->end();
 }
@@ -254,9 +286,10 @@ SVM_API int svmd_smo_multi(void* h, const double* K_d, int64_t ldk, const int32_
   rc = run_smo_multi(ctx, K_d, ldk, Y_d, n, nclass, A_d, q, r, batched);
   if (rc) return rc;
   if (r) {
-    std::vector<double> a(static_cast<size_t>(n) * size_t(nclass));
-    SVMD_CHECK(hipMemcpy(a.data(), A_d, a.size() * 8, hipMemcpyDeviceToHost));
-    for (int k = 0; k < nclass; ++k) r[k].n_sv = svm_sv_indices(a.data() + size_t(k) * size_t(n), n, q.sv_tol, nullptr);
+    std::vector<int64_t> c(static_cast<size_t>(nclass));
+    rc = count_sv(ctx, A_d, n, nclass, q.sv_tol, c.data());
+    if (rc) return rc;
+    for (int k = 0; k < nclass; ++k) r[k].n_sv = c[size_t(k)];
   }
   return ctx->end();
 }
@@ -305,16 +338,25 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
   int rc = ctx->begin();
   if (rc) return rc;
   double* K = K_d;
-  bool owned = false;
-  if (!K) {
+  if (!K) {  // library-owned Gram, cached in the context (see DeviceCtx::gram)
     ldk = (n + 1) / 2 * 2;  // keep rows 16-byte aligned
-    const hipError_t e = hipMalloc(&K, size_t(n) * size_t(ldk) * 8);
-    if (e != hipSuccess) {
-      set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s",
-                double(n) * double(ldk) * 8e-9, hipGetErrorString(e));
-      return SVM_ERR_OOM;
+    const size_t bytes = size_t(n) * size_t(ldk) * 8;
+    if (bytes > ctx->gram_bytes) {
+      if (ctx->gram) {
+        SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+        SVMD_CHECK(hipFree(ctx->gram));
+        ctx->gram = nullptr;
+        ctx->gram_bytes = 0;
+      }
+      const hipError_t e = hipMalloc(&ctx->gram, bytes);
+      if (e != hipSuccess) {
+        set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s", double(bytes) * 1e-9,
+                  hipGetErrorString(e));
+        return SVM_ERR_OOM;
+      }
+      ctx->gram_bytes = bytes;
     }
-    owned = true;
+    K = ctx->gram;
   }
   rc = gram_any(ctx, X_d, sqn_d, n, ld, kdim, mn_h, mx_h, d, gram_mode, q.gamma, K, ldk, gram_used);
   if (!rc && timing) {
@@ -330,18 +372,9 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
     rc = run_smo(ctx, K, ldk, y_d, n, alpha_d, warm, q, r, nullptr, 0);
   }
   if (!rc && r) {
-    std::vector<double> a(static_cast<size_t>(n));
-    const hipError_t e = hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-      set_error("svmd_train: %s", hipGetErrorString(e));
-      rc = SVM_ERR_DEVICE;
-    } else {
-      r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
-    }
-  }
-  if (owned) {
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(K);
+    int64_t c = 0;
+    rc = count_sv(ctx, alpha_d, n, 1, q.sv_tol, &c);
+    if (!rc) r->n_sv = c;
   }
   if (rc) return rc;
   if (timing) {
@@ -381,7 +414,8 @@ SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int
   if (gram_mode != 1 && mn_h && mx_h) plan_quant(mn_h, mx_h, d, &P);
   if (cache_bytes <= 0) {
     // Default: room for 16384 rows (an SMO touches a few thousand distinct rows at MNIST scale),
-    // capped at 60% of the free HBM.
+    // capped at 60% of the free HBM (after releasing a cached library-owned Gram).
+    svmd_release_cache(ctx);
     size_t fr = 0, tot = 0;
     SVMD_CHECK(hipMemGetInfo(&fr, &tot));
     cache_bytes = std::min<int64_t>(int64_t(double(fr) * 0.6), int64_t(16384) * ((n + 1) / 2 * 2) * 8);
@@ -397,9 +431,10 @@ SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int
   }
   if (gram_used) *gram_used = used;
   if (r) {
-    std::vector<double> a(static_cast<size_t>(n));
-    SVMD_CHECK(hipMemcpy(a.data(), alpha_d, size_t(n) * 8, hipMemcpyDeviceToHost));
-    r->n_sv = svm_sv_indices(a.data(), n, q.sv_tol, nullptr);
+    int64_t c = 0;
+    rc = count_sv(ctx, alpha_d, n, 1, q.sv_tol, &c);
+    if (rc) return rc;
+    r->n_sv = c;
   }
   return ctx->end();
 }

@@ -16,6 +16,12 @@ struct DeviceCtx {
   size_t ws_bytes = 0;
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
+  // Library-owned Gram (svmd_train* with K_d == NULL): kept between calls so a repeated fit of the
+  // same size neither re-allocates nor frees 10s of GB inside the timed region; freed by
+  // svmd_release_cache / svmd_destroy or when a larger one is needed.
+  double* gram = nullptr;
+  size_t gram_bytes = 0;
+  unsigned long long* count_d = nullptr;  // device counter for count_sv
   // Cached SMO iteration graph (smo.hip) and the argument key it was captured for.
   hipGraphExec_t smo_exec = nullptr;
   hipGraph_t smo_graph = nullptr;
@@ -120,6 +126,8 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
 // nclass cold-start solves on one Gram (Y, A: nclass x n, class-major): XCD teams (smo.hip).
+// Number of alpha[i] > tol for i < n (device reduction; one 8-byte read-back per row of alphas).
+int count_sv(DeviceCtx* ctx, const double* alpha, int64_t n, int64_t rows, double tol, int64_t* out);
 int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y, int64_t n, int nclass, double* A,
                   const svm_params& p, svm_result* r, int32_t* batched);
 

@@ -1444,4 +1444,44 @@ int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y
   return SVM_OK;
 }
 
+namespace {
+// counts[r] = #{i < n : alpha[r*n + i] > tol}; grid (x: row chunks, y: rows).
+__global__ __launch_bounds__(256) void count_above_kernel(const double* __restrict__ alpha, int64_t n, double tol,
+                                                          unsigned long long* __restrict__ counts) {
+  const int64_t r = blockIdx.y;
+  const double* a = alpha + r * n;
+  unsigned c = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    c += a[i] > tol ? 1u : 0u;
+  // wave64 sum, then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(counts + r, (unsigned long long)c);
+}
+}  // namespace
+
+int count_sv(DeviceCtx* ctx, const double* alpha, int64_t n, int64_t rows, double tol, int64_t* out) {
+  if (n <= 0 || rows <= 0) {
+    for (int64_t r = 0; r < rows; ++r) out[r] = 0;
+    return SVM_OK;
+  }
+  hipStream_t s = ctx->stream;
+  constexpr int64_t kMaxRows = 1024;
+  if (rows > kMaxRows) {
+    set_error("count_sv: %lld rows (max %lld)", (long long)rows, (long long)kMaxRows);
+    return SVM_ERR_ARG;
+  }
+  if (!ctx->count_d) SVMD_CHECK(hipMalloc(&ctx->count_d, kMaxRows * 8));
+  int rc = ctx->ensure_pinned(size_t(kMaxRows) * 8);
+  if (rc) return rc;
+  SVMD_CHECK(hipMemsetAsync(ctx->count_d, 0, size_t(rows) * 8, s));
+  const unsigned bx = unsigned(std::min<int64_t>((n + 255) / 256, 256));
+  hipLaunchKernelGGL(count_above_kernel, dim3(bx, unsigned(rows)), dim3(256), 0, s, alpha, n, tol, ctx->count_d);
+  SVMD_LAUNCH_CHECK();
+  auto* h = static_cast<unsigned long long*>(ctx->pinned);
+  SVMD_CHECK(hipMemcpyAsync(h, ctx->count_d, size_t(rows) * 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  for (int64_t r = 0; r < rows; ++r) out[r] = int64_t(h[r]);
+  return SVM_OK;
+}
+
 }  // namespace svm355

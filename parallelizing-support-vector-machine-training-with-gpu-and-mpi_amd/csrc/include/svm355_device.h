@@ -38,6 +38,9 @@ SVM_API int svmd_memcpy_d2h(void* ctx, void* dst_h, const void* src_d, int64_t b
 
 SVM_API void* svmd_create(int32_t device);
 SVM_API void svmd_destroy(void* ctx);
+// Free the Gram matrix the library allocated for svmd_train* with K_d == NULL (it is kept in the
+// context between calls so repeated fits of the same size do not re-allocate it).
+SVM_API int svmd_release_cache(void* ctx);
 // stream = hipStream_t of the caller (may be NULL = legacy default stream).  Work enqueued by the
 // context is ordered after everything already on that stream, and the caller's stream waits for
 // the context's work before each call returns.

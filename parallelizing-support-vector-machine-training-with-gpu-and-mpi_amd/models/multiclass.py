@@ -136,7 +136,8 @@ class OneVsRestSVC:
         mn, mx, sqn = D.minmax_scale_(Xd, d)
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
-        K, path = D.rbf_gram_sym(Xd, sqn, self.params.gamma, mn=mn, mx=mx, gram=self.gram)
+        K, path = D.rbf_gram_sym(Xd, sqn, self.params.gamma, mn=mn, mx=mx, gram=self.gram,
+                                 out=D.gram_buffer(X.shape[0], device))
         torch.cuda.synchronize(device)
         t2 = time.perf_counter()
         n = X.shape[0]

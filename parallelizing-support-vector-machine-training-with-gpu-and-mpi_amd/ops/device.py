@@ -228,6 +228,31 @@ def _host_stats(mn, mx):
     return a, b, int(a.shape[0])
 
 
+_GRAM_BUFS: dict = {}
+
+
+def gram_buffer(n: int, device) -> torch.Tensor:
+    """(n, ldk) float64 scratch Gram for the library's own transient use (SVC fit, one-vs-rest,
+    cascade solves): one grow-only buffer per (device, host thread), so repeated fits of the same or
+    smaller size never go back to the allocator — a fresh multi-GB device allocation can take
+    hundreds of milliseconds.  The view is overwritten by the next call on the same thread; free the
+    buffers with ``release_gram_buffers()``."""
+    device = torch.device(device)
+    ldk = (n + 1) // 2 * 2
+    key = (device.index if device.index is not None else torch.cuda.current_device(), threading.get_ident())
+    buf = _GRAM_BUFS.get(key)
+    if buf is None or buf.numel() < n * ldk:
+        _GRAM_BUFS.pop(key, None)
+        del buf
+        buf = _GRAM_BUFS[key] = torch.empty(n * ldk, dtype=torch.float64, device=device)
+    return buf[: n * ldk].view(n, ldk)
+
+
+def release_gram_buffers() -> None:
+    """Drop the cached Gram buffers of every thread (``gram_buffer``)."""
+    _GRAM_BUFS.clear()
+
+
 def gram_fits(n: int, device, fraction: float = 0.8) -> bool:
     """Does the full n x n float64 Gram fit in `fraction` of the free device memory?"""
     free, _ = torch.cuda.mem_get_info(torch.device(device))
@@ -259,6 +284,11 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
     if kcache == "rows":
         import time as _t
 
+        # the row cache sizes itself from the free HBM: hand this thread's scratch Gram back first
+        key = (X.device.index, threading.get_ident())
+        if _GRAM_BUFS.pop(key, None) is not None:
+            torch.cuda.empty_cache()
+
         t0 = _t.perf_counter()
         N.check(ctx.lib.svmd_train_rows(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],
                                         X.shape[1], N.ptr(y), N.ptr(alpha), int(warm), ctypes.byref(p),
@@ -277,7 +307,7 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
 
     ta = _t.perf_counter()
     if K is None:
-        K = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+        K = gram_buffer(n, X.device)
     alloc_ms = (_t.perf_counter() - ta) * 1e3
     tm = N.SvmdTiming()
     N.check(ctx.lib.svmd_train_q(ctx.bind(), N.ptr(X), N.ptr(sqn) if sqn is not None else None, n, X.shape[1],

@@ -122,10 +122,8 @@ class _HipBackend:
         sqn = D.row_norms(X, self.d)
         yd = torch.from_numpy(np.ascontiguousarray(y, dtype=np.int32)).to(self.device)
         ad = torch.from_numpy(np.ascontiguousarray(alpha, dtype=np.float64)).to(self.device)
-        K = torch.empty((m, (m + 1) // 2 * 2), dtype=torch.float64, device=self.device)
         mn, mx = self.stats if self.stats is not None else (None, None)
-        res, _ = D.train(X, sqn, yd, ad, self.params, warm=True, K=K, mn=mn, mx=mx)
-        del K
+        res, _ = D.train(X, sqn, yd, ad, self.params, warm=True, K=D.gram_buffer(m, self.device), mn=mn, mx=mx)
         return ad.cpu().numpy(), res
 
     def select(self, X: torch.Tensor, idx: np.ndarray) -> torch.Tensor:
