@@ -113,6 +113,8 @@ def _cascade(argv) -> int:
             args += ["--json", a.json]
         if a.model_dir:
             args += ["--model-dir", a.model_dir]
+        if a.checkpoint_dir:
+            args += ["--checkpoint-dir", a.checkpoint_dir] + (["--resume"] if a.resume else [])
         return _native("svm_cascade", args)
 
     if "RANK" not in os.environ and a.gpus > 0:

@@ -3,6 +3,7 @@
 // (classical).
 //
 //   svm_cascade [--topology star|tree] [--gpus P] [--transport auto|rccl|loopback] [--max-rounds R]
+//               [--checkpoint-dir D [--resume]]   (per-round state, cascade.h cascade_state.bin)
 //               [the svm_gpu options: --dataset | --train/--test | --synthetic N[,M] | --C ... --json F
 //                --model-dir D --quiet]
 //
@@ -37,6 +38,7 @@ namespace {
 void usage(const char* prog) {
   fprintf(stderr,
           "usage: %s [--topology star|tree] [--gpus P] [--transport auto|rccl|loopback] [--max-rounds R]\n"
+          "       [--checkpoint-dir D [--resume]]\n"
           "       [svm_gpu options, see svm_gpu --help]\n",
           prog);
 }
@@ -46,6 +48,8 @@ void usage(const char* prog) {
 int main(int argc, char** argv) {
   std::string topology = "star", transport = "auto";
   int P = 1, max_rounds = 50;
+  std::string checkpoint_dir;
+  bool resume = false;
   std::vector<char*> rest{argv[0]};
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -60,6 +64,8 @@ int main(int argc, char** argv) {
     else if (a == "--gpus") P = atoi(val().c_str());
     else if (a == "--transport") transport = val();
     else if (a == "--max-rounds") max_rounds = atoi(val().c_str());
+    else if (a == "--checkpoint-dir") checkpoint_dir = val();
+    else if (a == "--resume") resume = true;
     else if (a == "-h" || a == "--help") {
       usage(argv[0]);
       cli::usage(argv[0]);
@@ -115,6 +121,8 @@ int main(int argc, char** argv) {
   cfg.max_rounds = max_rounds;
   cfg.params = o.p;
   cfg.log = true;
+  cfg.checkpoint_dir = checkpoint_dir;
+  cfg.resume = resume;
 
   std::vector<CascadeOutput> outs(static_cast<size_t>(P));
   std::vector<void*> ctxs(size_t(P), nullptr);

@@ -10,6 +10,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <filesystem>
+#include <fstream>
 #include <numeric>
 #include <stdexcept>
 #include <unordered_set>
@@ -251,6 +253,71 @@ class Rank {
     return o;
   }
 
+  // ---- checkpoint (rank 0): packed records through the host
+  std::vector<double> pack_host(const SvSet& S) {
+    std::vector<double> h(size_t(S.k) * size_t(w_));
+    if (!S.k) return h;
+    pack_into(S, pack_, S.k);
+    HIPC(hipMemcpyAsync(h.data(), pack_.p, h.size() * 8, hipMemcpyDeviceToHost, stream_));
+    HIPC(hipStreamSynchronize(stream_));
+    return h;
+  }
+  SvSet unpack_host(const std::vector<double>& h, int64_t k) {
+    pack_.ensure(std::max<int64_t>(k, 1) * w_ * 8);
+    if (k) {
+      sync();
+      HIPC(hipMemcpyAsync(pack_.p, h.data(), size_t(k) * size_t(w_) * 8, hipMemcpyHostToDevice, stream_));
+      HIPC(hipStreamSynchronize(stream_));
+    }
+    return unpack(pack_.as<double>(), k);
+  }
+  void save_checkpoint(const std::string& dir, bool tree, int64_t next_round, double b, const SvSet& G) {
+    const std::vector<double> recs = pack_host(G);
+    std::filesystem::create_directories(dir);
+    const std::string path = dir + "/cascade_state.bin", tmp = path + ".tmp";
+    {
+      std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+      if (!f) throw std::runtime_error("cannot write checkpoint " + tmp);
+      const int32_t topo = tree ? 1 : 0, reserved = 0;
+      const int64_t d = d_, ld = ld_, k = G.k;
+      f.write(kCheckpointMagic, 8);
+      f.write(reinterpret_cast<const char*>(&topo), 4);
+      f.write(reinterpret_cast<const char*>(&reserved), 4);
+      f.write(reinterpret_cast<const char*>(&next_round), 8);
+      f.write(reinterpret_cast<const char*>(&b), 8);
+      f.write(reinterpret_cast<const char*>(&d), 8);
+      f.write(reinterpret_cast<const char*>(&ld), 8);
+      f.write(reinterpret_cast<const char*>(&k), 8);
+      f.write(reinterpret_cast<const char*>(recs.data()), std::streamsize(recs.size() * 8));
+      if (!f) throw std::runtime_error("short write on checkpoint " + tmp);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
+  }
+  // Returns false when there is no checkpoint file; throws when it does not match this run.
+  bool load_checkpoint(const std::string& dir, bool tree, int64_t* next_round, double* b, SvSet* G) {
+    std::ifstream f(dir + "/cascade_state.bin", std::ios::binary);
+    if (!f) return false;
+    char magic[8];
+    int32_t topo = 0, reserved = 0;
+    int64_t d = 0, ld = 0, k = 0;
+    f.read(magic, 8);
+    f.read(reinterpret_cast<char*>(&topo), 4);
+    f.read(reinterpret_cast<char*>(&reserved), 4);
+    f.read(reinterpret_cast<char*>(next_round), 8);
+    f.read(reinterpret_cast<char*>(b), 8);
+    f.read(reinterpret_cast<char*>(&d), 8);
+    f.read(reinterpret_cast<char*>(&ld), 8);
+    f.read(reinterpret_cast<char*>(&k), 8);
+    if (!f || std::memcmp(magic, kCheckpointMagic, 8) != 0) throw std::runtime_error("not a cascade checkpoint");
+    if (topo != (tree ? 1 : 0) || d != d_ || ld != ld_ || k < 0)
+      throw std::runtime_error("checkpoint does not match this cascade configuration");
+    std::vector<double> recs(size_t(k) * size_t(w_));
+    f.read(reinterpret_cast<char*>(recs.data()), std::streamsize(recs.size() * 8));
+    if (!f) throw std::runtime_error("truncated cascade checkpoint");
+    *G = unpack_host(recs, k);
+    return true;
+  }
+
   // ---- exchanges
   SvSet bcast_set(const SvSet& G) {  // G meaningful on rank 0
     Trace tr("cascade:bcast_svs");
@@ -376,8 +443,17 @@ CascadeOutput run_cascade(Transport& t, void* ctx, const double* X_host, const i
   SvSet G = R.empty();  // global SV set (meaningful on rank 0; broadcast each round)
   std::unordered_set<int64_t> global_ids;
   double b = 0.0;
-  auto tr_prev = Clock::now();
   int rnd = 0;
+  if (cfg.resume && !cfg.checkpoint_dir.empty()) {
+    int64_t has = 0, next = 0;
+    if (me == 0) has = R.load_checkpoint(cfg.checkpoint_dir, cfg.tree, &next, &b, &G) ? 1 : 0;
+    if (t.bcast_i64(has, 0)) {
+      rnd = int(t.bcast_i64(next, 0));
+      global_ids = std::unordered_set<int64_t>(G.ids.begin(), G.ids.end());
+      if (log) printf("[rank 0] resumed from checkpoint at round %d, SV count = %lld\n", rnd, (long long)G.k);
+    }
+  }
+  auto tr_prev = Clock::now();
   bool converged = false;
   while (rnd < cfg.max_rounds && !converged) {
     const int shown = cfg.tree ? rnd + 1 : rnd;
@@ -450,6 +526,7 @@ CascadeOutput run_cascade(Transport& t, void* ctx, const double* X_host, const i
           printf("[rank 0] Not converged yet. New SV count = %lld\n", (long long)G.k);
         fflush(stdout);
       }
+      if (!cfg.checkpoint_dir.empty()) R.save_checkpoint(cfg.checkpoint_dir, cfg.tree, rnd + 1, b, G);
     }
     converged = t.bcast_i64(same, 0) != 0;
     ++rnd;

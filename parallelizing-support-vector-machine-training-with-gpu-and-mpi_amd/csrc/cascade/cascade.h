@@ -22,7 +22,16 @@ struct CascadeConfig {
   int max_rounds = 50;  // mpi_svm_main3.cpp:544, mpi_svm_main2.cpp:428
   svm_params params{};  // C, gamma, tau, eps, sv_tol, max_iter
   bool log = true;      // rank 0 prints the reference's per-round lines
+  // Per-round checkpoint: rank 0 writes <checkpoint_dir>/cascade_state.bin after every
+  // round (global SV set with alphas, b, next round); resume = start from that file if present.
+  std::string checkpoint_dir;
+  bool resume = false;
 };
+
+// cascade_state.bin layout (little-endian): char magic[8] = "SVM355C1"; int32 topology (0 star,
+// 1 tree); int32 reserved; int64 next_round; double b; int64 d; int64 ld; int64 k; then k records of
+// ld + 3 doubles [scaled row (ld, zero padded) | y | alpha | global id].
+constexpr char kCheckpointMagic[9] = "SVM355C1";
 
 struct CascadeOutput {
   // Final global SV set (every rank holds it after the final broadcast).

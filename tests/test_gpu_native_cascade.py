@@ -68,3 +68,27 @@ def test_native_rccl_single_rank_equals_loopback(tmp_path, topology):
     lb, _ = _native(tmp_path, topology, 1, "loopback")
     assert rc["transport"] == "rccl" and lb["transport"] == "loopback"
     assert rc["sv_ids"] == lb["sv_ids"] and rc["b"] == lb["b"] and rc["rounds"] == lb["rounds"]
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_native_checkpoint_resume_matches_uninterrupted_run(tmp_path, topology):
+    """Stop after 2 rounds with a checkpoint, resume from it: the same rounds, SV ids and b, bit for
+    bit, as one uninterrupted run (the carried state is exactly the global SV set and b)."""
+    full, _ = _native(tmp_path, topology, 2, "loopback")
+    ck = tmp_path / f"ck_{topology}"
+
+    def run(extra, name):
+        out = tmp_path / name
+        r = subprocess.run([str(EXE), "--synthetic", f"{N},{M}", "--topology", topology, "--gpus", "2",
+                            "--transport", "loopback", "--json", str(out), "--quiet", *extra],
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return json.loads(out.read_text()), r.stdout
+
+    part, _ = run(["--max-rounds", "2", "--checkpoint-dir", str(ck)], "part.json")
+    assert part["rounds"] == 2 and not part["converged"] and (ck / "cascade_state.bin").exists()
+    res, stdout = run(["--checkpoint-dir", str(ck), "--resume"], "resumed.json")
+    assert "[rank 0] resumed from checkpoint at round 2" in stdout
+    assert res["converged"] and res["rounds"] == full["rounds"]
+    assert res["sv_ids"] == full["sv_ids"] and res["b"] == full["b"]
+    assert res["test_correct"] == full["test_correct"]
