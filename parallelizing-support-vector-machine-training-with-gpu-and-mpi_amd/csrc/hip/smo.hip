@@ -1012,6 +1012,21 @@ unsigned long long register_ticks() {
   return kRegisterTicks;
 }
 
+// Dynamic LDS reserved (unused) by the XCD-local launches so that at most one workgroup lands on a
+// CU: the team then spreads over the XCD's CUs instead of doubling up, e.g. 2.75 instead of 3.25
+// us/iter at n = 24k (SVM355_PSMO_LDS overrides; 0 = none).  1024-thread workgroups need none.
+size_t xcd_lds_pad(int NT) {
+  if (const char* v = getenv("SVM355_PSMO_LDS")) return size_t(std::max(0, atoi(v)));
+  return NT == 1024 ? 0 : size_t(96) << 10;
+}
+
+template <class Kern>
+void allow_lds(Kern k, size_t bytes) {
+  if (bytes > (size_t(64) << 10))
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(bytes));
+}
+
 // Launch the persistent solver for a (threads per workgroup NT, elements per thread E) shape.
 template <int NT, int E>
 int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
@@ -1023,14 +1038,18 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
   if (xlocal) {
     // Over-provisioned grid: ~2*G workgroups per XCD under round-robin dispatch; G of XCD 0's join.
     const int grid = 16 * G;
-    if (sv && atoi(sv))
-      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha, f,
-                         n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G,
-                         register_ticks());
-    else
-      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, true>), dim3(grid), dim3(NT), 0, s, K, ldk, y, alpha,
+    const size_t lds = xcd_lds_pad(NT);
+    if (sv && atoi(sv)) {
+      allow_lds(smo_persistent_kernel<NT, E, true, true>, lds);
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, true, true>), dim3(grid), dim3(NT), lds, s, K, ldk, y, alpha,
                          f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G,
                          register_ticks());
+    } else {
+      allow_lds(smo_persistent_kernel<NT, E, false, true>, lds);
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, true>), dim3(grid), dim3(NT), lds, s, K, ldk, y, alpha,
+                         f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22, stamps, G,
+                         register_ticks());
+    }
     SVMD_LAUNCH_CHECK();
     return SVM_OK;
   }
@@ -1050,7 +1069,6 @@ int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, cons
 constexpr int kDefaultNT = 512;
 constexpr int kXcdMaxG = 32;              // workgroups of the XCD-local solver (one XCD has 32 CUs)
 constexpr int64_t kXcdDefaultMax = 65536;  // default n limit of the XCD-local solver (tuned on MI355X)
-constexpr int64_t kXcdWideFrom = 24000;    // above this the XCD-local solver uses 1024-thread workgroups
 constexpr int64_t kSingleDefaultMax = 2048;  // auto mode: single workgroup up to this n (tuned on MI355X)
 constexpr int kSingleDefaultNT = 512;
 int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out, int gcap) {
@@ -1058,11 +1076,10 @@ int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out, int gcap) {
   if (const char* v = getenv("SVM355_PSMO_WG")) target = std::max(1, std::min(kMaxG, atoi(v)));
   if (gcap > 0) target = std::min(target, gcap);
   // Measured on MI355X (profiles/r1_smo_launch_shape.txt): the XCD-local solver wants 256-thread
-  // workgroups up to ~16k points and 1024-thread ones (E <= 2, <= 30 workgroups) from 24k to 64k,
-  // where it beats the device-wide exchange by 3-7 % per iteration.
+  // workgroups up to ~16k points and 512-thread ones above, one per CU (xcd_lds_pad): 2.45-3.44
+  // us/iter from 10k to 60k, 4-17 % below the device-wide exchange.
   int nt = kDefaultNT;
   if (gcap > 0 && n <= 16000) nt = 256;
-  if (gcap > 0 && n > kXcdWideFrom) nt = 1024;
   if (const char* v = getenv("SVM355_PSMO_NT")) nt = atoi(v);
   if (nt != 256 && nt != 512 && nt != 1024) nt = kDefaultNT;
   const int emax = nt == 256 ? 16 : nt == 512 ? 8 : 4;
@@ -1364,8 +1381,10 @@ template <int NT, int E>
 void launch_multi_e(hipStream_t s, int grid, const double* K, int64_t ldk, const int32_t* Y, double* A, double* F,
                     int64_t n, unsigned long long* slots, SmoState* st, int nclass, const svm_params& p, unsigned* ctl,
                     int G) {
-  hipLaunchKernelGGL((smo_multi_kernel<NT, E>), dim3(grid), dim3(NT), 0, s, K, ldk, Y, A, F, n, int64_t(NT) * E, slots,
-                     st, nclass, p.C, p.eps, p.tau, p.max_iter, ctl, int64_t(1) << 22, G, register_ticks());
+  const size_t lds = xcd_lds_pad(NT);
+  allow_lds(smo_multi_kernel<NT, E>, lds);
+  hipLaunchKernelGGL((smo_multi_kernel<NT, E>), dim3(grid), dim3(NT), lds, s, K, ldk, Y, A, F, n, int64_t(NT) * E,
+                     slots, st, nclass, p.C, p.eps, p.tau, p.max_iter, ctl, int64_t(1) << 22, G, register_ticks());
 }
 }  // namespace
 
@@ -1380,7 +1399,7 @@ int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y
   std::vector<SmoState> fin(static_cast<size_t>(nclass));
   int G = 0, E = 0, NT = 0;
   bool ok = nclass < 1000 && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT, kXcdMaxG);
-  ok = ok && ((NT == 256 && E <= 2) || (NT == 512 && E <= 2) || (NT == 1024 && E <= 4));
+  ok = ok && ((NT == 256 && E <= 2) || (NT == 512 && E <= 4));
   if (const char* v = getenv("SVM355_SMO_MULTI"); v && atoi(v) == 0) ok = false;
   if (batched) *batched = 0;
   if (ok) {
@@ -1410,7 +1429,7 @@ int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y
     if (false) {
     }
     SVM_MULTI_CASE(256, 1) SVM_MULTI_CASE(256, 2) SVM_MULTI_CASE(512, 1) SVM_MULTI_CASE(512, 2)
-    SVM_MULTI_CASE(1024, 1) SVM_MULTI_CASE(1024, 2) SVM_MULTI_CASE(1024, 4)
+    SVM_MULTI_CASE(512, 4)
 #undef SVM_MULTI_CASE
     SVMD_LAUNCH_CHECK();
     unsigned herr = 0;

@@ -22,7 +22,7 @@ K, _ = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
 yd = torch.from_numpy(tr.y).to(dev)
 os.environ["SVM355_SMO"] = "persistent"
 os.environ["SVM355_PSMO_STAMP"] = "2"
-for xcd in ("0", "1") if n <= 30000 else ("0",):
+for xcd in ("0", "1"):
     os.environ["SVM355_PSMO_XCD"] = xcd
     print(f"--- n={n} xcd-local={xcd}", file=sys.stderr, flush=True)
     a = torch.zeros(n, dtype=torch.float64, device=dev)

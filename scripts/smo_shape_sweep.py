@@ -17,10 +17,14 @@ from svm355.utils.data import synthetic_mnist  # noqa: E402
 
 VARIANTS = {
     "device-wide NT=512": {"SVM355_PSMO_XCD": "0", "SVM355_PSMO_NT": "512"},
-    "xcd-local NT=512": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "512"},
-    "xcd-local NT=1024": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "1024"},
+    "xcd NT=1024": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "1024", "SVM355_PSMO_LDS": "0"},
+    "xcd NT=512": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "512", "SVM355_PSMO_LDS": "0"},
+    "xcd NT=512 1/CU": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "512", "SVM355_PSMO_LDS": "98304"},
+    "xcd NT=256": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "256", "SVM355_PSMO_LDS": "0"},
+    "xcd NT=256 1/CU": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "256", "SVM355_PSMO_LDS": "98304"},
     "default": {},
 }
+KNOBS = ("SVM355_PSMO_XCD", "SVM355_PSMO_NT", "SVM355_PSMO_LDS")
 sizes = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16000,24000,30000,40000,50000,60000").split(",")]
 dev = torch.device("cuda:0")
 p = SVMParams()
@@ -32,7 +36,7 @@ for n in sizes:
     y = torch.from_numpy(tr.y).to(dev)
     ref = None
     for name, env in VARIANTS.items():
-        for k in ("SVM355_PSMO_XCD", "SVM355_PSMO_NT"):
+        for k in KNOBS:
             os.environ.pop(k, None)
         os.environ.update(env)
         ts = []
@@ -46,8 +50,8 @@ for n in sizes:
         sig = (r.iterations, r.b)
         ref = ref or sig
         best = min(ts[1:])
-        print(f"n={n:6d} {name:20s} smo {best:7.2f} ms  {best * 1e3 / r.iterations:6.3f} us/iter  "
+        print(f"n={n:6d} {name:18s} smo {best:7.2f} ms  {best * 1e3 / r.iterations:6.3f} us/iter  "
               f"iters {r.iterations}  identical={sig == ref}", flush=True)
-    for k in ("SVM355_PSMO_XCD", "SVM355_PSMO_NT"):
+    for k in KNOBS:
         os.environ.pop(k, None)
     del K
