@@ -172,6 +172,10 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       if (EXTRA) xacc[j][r] = 0.0;
     }
 
+  // After an extra group's flush the next k-step starts its accumulators from the inline constant 0
+  // (an MFMA operand) instead of zeroing 32 registers per lane with v_mov.
+  bool fresh = false;
+  const i32x16 zero16 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int k0 = 0; k0 < kq; k0 += BK) {
     __syncthreads();
 #pragma unroll
@@ -190,8 +194,14 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj)
         b[nj] = *reinterpret_cast<const i32x4*>(Bs + (nj * 32 + l32) * QLS + ks * 32 + 16 * h);
+      if (EXTRA && fresh) {
 #pragma unroll
-      for (int nj = 0; nj < 2; ++nj) acc[nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[nj], acc[nj], 0, 0, 0);
+        for (int nj = 0; nj < 2; ++nj) acc[nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[nj], zero16, 0, 0, 0);
+        fresh = false;
+      } else {
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) acc[nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[nj], acc[nj], 0, 0, 0);
+      }
       if (EXTRA) {
         const int step = k0 / 32 + ks;
         if (step < main_step0) {
@@ -200,10 +210,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 #pragma unroll
             for (int nj = 0; nj < 2; ++nj)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                xacc[nj][r] += wgt * double(acc[nj][r]);
-                acc[nj][r] = 0;
-              }
+              for (int r = 0; r < 16; ++r) xacc[nj][r] += wgt * double(acc[nj][r]);
+            fresh = true;
           }
         }
       }
