@@ -116,6 +116,7 @@ _HIP_SIGS = {
     "svmd_smo": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
                            POINTER(SvmResult), _P, c_int64]),
     "svmd_release_cache": (c_int32, [c_void_p]),
+    "svmd_selftest_exp": (c_int32, [c_void_p, _P, c_int64, _P, _P]),
     "svmd_smo_multi": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, c_int32, _P, POINTER(SvmParams),
                                  POINTER(SvmResult), POINTER(c_int32)]),
     "svmd_train": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, c_int64, _P, _P, c_int32,

@@ -129,6 +129,15 @@ SVM_API void svmd_destroy(void* h) {
   delete ctx;
 }
 
+SVM_API int svmd_selftest_exp(void* h, const double* x_d, int64_t n, double* lib_d, double* batch_d) {
+  SVMD_CTX(h);
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = exp_selftest(ctx->stream, x_d, n, lib_d, batch_d);
+  if (rc) return rc;
+  return ctx->end();
+}
+
 SVM_API int svmd_release_cache(void* h) {
   SVMD_CTX(h);
   if (ctx->gram) {

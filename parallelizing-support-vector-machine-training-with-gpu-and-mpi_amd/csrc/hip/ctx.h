@@ -126,6 +126,8 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
 // nclass cold-start solves on one Gram (Y, A: nclass x n, class-major): XCD teams (smo.hip).
+// exp self-test (igram.hip): device libm exp and the Gram epilogue's batched exp of x[0..n).
+int exp_selftest(hipStream_t s, const double* x, int64_t n, double* out_lib, double* out_batch);
 // Number of alpha[i] > tol for i < n (device reduction; one 8-byte read-back per row of alphas).
 int count_sv(DeviceCtx* ctx, const double* alpha, int64_t n, int64_t rows, double tol, int64_t* out);
 int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y, int64_t n, int nclass, double* A,

@@ -99,6 +99,66 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
   if (__any(bad) && lane == 0) atomicOr(fail, 1u);
 }
 
+// ---- exp over a batch of lanes' values, bit-identical to the device libm exp (same operation
+// sequence: x*log2e, round-to-even, two-part ln2 reduction, degree-11 polynomial in 12 FMAs,
+// ldexp, overflow/underflow clamps).  Evaluating B values per coefficient lets one VGPR copy of
+// each 64-bit coefficient serve all B FMAs; a scalar libm call reloads all twelve per value
+// (two v_mov each), which made v_mov the most frequent instruction of the Gram kernel.
+__device__ __forceinline__ constexpr double hexd(uint64_t u) { return __builtin_bit_cast(double, u); }
+// d = a * b + c with the wave-uniform c read from an SGPR pair (VOP3 src2): the compiler would
+// otherwise copy the constant into the tied destination of v_fmac_f64 before every use.
+__device__ __forceinline__ double fma_s(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+template <int B>
+__device__ __forceinline__ void exp_batch(double (&x)[B]) {
+  constexpr double kC[10] = {hexd(0x3ec71dee623fde64ull), hexd(0x3efa01997c89e6b0ull), hexd(0x3f2a01a014761f6eull),
+                             hexd(0x3f56c16c1852b7b0ull), hexd(0x3f81111111122322ull), hexd(0x3fa55555555502a1ull),
+                             hexd(0x3fc5555555555511ull), hexd(0x3fe000000000000bull), 1.0, 1.0};
+  double n[B], r[B], p[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) n[i] = __builtin_rint(x[i] * hexd(0x3ff71547652b82feull));
+#pragma unroll
+  for (int i = 0; i < B; ++i) r[i] = __builtin_fma(hexd(0xbfe62e42fefa39efull), n[i], x[i]);
+#pragma unroll
+  for (int i = 0; i < B; ++i) r[i] = __builtin_fma(hexd(0xbc7abc9e3b39803full), n[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < B; ++i) p[i] = fma_s(hexd(0x3e5ade156a5dcb37ull), r[i], hexd(0x3e928af3fca7ab0cull));
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int i = 0; i < B; ++i) p[i] = fma_s(r[i], p[i], kC[c]);
+#pragma unroll
+  for (int c = 8; c < 10; ++c)  // + 1.0 twice: an inline constant
+#pragma unroll
+    for (int i = 0; i < B; ++i) p[i] = __builtin_fma(r[i], p[i], kC[c]);
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    double e = __builtin_ldexp(p[i], int(n[i]));
+    e = x[i] > 1024.0 ? __builtin_inf() : e;
+    x[i] = x[i] < -1075.0 ? 0.0 : e;
+  }
+}
+
+// Self-test hook: out_lib[i] = exp(x[i]) (device libm), out_batch[i] = exp_batch (8 per lane).
+__global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict__ x, int64_t n,
+                                                        double* __restrict__ out_lib,
+                                                        double* __restrict__ out_batch) {
+  const int64_t base = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) * 8;
+  double v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = base + i < n ? x[base + i] : 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (base + i < n) out_lib[base + i] = exp(v[i]);
+  exp_batch<8>(v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (base + i < n) out_batch[base + i] = v[i];
+}
+
 // Upper-triangular 128x128 tiles of K = exp(-gamma * dist), each split into two 128x64 halves
 // (one workgroup each: 4 waves x 32 rows x 64 columns, 2 MFMA 32x32 tiles per wave), each
 // off-diagonal tile also stored transposed.  kq = int8 columns (multiple of BK); columns
@@ -223,24 +283,41 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
   double* im = img + w * (32 * 33);
   const bool mirror = tm != tn;
+  // Interior tiles (the vast majority) skip the per-element bounds tests; store addresses are a
+  // per-lane base plus a wave-uniform (scalar) row offset.
+  const bool interior = bm + QBM <= n && bn + QBM <= n;
+  const int64_t row0 = bm + w * 32 + 4 * h;  // this lane's row for r = 0
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj) {
     const int cl = bj * 32 + l32;
     const int64_t gj = bn + cl;
     const int32_t nbj = n0_c[cl];
     const double wbj = EXTRA ? wn_c[cl] : 0.0;
+    double* kp = K + row0 * ldk + gj;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int64_t gi = bm + w * 32 + rl;
-      const int32_t D0 = n0_r[w * 32 + rl] + nbj - 2 * acc[bj][r];  // exact
-      double dist = w0 * double(D0);
-      if (EXTRA) dist += (wn_r[w * 32 + rl] + wbj) - 2.0 * xacc[bj][r];
-      dist = dist > 0.0 ? dist : 0.0;
-      double kv = exp(neg_gamma * dist);
-      if (gi == gj) kv = 1.0;
-      if (gi < n && gj < n) __builtin_nontemporal_store(kv, K + gi * ldk + gj);
-      if (mirror) im[l32 * 33 + rl] = kv;  // im[col][row]
+    for (int half = 0; half < 2; ++half) {
+      double ex[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 8 * half + q;
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int32_t D0 = n0_r[w * 32 + rl] + nbj - 2 * acc[bj][r];  // exact
+        double dist = w0 * double(D0);
+        if (EXTRA) dist += (wn_r[w * 32 + rl] + wbj) - 2.0 * xacc[bj][r];
+        dist = dist > 0.0 ? dist : 0.0;
+        ex[q] = neg_gamma * dist;
+      }
+      exp_batch<8>(ex);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 8 * half + q;
+        const int ro = (r & 3) + 8 * (r >> 2);
+        const int rl = ro + 4 * h;
+        const int64_t gi = row0 + ro;
+        const double kv = gi == gj ? 1.0 : ex[q];
+        if (interior || (gi < n && gj < n)) __builtin_nontemporal_store(kv, kp + int64_t(ro) * ldk);
+        if (mirror) im[l32 * 33 + rl] = kv;  // im[col][row]
+      }
     }
     if (mirror) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -250,13 +327,16 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       // store instruction writes 4 whole 256-byte row segments.
       const int chunk = lane & 15;
       const int64_t gcol = bm + w * 32 + 2 * chunk;
+      const int64_t mrow0 = bn + bj * 32 + (lane >> 4);
+      double* mp = K + mrow0 * ldk + gcol;
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int mrow = it * 4 + (lane >> 4);
-        const int64_t grow = bn + bj * 32 + mrow;
         const double* sp = im + mrow * 33 + 2 * chunk;
-        if (grow < n) {
-          double* dst = K + grow * ldk + gcol;
+        double* dst = mp + int64_t(4 * it) * ldk;
+        if (interior) {
+          __builtin_nontemporal_store(f64x2{sp[0], sp[1]}, reinterpret_cast<f64x2*>(dst));
+        } else if (mrow0 + 4 * it < n) {
           if (gcol + 1 < n)
             __builtin_nontemporal_store(f64x2{sp[0], sp[1]}, reinterpret_cast<f64x2*>(dst));
           else if (gcol < n)
@@ -271,6 +351,13 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 }
 
 }  // namespace
+
+int exp_selftest(hipStream_t s, const double* x, int64_t n, double* out_lib, double* out_batch) {
+  if (n <= 0) return SVM_OK;
+  hipLaunchKernelGGL(exp_check_kernel, dim3(unsigned((n + 2047) / 2048)), dim3(256), 0, s, x, n, out_lib, out_batch);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
 
 // Host-side column plan (from the training min/max): the main group (most common range) and the
 // extra groups, each padded to a 32-column k-step, with per-column centring offsets.

@@ -41,6 +41,9 @@ SVM_API void svmd_destroy(void* ctx);
 // Free the Gram matrix the library allocated for svmd_train* with K_d == NULL (it is kept in the
 // context between calls so repeated fits of the same size do not re-allocate it).
 SVM_API int svmd_release_cache(void* ctx);
+// Self-test of the Gram epilogue's exp: lib_d[i] = device libm exp(x_d[i]), batch_d[i] = the
+// batched evaluation the Gram kernel uses (they must agree bit for bit).
+SVM_API int svmd_selftest_exp(void* ctx, const double* x_d, int64_t n, double* lib_d, double* batch_d);
 // stream = hipStream_t of the caller (may be NULL = legacy default stream).  Work enqueued by the
 // context is ordered after everything already on that stream, and the caller's stream waits for
 // the context's work before each call returns.

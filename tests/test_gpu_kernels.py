@@ -514,3 +514,27 @@ def test_ovr_batched_xcd_teams_equal_per_class_solves(dev, n):
     np.testing.assert_array_equal(b.intercepts_b_, s.intercepts_b_)
     np.testing.assert_array_equal(b.support_, s.support_)
     np.testing.assert_array_equal(b.dual_coef_, s.dual_coef_)
+
+
+def test_gram_epilogue_exp_is_bit_identical_to_libm(dev):
+    """The Gram kernel's batched exp (SGPR-sourced FMAs, igram.hip exp_batch) must equal the device
+    libm exp bit for bit, so the Gram -- and every SMO trajectory -- is unchanged by it."""
+    from svm355 import _native as N
+    from svm355.ops.device import DeviceContext
+
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([
+        rng.uniform(-1.0, 0.0, 200000), rng.uniform(-40.0, 40.0, 50000), rng.uniform(-1100.0, 1100.0, 50000),
+        np.array([0.0, -0.0, 1e-300, -1e-300, 5e-324, -5e-324, 1024.0, 1024.0000000000002, -1075.0,
+                  -1075.0000000000002, -745.2, -708.4, 709.78, 709.79, -1e-17, np.inf, -np.inf, np.nan]),
+    ])
+    x = torch.from_numpy(xs).to(dev)
+    lib = torch.empty_like(x)
+    bat = torch.empty_like(x)
+    ctx = DeviceContext.get(dev)
+    N.check(ctx.lib.svmd_selftest_exp(ctx.bind(), N.ptr(x), x.numel(), N.ptr(lib), N.ptr(bat)), "svmd_selftest_exp")
+    torch.cuda.synchronize()
+    a = lib.cpu().numpy().view(np.uint64)
+    b = bat.cpu().numpy().view(np.uint64)
+    bad = np.flatnonzero(a != b)
+    assert bad.size == 0, [(xs[i], lib.cpu().numpy()[i], bat.cpu().numpy()[i]) for i in bad[:5]]
