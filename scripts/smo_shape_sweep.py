@@ -24,6 +24,8 @@ VARIANTS = {
     "xcd NT=256 1/CU": {"SVM355_PSMO_XCD": "1", "SVM355_PSMO_NT": "256", "SVM355_PSMO_LDS": "98304"},
     "default": {},
 }
+if os.environ.get("SHAPE_QUICK"):
+    VARIANTS = {k: VARIANTS[k] for k in ("device-wide NT=512", "default")}
 KNOBS = ("SVM355_PSMO_XCD", "SVM355_PSMO_NT", "SVM355_PSMO_LDS")
 sizes = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16000,24000,30000,40000,50000,60000").split(",")]
 dev = torch.device("cuda:0")
