@@ -54,6 +54,10 @@ def compact_pixels(X: np.ndarray) -> Optional[np.ndarray]:
         return X
     if X.size == 0:
         return None
+    if X.dtype.kind == "f" and not np.isfinite(X).all():
+        return None
+    if X.min() < 0 or X.max() > 255:
+        return None
     Xc = X.astype(np.uint8)
     return Xc if np.array_equal(Xc, X) else None
 
