@@ -131,6 +131,7 @@ _HIP_SIGS = {
     "svmd_decision": (c_int32, [c_void_p, _P, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
                                 c_double, c_double, _P]),
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
+    "svmd_count_correct": (c_int32, [c_void_p, _P, _P, c_int64, c_int32, POINTER(c_int64)]),
     "svmd_trace_push": (None, [c_char_p]),
     "svmd_trace_pop": (None, []),
 }

@@ -203,9 +203,12 @@ int main(int argc, char** argv) {
     }
     ck(svmd_decision(ctx, nsv ? R0.X_d : nullptr, nsv ? nsq : nullptr, nsv ? coef : nullptr, nsv, ld, Xq, nq, m, ld,
                      ld, o.p.gamma, R0.b, out));
-    std::vector<double> dec(static_cast<size_t>(m));
-    ck(svmd_memcpy_d2h(ctx, dec.data(), out, m * 8));
-    for (int64_t i = 0; i < m; ++i) correct += ((dec[size_t(i)] >= 0 ? 1 : -1) == te.y[size_t(i)]);
+    // s >= 0 -> +1 (M3 :800), counted on the device
+    auto* yq = static_cast<int32_t*>(alloc(m * 4));
+    ck(svmd_memcpy_h2d(ctx, yq, te.y.data(), m * 4));
+    int64_t c = 0;
+    ck(svmd_count_correct(ctx, out, yq, m, 1, &c));
+    correct = c;
     for (void* p : bufs) svmd_free(ctx, p);
     printf("[rank 0] Test accuracy (final model) = %g (%lld/%lld)\n", double(correct) / double(m), correct,
            (long long)m);

@@ -130,9 +130,12 @@ int main(int argc, char** argv) {
       CK(svmd_memcpy_h2d(dev.ctx, nsq, nsh.data(), nsv * 8));
     }
     CK(svmd_decision(dev.ctx, Xs, nsq, coef, nsv, ld, Xq, nq, m, ld, ld, o.p.gamma, r.b, out));
-    std::vector<double> dec(static_cast<size_t>(m));
-    CK(svmd_memcpy_d2h(dev.ctx, dec.data(), out, m * 8));
-    for (long long i = 0; i < m; ++i) correct += ((dec[size_t(i)] > 0 ? 1 : -1) == te.y[size_t(i)]);
+    // predict flag + reduce_sum (gpu_svm_main3.cu:277-315) as one counting kernel on the device
+    auto* yq = static_cast<int32_t*>(dev.alloc(m * 4));
+    CK(svmd_memcpy_h2d(dev.ctx, yq, te.y.data(), m * 4));
+    int64_t c = 0;
+    CK(svmd_count_correct(dev.ctx, out, yq, m, 0, &c));
+    correct = c;
   }
   printf("Test accuracy = %.15f (%lld/%lld)\n", m ? double(correct) / double(m) : 0.0, correct, m);
   printf("Final SV count = %lld\n", (long long)nsv);

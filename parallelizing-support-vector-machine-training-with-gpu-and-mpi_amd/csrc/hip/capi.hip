@@ -492,6 +492,20 @@ SVM_API int svmd_decision(void* h, const double* Xs_d, const double* ns_d, const
   return ctx->end();
 }
 
+SVM_API int svmd_count_correct(void* h, const double* dec_d, const int32_t* y_d, int64_t m, int32_t zero_positive,
+                               int64_t* correct) {
+  SVMD_CTX(h);
+  if (!correct) {
+    set_error("svmd_count_correct: null output");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = count_correct(ctx, dec_d, y_d, m, zero_positive != 0, correct);
+  if (rc) return rc;
+  return ctx->end();
+}
+
 SVM_API int svmd_gather_rows(void* h, const double* src_d, int64_t ld, const int64_t* idx_d, int64_t k,
                              double* dst_d) {
   SVMD_CTX(h);

@@ -130,6 +130,8 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
 int exp_selftest(hipStream_t s, const double* x, int64_t n, double* out_lib, double* out_batch);
 // Number of alpha[i] > tol for i < n (device reduction; one 8-byte read-back per row of alphas).
 int count_sv(DeviceCtx* ctx, const double* alpha, int64_t n, int64_t rows, double tol, int64_t* out);
+int count_correct(DeviceCtx* ctx, const double* dec, const int32_t* y, int64_t m, bool zero_positive,
+                  int64_t* out);
 int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y, int64_t n, int nclass, double* A,
                   const svm_params& p, svm_result* r, int32_t* batched);
 

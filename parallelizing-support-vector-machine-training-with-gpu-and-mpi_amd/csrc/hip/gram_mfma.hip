@@ -189,7 +189,44 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const double* __restrict
   if (lane == 0) out[row] = acc - b;
 }
 
+// Accuracy epilogue of prediction (the reference's predict flag + reduce_sum, gpu_svm_main3.cu:277-315,
+// which sums 0/1 doubles in a multi-pass tree): count rows whose sign matches the label, integer
+// wave sums and one atomic per wave.  zero_positive: s >= 0 -> +1 (cascade rule, M3 :800), else s > 0.
+__global__ __launch_bounds__(256) void count_correct_kernel(const double* __restrict__ dec,
+                                                            const int32_t* __restrict__ y, int64_t m,
+                                                            int zero_positive,
+                                                            unsigned long long* __restrict__ count) {
+  unsigned c = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const double s = dec[i];
+    const int pred = (zero_positive ? s >= 0.0 : s > 0.0) ? 1 : -1;
+    c += pred == y[i] ? 1u : 0u;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
 }  // namespace
+
+int count_correct(DeviceCtx* ctx, const double* dec, const int32_t* y, int64_t m, bool zero_positive,
+                  int64_t* out) {
+  *out = 0;
+  if (m <= 0) return SVM_OK;
+  hipStream_t s = ctx->stream;
+  if (!ctx->count_d) SVMD_CHECK(hipMalloc(&ctx->count_d, 1024 * 8));
+  int rc = ctx->ensure_pinned(8);
+  if (rc) return rc;
+  SVMD_CHECK(hipMemsetAsync(ctx->count_d, 0, 8, s));
+  const unsigned bx = unsigned(std::min<int64_t>((m + 255) / 256, 1024));
+  hipLaunchKernelGGL(count_correct_kernel, dim3(bx), dim3(256), 0, s, dec, y, m, zero_positive ? 1 : 0,
+                     static_cast<unsigned long long*>(ctx->count_d));
+  SVMD_LAUNCH_CHECK();
+  auto* h = static_cast<unsigned long long*>(ctx->pinned);
+  SVMD_CHECK(hipMemcpyAsync(h, ctx->count_d, 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  *out = int64_t(h[0]);
+  return SVM_OK;
+}
 
 int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m, int64_t lda,
                     const double* B, const double* nB, int64_t n, int64_t ldb, int64_t kdim,

@@ -122,6 +122,11 @@ SVM_API int svmd_decision(void* ctx, const double* Xs_d, const double* ns_d, con
                           int64_t nsv, int64_t lds, const double* Xq_d, const double* nq_d, int64_t m,
                           int64_t ldq, int64_t kdim, double gamma, double b, double* out_d);
 
+// *correct = #{i : sign(dec_d[i]) == y_d[i]} on the device (prediction accuracy numerator);
+// zero_positive = 1 maps s >= 0 to +1 (cascade programs), 0 maps s > 0 to +1 (serial / GPU programs).
+SVM_API int svmd_count_correct(void* ctx, const double* dec_d, const int32_t* y_d, int64_t m,
+                               int32_t zero_positive, int64_t* correct);
+
 // dst[k] = src[idx[k]] rows (device gather), for SV compaction and cascade training-set assembly.
 SVM_API int svmd_gather_rows(void* ctx, const double* src_d, int64_t ld, const int64_t* idx_d,
                              int64_t k, double* dst_d);

@@ -149,19 +149,27 @@ class SVC:
 
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
-        X = np.ascontiguousarray(X, dtype=np.uint8 if (self._dev is not None and _is_u8(X)) else np.float64)
         if self._dev is not None:
-            from ..ops import device as D
+            return self._device_decision(X).cpu().numpy()
+        return self._host_decision(X)
 
-            dv = self._dev
-            Xq = D.upload_rows(X, dv["device"])
-            if self.scale:
-                _, _, nq = D.minmax_scale_(Xq, dv["d"], dv["mn"], dv["mx"])
-            else:
-                nq = D.row_norms(Xq, dv["d"])
-            return D.decision(dv["Xs"], dv["ns"], dv["coef"], Xq, nq, self.params.gamma, self.b_).cpu().numpy()
+    def _device_decision(self, X: np.ndarray):
+        """Decision values as a device tensor (device models only)."""
+        from ..ops import device as D
+
+        X = np.ascontiguousarray(X, dtype=np.uint8 if _is_u8(X) else np.float64)
+        dv = self._dev
+        Xq = D.upload_rows(X, dv["device"])
+        if self.scale:
+            _, _, nq = D.minmax_scale_(Xq, dv["d"], dv["mn"], dv["mx"])
+        else:
+            nq = D.row_norms(Xq, dv["d"])
+        return D.decision(dv["Xs"], dv["ns"], dv["coef"], Xq, nq, self.params.gamma, self.b_)
+
+    def _host_decision(self, X: np.ndarray) -> np.ndarray:
         from ..ops import cpu as C
 
+        X = np.ascontiguousarray(X, dtype=np.float64)
         Xq = self.scaler_.transform(X) if self.scaler_ is not None else X
         return C.decision(self.support_vectors_, self.support_labels_, self.alpha_[self.support_], Xq,
                           self.params.gamma, self.b_, self.params.n_threads)
@@ -172,7 +180,13 @@ class SVC:
         return np.where(pos, 1, -1).astype(np.int32)
 
     def score(self, X: np.ndarray, y: np.ndarray) -> float:
-        return float(np.mean(self.predict(X) == np.asarray(y)))
+        """Accuracy.  Device models count the correct signs on the device (count_correct)."""
+        y = np.asarray(y)
+        if self._dev is not None and len(y):
+            from ..ops import device as D
+
+            return D.count_correct(self._device_decision(X), y, self.zero_is_positive) / len(y)
+        return float(np.mean(self.predict(X) == y))
 
     # ------------------------------------------------------------------ persistence
     def save(self, directory: str | os.PathLike, ids: Optional[np.ndarray] = None) -> None:

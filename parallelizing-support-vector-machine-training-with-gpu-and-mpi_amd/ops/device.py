@@ -349,6 +349,23 @@ def decision(Xs: torch.Tensor, ns: torch.Tensor, coef: torch.Tensor, Xq: torch.T
     return out
 
 
+def count_correct(dec: torch.Tensor, y, zero_is_positive: bool = False) -> int:
+    """#{i : sign(dec[i]) == y[i]} counted on the device (the reference's predict flag + reduce_sum,
+    gpu_svm_main3.cu:277-315); s >= 0 -> +1 if zero_is_positive (cascade rule) else s > 0 -> +1."""
+    dec = dec.contiguous()
+    m = dec.numel()
+    yd = torch.as_tensor(np.ascontiguousarray(y, dtype=np.int32) if not torch.is_tensor(y) else y)
+    yd = yd.to(device=dec.device, dtype=torch.int32).contiguous()
+    if yd.numel() != m:
+        raise ValueError(f"count_correct: {m} decision values but {yd.numel()} labels")
+    out = ctypes.c_int64(0)
+    if m:
+        ctx = _ctx_for(dec)
+        N.check(ctx.lib.svmd_count_correct(ctx.bind(), N.ptr(dec), N.ptr(yd), m, int(bool(zero_is_positive)),
+                                           ctypes.byref(out)), "svmd_count_correct")
+    return int(out.value)
+
+
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """dst[k] = src[idx[k]] (device row gather, idx int64 on the same device)."""
     _check_rows(src, "src")

@@ -255,6 +255,19 @@ def test_decision_vs_fp64_reference(dev, D, mn_data):
     np.testing.assert_allclose(out, ref, rtol=0, atol=1e-11)
 
 
+@pytest.mark.parametrize("m", [1, 255, 257, 10000, 300001])
+def test_count_correct_vs_numpy(dev, D, m):
+    """Device accuracy count (predict flag + reduce_sum) for both sign rules, exact zeros included."""
+    rng = np.random.default_rng(m)
+    dec = rng.normal(size=m)
+    dec[rng.random(m) < 0.05] = 0.0
+    y = np.where(rng.random(m) < 0.5, 1, -1).astype(np.int32)
+    dd = torch.from_numpy(dec).to(dev)
+    for zp in (False, True):
+        pred = np.where(dec >= 0 if zp else dec > 0, 1, -1)
+        assert D.count_correct(dd, y, zp) == int(np.sum(pred == y))
+
+
 def test_svc_cuda_matches_cpu(dev, mn_data):
     tr, te = mn_data
     g = SVC(device="cuda").fit(tr.X, tr.y)
