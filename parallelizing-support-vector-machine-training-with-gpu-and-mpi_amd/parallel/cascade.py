@@ -130,11 +130,17 @@ class _HipBackend:
         return self.D.gather_rows(X, torch.from_numpy(np.asarray(idx, dtype=np.int64)))
 
     def decision(self, sv_X, coef, y_sv, alpha_sv, Xq, b):
+        return self.decision_device(sv_X, coef, Xq, b).cpu().numpy()
+
+    def decision_device(self, sv_X, coef, Xq, b) -> torch.Tensor:
         D = self.D
         ns = D.row_norms(sv_X, self.d)
         nq = D.row_norms(Xq, self.d)
         c = torch.from_numpy(np.ascontiguousarray(coef)).to(self.device)
-        return D.decision(sv_X, ns, c, Xq, nq, self.params.gamma, b).cpu().numpy()
+        return D.decision(sv_X, ns, c, Xq, nq, self.params.gamma, b)
+
+    def count_correct(self, dec: torch.Tensor, y: np.ndarray) -> int:
+        return self.D.count_correct(dec, y, zero_is_positive=True)  # s >= 0 -> +1 (M3 :800)
 
     def sync(self):
         torch.cuda.synchronize(self.device)
@@ -450,7 +456,14 @@ class CascadeSVM:
         return np.where(dec >= 0 if zero_is_positive else dec > 0, 1, -1).astype(np.int32)
 
     def score(self, X: np.ndarray, y: np.ndarray) -> float:
-        return float(np.mean(self.predict(X) == np.asarray(y)))
+        """Accuracy with the cascade's s >= 0 rule; the HIP backend counts on the device."""
+        r, be, y = self.result, self._be, np.asarray(y)
+        if be.name == "hip" and len(r.sv) and len(y):
+            X = np.ascontiguousarray(X, dtype=np.uint8 if X.dtype == np.uint8 else np.float64)
+            Xq = be.to_rows(X, self.device)
+            be.scale_(Xq, r.mn, r.mx)
+            return be.count_correct(be.decision_device(r.sv.X, r.sv.alpha * r.sv.y, Xq, r.b), y) / len(y)
+        return float(np.mean(self.predict(X) == y))
 
     def save(self, directory) -> None:
         from ..models.model_io import save_model
