@@ -4,23 +4,26 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 60000] [--topology star|tree]
 
 One "step" is one complete training run on the fixed synthetic 60k x 784 MNIST-shaped matrix
-(random-init is meaningless for an SVM; the data are a deterministic synthetic draw of MNIST's
-shape and value domain because MNIST itself is not available offline):
+(an SVM has no random init; the data are a deterministic synthetic draw of MNIST's shape and value
+domain because MNIST itself is not available offline):
 
-* N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's
-  GPU "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram,
-  device SMO to convergence.
-* The pixel rows are held as uint8 (what MNIST is) and cross PCIe as bytes; they are widened to
-  FP64 on the device, where every value is exact, so all results are identical to an FP64 upload.
-  ``--input f64`` ships FP64 rows like the reference does (+~6 ms of H2D at 60k).
-* N > 1: one rank per GPU (torchrun, RCCL over xGMI), the modified two-layer Cascade SVM
-  (mpi_svm_main2.cpp, default) or the classical tree (--topology tree).  Timed scope = a whole
-  cascade fit of each rank's partition (H2D, global scaling, all rounds to convergence).
+* N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's GPU
+  "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram, device
+  SMO to convergence.  Rows are held as uint8 (what MNIST is) and widened to FP64 on the device,
+  where every value is exact (``--input f64`` ships FP64 rows like the reference, same results).
+* N > 1: the Cascade SVM (modified two-layer star, mpi_svm_main2.cpp, default; ``--topology tree`` =
+  classical mpi_svm_main3.cpp) on N GPUs, one rank per GPU, RCCL over xGMI, all on the ONE native
+  driver (csrc/cascade):
+    - launched directly (``python bench.py --gpus N``): N thread-ranks of this process, one GPU and
+      one communicator each (ncclCommInitAll) — nothing is re-launched;
+    - launched by torchrun (WORLD_SIZE = N): one rank per process on GPU LOCAL_RANK; the
+      ncclUniqueId travels over the launcher's store (gloo group), ncclCommInitRank.
+  Timed scope = a whole cascade fit: each rank's H2D of its partition, global scaling, all rounds to
+  convergence, the final model on the host.
 
-The timed region is bracketed by a barrier + device synchronisation on both sides and the
-maximum over ranks is reported.  value = seconds per training run (lower is better);
-vs_baseline = value / 58.570 s (the reference's single-GPU SMO time).
-Accuracy, #SV, b and iterations of the last run are reported alongside (parity fields).
+The timed region is bracketed by a barrier + device synchronisation on both sides and the maximum
+over ranks is reported.  value = seconds per training run (lower is better); vs_baseline = value /
+58.570 s (the reference's single-GPU SMO time).
 """
 from __future__ import annotations
 
@@ -38,10 +41,33 @@ REF_SERIAL_S = 3285.662  # serial SMO training time, 60k
 REF_GPU_PRED_S = 38.297  # GPU prediction time, 60k train / 10k test
 REF_STAR_S = {4: 886.733, 8: 649.773, 16: 440.705, 32: 333.696, 64: 301.263}
 REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
-# A rank that dies leaves the others blocked in a collective: RCCL's watchdog aborts the job after
-# this long instead of hanging it (the reference has no failure handling).
-COLLECTIVE_TIMEOUT = datetime.timedelta(minutes=10)
 METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
+
+
+def critical_path(solves, topology):
+    """Per round: the slowest rank's local solve (tree: slowest rank of every layer) + rank 0's merge.
+    Returns ([[round, local_max_ms, merge_ms, local_max_iterations, merge_iterations]], total ms)."""
+    rounds = sorted({s["round"] for s in solves})
+    out, tot = [], 0.0
+    for r in rounds:
+        rs = [s for s in solves if s["round"] == r]
+        if topology == "star":
+            loc = [s for s in rs if s["layer"] == "local"]
+            mer = [s for s in rs if s["layer"] == "merge"]
+            lm = max((s["ms"] for s in loc), default=0.0)
+            li = max((s["iterations"] for s in loc), default=0)
+            mm = sum(s["ms"] for s in mer)
+            mi = sum(s["iterations"] for s in mer)
+        else:
+            layers = sorted({s["layer"] for s in rs}, key=lambda x: int(x[5:]))
+            first = [s for s in rs if s["layer"] == layers[0]] if layers else []
+            lm = max((s["ms"] for s in first), default=0.0)
+            li = max((s["iterations"] for s in first), default=0)
+            mm = sum(max(s["ms"] for s in rs if s["layer"] == L) for L in layers[1:])
+            mi = sum(max(s["iterations"] for s in rs if s["layer"] == L) for L in layers[1:])
+        out.append([r, round(lm, 3), round(mm, 3), li, mi])
+        tot += lm + mm
+    return out, round(tot, 3)
 
 
 def main(argv=None):
@@ -53,64 +79,77 @@ def main(argv=None):
     ap.add_argument("--m", type=int, default=10000, help="test rows for the parity fields")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
+    ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
+                    help="direct launch, N > 1: rccl (one GPU per rank) or loopback (a rehearsal of N ranks "
+                         "sharing the visible GPUs, host-staged exchanges)")
     ap.add_argument("--input", choices=["u8", "f64"], default="u8",
                     help="host row format: uint8 pixels (default) or FP64 as in the reference")
+    ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
+    ap.add_argument("--baseline-1gpu", type=int, default=3,
+                    help="N > 1: single-GPU fits timed after the cascade for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--cascade", action="store_true",
-                    help="run the cascade path even on one rank (rehearsal of the RCCL code path)")
-    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
-                    help="process-group backend for N > 1 (gloo: CPU-staged exchanges, for rehearsals of the "
-                         "multi-rank path on fewer GPUs than ranks)")
     a = ap.parse_args(argv)
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if a.gpus > 1:
-            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run",
-                  file=sys.stderr)
-            return 2
-    ndev = torch.cuda.device_count()
-    dev_index = local_rank % max(1, ndev)
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
+    multiproc = world_env > 1
+    if multiproc and world_env != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, {ndev} visible "
+              "(use --transport loopback for a one-GPU rehearsal)", file=sys.stderr)
+        return 2
+    if multiproc and ndev <= local_rank:
+        print(f"bench.py: LOCAL_RANK {local_rank} but {ndev} visible GPUs", file=sys.stderr)
+        return 2
 
     from svm355 import SVC, SVMParams
     from svm355.parallel.cascade import CascadeSVM, partition_bounds
     from svm355.utils.data import synthetic_mnist
 
-    use_cascade = world > 1 or a.cascade
+    dev_index = local_rank if multiproc else 0
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    use_cascade = a.gpus > 1 or a.cascade
     dist = None
-    if use_cascade:
+    if multiproc:
         import torch.distributed as dist
 
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev, timeout=COLLECTIVE_TIMEOUT)
-        else:
-            dist.init_process_group("gloo", timeout=COLLECTIVE_TIMEOUT)
-    comm_dev = dev if a.backend == "nccl" else torch.device("cpu")
-    params = SVMParams()
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))  # bootstrap store + timing max
 
-    if not use_cascade:
-        tr = synthetic_mnist(a.n, seed=a.seed)
-    else:
-        lo, hi = partition_bounds(a.n, world, rank)
-        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo)
+    params = SVMParams()
     te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
+    if multiproc:
+        lo, hi = partition_bounds(a.n, world_env, rank)
+        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo)
+    else:
+        tr = synthetic_mnist(a.n, seed=a.seed)
     if a.input == "u8":
         tr = tr.compact()
         te = te.compact() if te is not None else None
 
+    group = crank = None
+    if use_cascade:
+        if multiproc:
+            from svm355.parallel.rccl import RcclRank
+
+            crank = RcclRank.from_torch_dist(dev_index)
+        else:
+            from svm355.parallel.rccl import DeviceGroup
+
+            group = DeviceGroup(a.gpus, a.transport)
+
     def barrier_sync():
         torch.cuda.synchronize(dev)
+        if crank is not None:
+            crank.barrier()  # RCCL all-reduce over the cascade's own communicators
         if dist is not None:
-            if a.backend == "nccl":
-                dist.barrier(device_ids=[dev_index])
-            else:
-                dist.barrier()
+            dist.barrier()
         torch.cuda.synchronize(dev)
 
     model = None
@@ -119,13 +158,10 @@ def main(argv=None):
         nonlocal model
         if not use_cascade:
             model = SVC(device=str(dev)).fit(tr.X, tr.y)
+        elif multiproc:
+            model = CascadeSVM(params, topology=a.topology).fit_rank(crank, tr.X, tr.y, np.arange(lo, hi), a.n)
         else:
-            from svm355.parallel.transport import TorchDistTransport
-
-            t = TorchDistTransport(comm_dev)
-            model = CascadeSVM(t, params, topology=a.topology, verbose=0, device=dev)
-            lo, hi = partition_bounds(a.n, world, rank)
-            model.fit(tr.X, tr.y, np.arange(lo, hi), n_total=a.n)
+            model = CascadeSVM(params, topology=a.topology).fit(tr.X, tr.y, world=a.gpus, device="cuda", group=group)
 
     for _ in range(a.warmup):
         step()
@@ -143,7 +179,7 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     step_ms = [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + marks[:-1], marks)]
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
@@ -164,24 +200,55 @@ def main(argv=None):
                  "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
                  "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S}
     else:
-        acc = model.score(te.X, te.y) if rank == 0 else None
-        s = model.summary()
-        sol = model.result.solves  # this rank's solves of the last fit (rank 0: local + merge per round)
-        extra = {"n_sv": s["n_sv"], "rounds": s["rounds"], "b": s["b"], "accuracy": acc,
-                 "sv_history": s["sv_history"], "round_ms": s["round_ms"], "converged": s["converged"],
-                 "rank0_smo_iterations": int(sum(x["iterations"] for x in sol)),
-                 "rank0_solves": [[x["round"], x["layer"], x["n"], x["iterations"], round(x["ms"], 2)] for x in sol],
-                 "note": "rank0_solves = [round, layer, rows, SMO iterations, ms]; the cascade's critical path "
-                         "is its SMO iterations (the single-GPU solve of the same 60k problem takes 12,793)"}
-        ref = (REF_STAR_S if a.topology == "star" else REF_TREE_S).get(world)
+        r = model.result
+        solves = r.solves
+        if dist is not None:  # every rank's solve log (fit_rank returns this rank's only)
+            allv = [None] * world_env
+            dist.all_gather_object(allv, solves)
+            solves = [s for v in allv for s in v]
+        crit, crit_ms = critical_path(solves, a.topology)
+        r0 = [s for s in solves if s["rank"] == 0]
+        extra = {"n_sv": int(len(r.ids)), "rounds": r.rounds, "b": r.b, "converged": r.converged,
+                 "sv_history": r.sv_history, "merged_history": r.merged_history,
+                 "round_ms": [round(x, 3) for x in r.round_ms], "transport": r.transport,
+                 "driver_train_ms": round(r.train_ms, 3), "rank0_phase_ms": r.phase_ms,
+                 "per_round_critical_path": crit, "critical_path_solve_ms": crit_ms,
+                 "rank0_smo_iterations": int(sum(s["iterations"] for s in r0)),
+                 "max_rank_smo_iterations": max(sum(s["iterations"] for s in solves if s["rank"] == q)
+                                                for q in range(max(1, r.world))),
+                 "note": "per_round_critical_path = [round, slowest local solve ms (tree: first layer), rank-0 "
+                         "merge ms (tree: slowest rank of each later layer), their SMO iterations]; "
+                         "the single-GPU trainer solves the same 60k problem in one 12,793-iteration SMO"}
+        if rank == 0:
+            extra["accuracy"] = model.score(te.X, te.y)
+        ref = (REF_STAR_S if a.topology == "star" else REF_TREE_S).get(a.gpus)
         if ref:
-            extra["speedup_vs_ref_cascade_same_P"] = ref / value
+            extra["speedup_vs_ref_cascade_same_P"] = round(ref / value, 2)
+        if a.baseline_1gpu > 0:  # the single-GPU trainer on this rank's GPU, same data, same process
+            if dist is not None:
+                dist.barrier()
+            if rank == 0:
+                full = tr if not multiproc else synthetic_mnist(a.n, seed=a.seed)
+                full = full.compact() if a.input == "u8" else full
+                SVC(device=str(dev)).fit(full.X, full.y)  # warm
+                ts = []
+                for _ in range(a.baseline_1gpu):
+                    torch.cuda.synchronize(dev)
+                    tb = time.perf_counter()
+                    SVC(device=str(dev)).fit(full.X, full.y)
+                    torch.cuda.synchronize(dev)
+                    ts.append(time.perf_counter() - tb)
+                one = float(np.median(ts))
+                extra["single_gpu_s"] = round(one, 6)
+                extra["speedup_vs_1gpu"] = round(one / value, 4)
+            if dist is not None:
+                dist.barrier()
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": round(value, 6),
             "unit": "s",
-            "n_gpus": world,
+            "n_gpus": a.gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms, 3),
@@ -194,8 +261,10 @@ def main(argv=None):
                 "model": "RBF SVM, first-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,
-                "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{world}",
+                "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{a.gpus}",
             },
+            "launch": "torchrun (one rank per process)" if multiproc else
+                      ("in-process thread ranks" if use_cascade else "single process"),
             "host_rows": "uint8 (widened to fp64 on device)" if a.input == "u8" else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
@@ -208,6 +277,10 @@ def main(argv=None):
         if a.out:
             with open(a.out, "w") as f:
                 f.write(s + "\n")
+    if crank is not None:
+        crank.close()
+    if group is not None:
+        group.close()
     if dist is not None:
         dist.destroy_process_group()
     return 0

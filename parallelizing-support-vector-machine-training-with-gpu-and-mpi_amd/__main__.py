@@ -6,11 +6,10 @@ gpu      the single-GPU program (code/gpu_svm_main3.cu; ``--n-limit N`` = gpu_sv
 sweep    the training-set-size sweep of code/gpu_svm4.sh (n = 10k, 20k, ..., 60k on one GPU),
          printing the reference's Table 2 layout (training / prediction seconds per n)
 cascade  the MPI Cascade programs (code/mpi_svm_main2.cpp ``--topology star`` = modified two-layer,
-         code/mpi_svm_main3.cpp ``--topology tree`` = classical), one process per GPU over
-         torch.distributed (RCCL/xGMI; ``--backend gloo`` for CPU ranks).  Run it under
-         ``torchrun --nproc-per-node P`` or pass ``--gpus P`` and it launches torchrun itself.
-         stdout follows the reference's ``[rank 0] ...`` lines.  ``--native`` runs
-         the C++ driver bin/svm_cascade instead (one process, a thread per GPU, RCCL from C++).
+         code/mpi_svm_main3.cpp ``--topology tree`` = classical) on the native driver: ``--gpus P``
+         thread-ranks, one GPU and one RCCL communicator each (ncclCommInitAll, xGMI), or ``--cpu``
+         thread-ranks on the C++ oracle.  stdout follows the reference's ``[rank 0] ...`` lines
+         (SURVEY §5.5).  ``--native`` runs the C++ CLI bin/svm_cascade (same driver, no Python).
 
 multiclass  all-digit one-vs-rest (models/multiclass.py): one shared Gram per GPU, class solves
          concurrent on streams; ``--gpus P`` deals the classes over P ranks (torchrun, RCCL).
@@ -87,24 +86,23 @@ def _cascade(argv) -> int:
     ap.add_argument("--gamma", type=float, default=0.00125)
     ap.add_argument("--tau", type=float, default=1e-5)
     ap.add_argument("--max-rounds", type=int, default=50)
-    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
-    ap.add_argument("--cpu", action="store_true", help="solve on CPU ranks (native oracle) instead of GPUs")
-    ap.add_argument("--gpus", type=int, default=0, help="launch torchrun with this many ranks (if not under it)")
+    ap.add_argument("--cpu", action="store_true", help="CPU thread-ranks on the native oracle instead of GPUs")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU; thread-ranks of this process)")
+    ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
+                    help="GPU ranks: RCCL (one GPU per rank) or loopback (ranks share GPUs, host-staged)")
     ap.add_argument("--model-dir", default=None)
     ap.add_argument("--json", default=None)
     ap.add_argument("--checkpoint-dir", default=None, help="per-round cascade state (resume with --resume)")
     ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--comm-timeout", type=float, default=600.0, help="deadline of one exchange (s)")
     ap.add_argument("-v", "--verbose", type=int, default=1)
-    ap.add_argument("--native", action="store_true",
-                    help="run bin/svm_cascade instead: one process, a thread per GPU, RCCL driven from C++")
-    ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
-                    help="--native only: RCCL (one GPU per rank) or loopback (ranks share GPUs)")
+    ap.add_argument("--native", action="store_true", help="run the C++ CLI bin/svm_cascade instead")
     a = ap.parse_args(argv)
 
     if a.native:
         args = ["--topology", a.topology, "--gpus", str(max(1, a.gpus)), "--transport", a.transport,
                 "--max-rounds", str(a.max_rounds), "--C", str(a.C), "--gamma", str(a.gamma), "--tau", str(a.tau),
-                "--positive-label", str(a.positive_label), "--seed", str(a.seed)]
+                "--positive-label", str(a.positive_label), "--seed", str(a.seed), "--comm-timeout", str(a.comm_timeout)]
         if a.synthetic:
             args += ["--synthetic", a.synthetic]
         else:
@@ -117,83 +115,51 @@ def _cascade(argv) -> int:
             args += ["--checkpoint-dir", a.checkpoint_dir] + (["--resume"] if a.resume else [])
         return _native("svm_cascade", args)
 
-    if "RANK" not in os.environ and a.gpus > 0:
-        # Not under a launcher: start one (a child process — never exec from here).
-        return _launch_self("cascade", argv, a.gpus)
-
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
-    from .parallel.cascade import CascadeSVM, partition_bounds
-    from .parallel.transport import TorchDistTransport
+    from .parallel.cascade import CascadeSVM
     from .utils.config import SVMParams, default_threads
     from .utils.data import load_csv, synthetic_mnist
-
-    if "RANK" not in os.environ:  # single process: a world of one
-        os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                           "MASTER_PORT": os.environ.get("MASTER_PORT", "29534")})
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = not a.cpu and torch.cuda.is_available()
-    if use_gpu:
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        dev = torch.device("cuda", torch.cuda.current_device())
-    else:
-        dev = torch.device("cpu")
-    backend = a.backend if use_gpu else "gloo"
-    if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev, timeout=COLLECTIVE_TIMEOUT)
-    else:
-        dist.init_process_group("gloo", timeout=COLLECTIVE_TIMEOUT)
-    comm_dev = dev if backend == "nccl" else torch.device("cpu")
 
     if a.synthetic:
         parts = a.synthetic.split(",")
         n_total, m = int(parts[0]), int(parts[1]) if len(parts) > 1 else 10000
-        lo, hi = partition_bounds(n_total, world, rank)
-        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo, positive_label=a.positive_label)
-        te = synthetic_mnist(m, seed=a.seed, offset=n_total, positive_label=a.positive_label) if rank == 0 else None
+        tr = synthetic_mnist(n_total, seed=a.seed, positive_label=a.positive_label)
+        te = synthetic_mnist(m, seed=a.seed, offset=n_total, positive_label=a.positive_label)
     else:
-        full = load_csv(a.train or f"{a.dataset}_train_data.csv", positive_label=a.positive_label)
-        n_total = full.n
-        if n_total == 0:
-            print("Error: No data read from file.", file=sys.stderr)
-            return 1
-        lo, hi = partition_bounds(n_total, world, rank)
-        tr = full.subset(lo, hi)
-        te = load_csv(a.test or f"{a.dataset}_test_data.csv", positive_label=a.positive_label) if rank == 0 else None
-
-    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=default_threads())
-    model = CascadeSVM(TorchDistTransport(comm_dev), params, topology=a.topology, max_rounds=a.max_rounds,
-                       verbose=a.verbose, checkpoint_dir=a.checkpoint_dir, resume=a.resume, device=dev)
+        tr = load_csv(a.train or f"{a.dataset}_train_data.csv", positive_label=a.positive_label)
+        te = load_csv(a.test or f"{a.dataset}_test_data.csv", positive_label=a.positive_label)
+    if tr.n == 0:
+        print("Error: No data read from file.", file=sys.stderr)
+        return 1
+    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // max(1, a.gpus)))
+    model = CascadeSVM(params, topology=a.topology, max_rounds=a.max_rounds, verbose=a.verbose,
+                       checkpoint_dir=a.checkpoint_dir, resume=a.resume, comm_timeout_s=a.comm_timeout)
+    device = "cpu" if a.cpu else "cuda"
+    X = tr.X if a.cpu else tr.compact().X
     t0 = time.perf_counter()
-    res = model.fit(tr.X, tr.y, np.arange(lo, hi), n_total=n_total)
+    model.fit(X, tr.y, world=max(1, a.gpus), device=device, transport=a.transport)
     t1 = time.perf_counter()
-    out = {}
-    if rank == 0:
-        acc = None
-        if te is not None and te.n:
-            pred = model.predict(te.X)
-            correct = int((pred == te.y).sum())
-            acc = correct / te.n
-            print(f"[rank 0] Test accuracy (final model) = {acc} ({correct}/{te.n})")
-        else:
-            print("[rank 0] No test data found or test file empty.")
-        t2 = time.perf_counter()
-        train_ms, pred_ms = res.train_ms, (t2 - t1) * 1e3
-        print(f"[rank 0] Final global SV count = {len(res.sv)}")
-        print(f"[rank 0] Cascade finished in {res.rounds} rounds")
-        print(f"[rank 0] training time = {int(train_ms)} ms")
-        print(f"[rank 0] prediction time = {int(pred_ms)} ms")
-        print(f"[rank 0] elapsed time = {int(train_ms + pred_ms)} ms")
-        out = {"program": f"svm355 cascade ({a.topology})", "world": world, "n": n_total, **model.summary(),
-               "accuracy": acc, "training_ms": train_ms, "prediction_ms": pred_ms, "fit_wall_ms": (t1 - t0) * 1e3}
-        if a.json:
-            Path(a.json).write_text(json.dumps(out) + "\n")
-        if a.model_dir:
-            model.save(a.model_dir)
-    dist.destroy_process_group()
+    res = model.result
+    acc = None
+    if te.n:
+        correct = int(round(model.score(te.X, te.y) * te.n))
+        acc = correct / te.n
+        print(f"[rank 0] Test accuracy (final model) = {acc} ({correct}/{te.n})")
+    else:
+        print("[rank 0] No test data found or test file empty.")
+    t2 = time.perf_counter()
+    pred_ms = (t2 - t1) * 1e3
+    print(f"[rank 0] Final global SV count = {len(res.ids)}")
+    print(f"[rank 0] Cascade finished in {res.rounds} rounds")
+    print(f"[rank 0] training time = {int(res.train_ms)} ms")
+    print(f"[rank 0] prediction time = {int(pred_ms)} ms")
+    print(f"[rank 0] elapsed time = {int(res.train_ms + pred_ms)} ms")
+    if a.json:
+        out = {"program": f"svm355 cascade ({a.topology})", "n": tr.n, **model.summary(), "accuracy": acc,
+               "training_ms": res.train_ms, "prediction_ms": pred_ms, "fit_wall_ms": (t1 - t0) * 1e3,
+               "solves": res.solves}
+        Path(a.json).write_text(json.dumps(out) + "\n")
+    if a.model_dir:
+        model.save(a.model_dir)
     return 0
 
 

@@ -70,6 +70,56 @@ class SvmdTiming(ctypes.Structure):
     ]
 
 
+class SvmCascadeCfg(ctypes.Structure):
+    _fields_ = [
+        ("tree", c_int32),
+        ("max_rounds", c_int32),
+        ("params", SvmParams),
+        ("log", c_int32),
+        ("resume", c_int32),
+        ("checkpoint_dir", c_char_p),
+        ("comm_timeout_s", c_double),
+        ("fail_rank", c_int32),
+        ("fail_round", c_int32),
+        ("fail_stall_s", c_double),
+    ]
+
+
+class SvmCascadeOut(ctypes.Structure):
+    _fields_ = [
+        ("world", c_int32),
+        ("rank", c_int32),
+        ("rounds", c_int32),
+        ("converged", c_int32),
+        ("b", c_double),
+        ("train_ms", c_double),
+        ("d", c_int64),
+        ("n_sv", c_int64),
+        ("ids", POINTER(c_int64)),
+        ("y", POINTER(c_int32)),
+        ("alpha", POINTER(c_double)),
+        ("sv_rows", POINTER(c_double)),
+        ("mn", POINTER(c_double)),
+        ("mx", POINTER(c_double)),
+        ("n_hist", c_int64),
+        ("sv_history", POINTER(c_int64)),
+        ("round_ms", POINTER(c_double)),
+        ("n_merged", c_int64),
+        ("merged_history", POINTER(c_int64)),
+        ("n_solves", c_int64),
+        ("solves", POINTER(c_double)),
+        ("n_ranks", c_int64),
+        ("rank_train_ms", POINTER(c_double)),
+        ("transport", ctypes.c_char * 16),
+        ("backend", ctypes.c_char * 16),
+        ("phase_ms", c_double * 10),
+    ]
+
+
+CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
+                  "final")
+
+
 _P = c_void_p  # raw pointers are passed as integers / c_void_p
 _CORE_SIGS = {
     "svm_last_error": (c_char_p, []),
@@ -93,6 +143,9 @@ _CORE_SIGS = {
                                c_int32]),
     "svm_sv_indices": (c_int64, [_P, c_int64, c_double, _P]),
     "svm_model_save": (c_int32, [c_char_p, _P, _P, _P, c_int64, c_double]),
+    "svm_cascade_default_cfg": (None, [POINTER(SvmCascadeCfg)]),
+    "svm_cascade_fit_cpu": (POINTER(SvmCascadeOut), [_P, _P, c_int64, c_int64, c_int32, POINTER(SvmCascadeCfg)]),
+    "svm_cascade_free": (None, [POINTER(SvmCascadeOut)]),
 }
 
 _HIP_SIGS = {
@@ -132,6 +185,18 @@ _HIP_SIGS = {
                                 c_double, c_double, _P]),
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
     "svmd_count_correct": (c_int32, [c_void_p, _P, _P, c_int64, c_int32, POINTER(c_int64)]),
+    "svmd_cascade_group_create": (c_void_p, [c_int32, c_char_p, c_double]),
+    "svmd_cascade_group_world": (c_int32, [c_void_p]),
+    "svmd_cascade_group_fit": (POINTER(SvmCascadeOut), [c_void_p, _P, c_int32, _P, c_int64, c_int64,
+                                                        POINTER(SvmCascadeCfg)]),
+    "svmd_cascade_group_destroy": (None, [c_void_p]),
+    "svmd_nccl_unique_id_bytes": (c_int64, []),
+    "svmd_nccl_unique_id": (c_int32, [_P, c_int64]),
+    "svmd_cascade_rank_create": (c_void_p, [c_int32, _P, c_int32, c_int32, c_double]),
+    "svmd_cascade_rank_fit": (POINTER(SvmCascadeOut), [c_void_p, _P, c_int32, _P, _P, c_int64, c_int64, c_int64,
+                                                       POINTER(SvmCascadeCfg)]),
+    "svmd_cascade_rank_barrier": (c_int32, [c_void_p]),
+    "svmd_cascade_rank_destroy": (None, [c_void_p]),
     "svmd_trace_push": (None, [c_char_p]),
     "svmd_trace_pop": (None, []),
 }

@@ -30,19 +30,21 @@ ARCH = os.environ.get("SVM355_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", "-pthread", "-Wall", "-Wextra",
-            "-Wno-unused-parameter", f"-I{CSRC / 'include'}"]
+            "-Wno-unused-parameter", f"-I{CSRC / 'include'}", f"-I{CSRC / 'cascade'}"]
 HIPFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", f"-I{ROCM / 'include'}",
             "-Wall", "-Wno-unused-parameter", "-Wno-unused-result", f"-I{CSRC / 'include'}",
-            f"-I{CSRC / 'hip'}"]
+            f"-I{CSRC / 'hip'}", f"-I{CSRC / 'cascade'}"]
 
 # Per-file extra flags.  (Measured and rejected: -fno-honor-nans -mno-amdgpu-ieee on smo.hip was 3%
 # faster but changed the f64 division expansion, breaking bit-identity with the CPU oracle.)
 HIP_EXTRA: dict = {}
 
-CORE_SRCS = sorted((CSRC / "core").glob("*.cpp"))
+CORE_SRCS = sorted((CSRC / "core").glob("*.cpp")) + sorted((CSRC / "cascade").glob("*.cpp"))
 HIP_SRCS = sorted((CSRC / "hip").glob("*.hip"))
-HIP_HDRS = sorted((CSRC / "hip").glob("*.h")) + sorted((CSRC / "include").glob("*.h"))
-CORE_HDRS = sorted((CSRC / "core").glob("*.h")) + sorted((CSRC / "include").glob("*.h"))
+HIP_HDRS = (sorted((CSRC / "hip").glob("*.h")) + sorted((CSRC / "include").glob("*.h"))
+            + sorted((CSRC / "cascade").glob("*.h")))
+CORE_HDRS = (sorted((CSRC / "core").glob("*.h")) + sorted((CSRC / "include").glob("*.h"))
+             + sorted((CSRC / "cascade").glob("*.h")))
 
 
 def _stale(out: Path, deps) -> bool:
@@ -103,7 +105,7 @@ def build_hip(force=False, verbose=False) -> Path:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _stale(out, objs):
         _run([cc, "-shared", f"--offload-arch={ARCH}", *objs, f"-L{LIB}", "-lsvm355_core",
-              f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}",
+              f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", "-lrccl", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}",
               "-o", out], verbose)
     return out
 
@@ -126,16 +128,12 @@ def build_apps(force=False, verbose=False):
         _run(["g++", *CXXFLAGS, src, f"-L{LIB}", "-lsvm355_hip", "-lsvm355_core", rpath,
               "-o", gpu], verbose)
     outs.append(gpu)
-    # Native cascade (one process, one thread per GPU, RCCL): hipcc for the HIP runtime + RCCL headers.
+    # Native cascade (one process, one thread per GPU, RCCL inside libsvm355_hip): C ABI only.
     casc = BIN / "svm_cascade"
-    srcs = [CSRC / "apps" / "svm_cascade.cpp", *sorted((CSRC / "cascade").glob("*.cpp"))]
-    deps = [*srcs, *sorted((CSRC / "cascade").glob("*.h")), LIB / "libsvm355_core.so", LIB / "libsvm355_hip.so",
-            *HIP_HDRS, CSRC / "apps" / "cli_common.h"]
+    src = CSRC / "apps" / "svm_cascade.cpp"
+    deps = [src, LIB / "libsvm355_core.so", LIB / "libsvm355_hip.so", *CORE_HDRS, CSRC / "apps" / "cli_common.h"]
     if force or _stale(casc, deps):
-        _run([hipcc(), "-std=c++17", "-O2", "-fPIC", "-pthread", "-Wall", "-Wno-unused-parameter",
-              f"-I{CSRC / 'include'}", f"-I{CSRC / 'cascade'}", f"-I{ROCM / 'include'}", *srcs, f"-L{LIB}",
-              "-lsvm355_hip", "-lsvm355_core", f"-L{ROCM / 'lib'}", "-lrccl", rpath, f"-Wl,-rpath,{ROCM / 'lib'}",
-              "-o", casc], verbose)
+        _run(["g++", *CXXFLAGS, src, f"-L{LIB}", "-lsvm355_hip", "-lsvm355_core", rpath, "-o", casc], verbose)
     outs.append(casc)
     return outs
 

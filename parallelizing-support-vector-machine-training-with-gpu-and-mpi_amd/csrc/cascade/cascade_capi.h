@@ -1,0 +1,18 @@
+// Helpers shared by the C ABIs of the cascade (CPU group in libsvm355_core, device groups and
+// ranks in libsvm355_hip).
+#pragma once
+#include <vector>
+
+#include "cascade.h"
+
+namespace svm355 {
+
+CascadeConfig config_from(const svm_cascade_cfg* c);
+// Builds the C result from rank outputs (outs[0] = the lowest rank this call drove; it provides
+// the model); B0 is that rank's backend (for the SV rows).
+svm_cascade_out* build_cascade_out(const std::vector<const CascadeOutput*>& outs, Backend& B0, int world,
+                                   int first_rank, const char* transport, const char* backend);
+// Row-major host rows of rank r's partition (contiguous ceil(n / P) chunks) and their global ids.
+std::vector<int64_t> partition_ids(int64_t n, int P, int r, int64_t* lo, int64_t* hi);
+
+}  // namespace svm355

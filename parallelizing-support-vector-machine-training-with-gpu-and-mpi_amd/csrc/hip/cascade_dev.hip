@@ -1,0 +1,620 @@
+// Device side of the native Cascade SVM (csrc/cascade): the gfx950 backend, the RCCL transport
+// and the C ABI of the multi-GPU runs.
+//
+//   HipBackend     SV sets in HBM; assembly / packing are row-copy kernels on the rank's stream;
+//                  every solve is the device trainer (MFMA / exact-integer RBF Gram + device SMO,
+//                  warm start f from the resident Gram).  A caching allocator keeps the per-round
+//                  sets from going back to hipMalloc / hipFree (hipFree synchronises the device).
+//   RcclTransport  one communicator per GPU, collectives on the backend's stream (so they are
+//                  ordered after the kernels that produced their buffers); every wait polls
+//                  hipStreamQuery + ncclCommGetAsyncError against the WaitPolicy (abort token and
+//                  deadline) instead of blocking in hipStreamSynchronize; abort() = ncclCommAbort.
+//   C ABI          svmd_cascade_group_* : P thread-ranks over P GPUs of this process
+//                                         (ncclCommInitAll) or a loopback rehearsal;
+//                  svmd_cascade_rank_*  : one rank per process (ncclCommInitRank with an id the
+//                                         launcher distributes, e.g. torchrun + a TCP store).
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "cascade.h"
+#include "cascade_capi.h"
+#include "ctx.h"
+#include "svm355_device.h"
+
+namespace svm355 {
+namespace {
+
+// ------------------------------------------------------------------------------------- kernels
+// One workgroup per row (grid-stride); rows of stored sets are 16-byte aligned (ld % 16 == 0), record
+// rows (width ld + 3) are only 8-byte aligned.
+__global__ __launch_bounds__(256) void assemble_set_kernel(const double* __restrict__ sX,
+                                                           const int32_t* __restrict__ sy,
+                                                           const double* __restrict__ sa,
+                                                           const int64_t* __restrict__ sid,
+                                                           const int64_t* __restrict__ idx, int64_t m, int64_t ld,
+                                                           double* __restrict__ dX, int32_t* __restrict__ dy,
+                                                           double* __restrict__ da, int64_t* __restrict__ did,
+                                                           int zero_alpha) {
+  for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
+    const int64_t src = idx ? idx[i] : i;
+    const double2* s = reinterpret_cast<const double2*>(sX + src * ld);
+    double2* d = reinterpret_cast<double2*>(dX + i * ld);
+    for (int64_t c = threadIdx.x; c < ld / 2; c += blockDim.x) d[c] = s[c];
+    if (threadIdx.x == 0) {
+      dy[i] = sy[src];
+      da[i] = zero_alpha ? 0.0 : sa[src];
+      did[i] = sid[src];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void assemble_rec_kernel(const double* __restrict__ rec, int64_t w,
+                                                           const int64_t* __restrict__ idx, int64_t m, int64_t ld,
+                                                           double* __restrict__ dX, int32_t* __restrict__ dy,
+                                                           double* __restrict__ da, int64_t* __restrict__ did,
+                                                           int zero_alpha) {
+  for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
+    const double* r = rec + (idx ? idx[i] : i) * w;
+    double* d = dX + i * ld;
+    for (int64_t c = threadIdx.x; c < ld; c += blockDim.x) d[c] = r[c];
+    if (threadIdx.x == 0) {
+      dy[i] = int32_t(r[ld]);
+      da[i] = zero_alpha ? 0.0 : r[ld + 1];
+      did[i] = int64_t(r[ld + 2]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const double* __restrict__ X, const int32_t* __restrict__ y,
+                                                   const double* __restrict__ a, const int64_t* __restrict__ id,
+                                                   int64_t k, int64_t ld, double* __restrict__ rec) {
+  const int64_t w = ld + 3;
+  for (int64_t i = blockIdx.x; i < k; i += gridDim.x) {
+    const double* s = X + i * ld;
+    double* r = rec + i * w;
+    for (int64_t c = threadIdx.x; c < ld; c += blockDim.x) r[c] = s[c];
+    if (threadIdx.x == 0) {
+      r[ld] = double(y[i]);
+      r[ld + 1] = a[i];
+      r[ld + 2] = double(id[i]);
+    }
+  }
+}
+
+__global__ void record_ids_kernel(const double* __restrict__ rec, int64_t k, int64_t w, int64_t ld,
+                                  int64_t* __restrict__ out) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < k) out[i] = int64_t(rec[i * w + ld + 2]);
+}
+
+unsigned row_grid(int64_t m) { return unsigned(std::min<int64_t>(m, 8192)); }
+
+// --------------------------------------------------------------------------------- HipBackend
+class HipBackend final : public Backend {
+ public:
+  explicit HipBackend(int device) : device_(device) {
+    ctx_ = svmd_create(device);
+    if (!ctx_) throw CascadeError(std::string("svmd_create: ") + svm_last_error());
+    stream_ = static_cast<DeviceCtx*>(ctx_)->stream;
+  }
+  ~HipBackend() override {
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    for (auto& kv : cache_) (void)hipFree(kv.second);
+    for (auto& kv : live_) (void)hipFree(kv.first);
+    if (idx_) (void)hipFree(idx_);
+    if (ids_d_) (void)hipFree(ids_d_);
+    if (sqn_) (void)hipFree(sqn_);
+    svmd_destroy(ctx_);
+  }
+  HipBackend(const HipBackend&) = delete;
+  HipBackend& operator=(const HipBackend&) = delete;
+
+  hipStream_t stream() const { return stream_; }
+  int device() const { return device_; }
+  const char* name() const override { return "hip"; }
+  int64_t ld(int64_t d) const override { return svmd_padded_dim(d); }
+
+  // Size-class caching allocator: blocks go back to a free list, never to hipFree, until the
+  // backend is destroyed.  All users run on this backend's one stream, so reuse is stream-ordered.
+  void* alloc(int64_t bytes) override {
+    size_t cls = 256;
+    while (cls < size_t(bytes)) cls <<= 1;
+    auto it = cache_.find(cls);
+    void* p = nullptr;
+    if (it != cache_.end()) {
+      p = it->second;
+      cache_.erase(it);
+    } else {
+      hipcheck(hipSetDevice(device_), "hipSetDevice");
+      if (hipMalloc(&p, cls) != hipSuccess) {
+        release_cache();  // retry once with the cached blocks returned
+        hipcheck(hipMalloc(&p, cls), "hipMalloc");
+      }
+    }
+    live_[p] = cls;
+    return p;
+  }
+  void free(void* p) override {
+    auto it = live_.find(p);
+    if (it == live_.end()) return;
+    cache_.emplace(it->second, p);
+    live_.erase(it);
+  }
+  void h2d(void* dst, const void* src, int64_t bytes) override {
+    if (bytes > 0) check(svmd_memcpy_h2d(ctx_, dst, src, bytes), "svmd_memcpy_h2d");
+  }
+  void d2h(void* dst, const void* src, int64_t bytes) override {
+    if (bytes > 0) check(svmd_memcpy_d2h(ctx_, dst, src, bytes), "svmd_memcpy_d2h");
+  }
+  void sync() override { check(svmd_synchronize(ctx_), "svmd_synchronize"); }
+  void upload_rows(const void* X, bool u8, int64_t n, int64_t d, double* dst) override {
+    if (!n) return;
+    if (u8)
+      check(svmd_upload_rows_u8(ctx_, static_cast<const uint8_t*>(X), n, d, dst, ld(d)), "svmd_upload_rows_u8");
+    else
+      check(svmd_upload_rows(ctx_, static_cast<const double*>(X), n, d, dst, ld(d)), "svmd_upload_rows");
+  }
+  void minmax(const double* X, int64_t n, int64_t d, double* mn, double* mx) override {
+    if (n == 0) {  // an empty partition contributes the identities of min / max
+      const std::vector<double> hi(size_t(d), __builtin_inf()), lo(size_t(d), -__builtin_inf());
+      h2d(mn, hi.data(), d * 8);
+      h2d(mx, lo.data(), d * 8);
+      return;
+    }
+    check(svmd_minmax(ctx_, X, n, d, ld(d), mn, mx), "svmd_minmax");
+  }
+  void scale(double* X, int64_t n, int64_t d, const double* mn, const double* mx) override {
+    check(svmd_preprocess(ctx_, X, n, d, ld(d), const_cast<double*>(mn), const_cast<double*>(mx), nullptr, 1),
+          "svmd_preprocess");
+  }
+  void assemble(const Segment& s, int64_t ld, DSet& o, int64_t off) override {
+    const int64_t m = s.rows();
+    if (!m) return;
+    const int64_t* idx = nullptr;
+    if (s.idx) idx = stage_idx(*s.idx);
+    if (s.set) {
+      hipLaunchKernelGGL(assemble_set_kernel, dim3(row_grid(m)), dim3(256), 0, stream_, s.set->X.as<double>(),
+                         s.set->y.as<int32_t>(), s.set->a.as<double>(), s.set->id.as<int64_t>(), idx, m, ld,
+                         o.X.as<double>() + off * ld, o.y.as<int32_t>() + off, o.a.as<double>() + off,
+                         o.id.as<int64_t>() + off, int(s.zero_alpha));
+    } else {
+      hipLaunchKernelGGL(assemble_rec_kernel, dim3(row_grid(m)), dim3(256), 0, stream_, s.rec, ld + 3, idx, m, ld,
+                         o.X.as<double>() + off * ld, o.y.as<int32_t>() + off, o.a.as<double>() + off,
+                         o.id.as<int64_t>() + off, int(s.zero_alpha));
+    }
+    hipcheck(hipGetLastError(), "assemble kernel");
+  }
+  void pack(const DSet& S, int64_t ld, double* rec) override {
+    if (!S.k) return;
+    hipLaunchKernelGGL(pack_kernel, dim3(row_grid(S.k)), dim3(256), 0, stream_, S.X.as<double>(), S.y.as<int32_t>(),
+                       S.a.as<double>(), S.id.as<int64_t>(), S.k, ld, rec);
+    hipcheck(hipGetLastError(), "pack kernel");
+  }
+  void record_ids(const double* rec, int64_t k, int64_t ld, int64_t* ids) override {
+    if (!k) return;
+    grow(&ids_d_, &ids_cap_, size_t(k) * 8);
+    hipLaunchKernelGGL(record_ids_kernel, dim3(unsigned((k + 255) / 256)), dim3(256), 0, stream_, rec, k, ld + 3, ld,
+                       static_cast<int64_t*>(ids_d_));
+    hipcheck(hipGetLastError(), "record_ids kernel");
+    d2h(ids, ids_d_, k * 8);
+  }
+  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
+    const int64_t ldd = ld(d);
+    grow(&sqn_, &sqn_cap_, size_t(S.k) * 8);
+    auto* sqn = static_cast<double*>(sqn_);
+    check(svmd_row_norms(ctx_, S.X.as<double>(), S.k, d, ldd, sqn), "svmd_row_norms");
+    svm_result r{};
+    svmd_timing tm{};
+    int32_t used = 0;
+    check(svmd_train_q(ctx_, S.X.as<double>(), sqn, S.k, ldd, ldd, S.y.as<int32_t>(), S.a.as<double>(), 1, &p, &r,
+                       nullptr, 0, &tm, mn_h, mx_h, d, 0, &used),
+          "svmd_train_q");
+    return SolveStats{r.iterations, r.b, r.stop_reason, tm.gram_ms};
+  }
+  void trace_push(const char* name) override { svmd_trace_push(name); }
+  void trace_pop() override { svmd_trace_pop(); }
+
+ private:
+  static void check(int rc, const char* what) {
+    if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
+  }
+  static void hipcheck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw CascadeError(std::string(what) + ": " + hipGetErrorString(e));
+  }
+  void grow(void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return;
+    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (*p) hipcheck(hipFree(*p), "hipFree");
+    *p = nullptr;
+    *cap = 0;
+    const size_t sz = std::max<size_t>(bytes, 4096) * 2;
+    hipcheck(hipMalloc(p, sz), "hipMalloc");
+    *cap = sz;
+  }
+  const int64_t* stage_idx(const std::vector<int64_t>& v) {
+    // one staging buffer per backend: the copy is stream-ordered after earlier users of it
+    grow(&idx_, &idx_cap_, v.size() * 8);
+    hipcheck(hipMemcpyAsync(idx_, v.data(), v.size() * 8, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync idx");
+    // pageable source: make sure the host vector may be released by the caller
+    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    return static_cast<const int64_t*>(idx_);
+  }
+  void release_cache() {
+    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    for (auto& kv : cache_) (void)hipFree(kv.second);
+    cache_.clear();
+  }
+
+  int device_;
+  void* ctx_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::multimap<size_t, void*> cache_;
+  std::map<void*, size_t> live_;
+  void *idx_ = nullptr, *ids_d_ = nullptr, *sqn_ = nullptr;
+  size_t idx_cap_ = 0, ids_cap_ = 0, sqn_cap_ = 0;
+};
+
+// ------------------------------------------------------------------------------ RcclTransport
+#define NCCLT(expr)                                                                                 \
+  do {                                                                                              \
+    const ncclResult_t r_ = (expr);                                                                 \
+    if (r_ != ncclSuccess) throw TransportError(std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+#define HIPT(expr)                                                                                    \
+  do {                                                                                                \
+    const hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) throw TransportError(std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+class RcclTransport final : public Transport {
+ public:
+  RcclTransport(ncclComm_t comm, int device, hipStream_t stream, WaitPolicy wp)
+      : comm_(comm), device_(device), stream_(stream), wp_(std::move(wp)) {
+    HIPT(hipSetDevice(device_));
+    NCCLT(ncclCommUserRank(comm_, &rank_));
+    NCCLT(ncclCommCount(comm_, &world_));
+    HIPT(hipMalloc(&scratch_, size_t(64 + world_) * 8));
+    HIPT(hipHostMalloc(&pinned_, size_t(64 + world_) * 8, hipHostMallocDefault));
+  }
+  ~RcclTransport() override {
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    if (scratch_) (void)hipFree(scratch_);
+    if (pinned_) (void)hipHostFree(pinned_);
+  }
+  bool aborted() const { return aborted_; }
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  const char* name() const override { return "rccl"; }
+
+  int64_t bcast_i64(int64_t v, int root) override {
+    pinned_[0] = v;
+    HIPT(hipMemcpyAsync(scratch_, pinned_, 8, hipMemcpyHostToDevice, stream_));
+    NCCLT(ncclBroadcast(scratch_, scratch_, 1, ncclInt64, root, comm_, stream_));
+    HIPT(hipMemcpyAsync(pinned_ + 1, scratch_, 8, hipMemcpyDeviceToHost, stream_));
+    wait("ncclBroadcast(i64)");
+    return pinned_[1];
+  }
+  std::vector<int64_t> allgather_i64(int64_t v) override {
+    pinned_[0] = v;
+    HIPT(hipMemcpyAsync(scratch_, pinned_, 8, hipMemcpyHostToDevice, stream_));
+    NCCLT(ncclAllGather(scratch_, scratch_ + 1, 1, ncclInt64, comm_, stream_));
+    HIPT(hipMemcpyAsync(pinned_ + 1, scratch_ + 1, size_t(world_) * 8, hipMemcpyDeviceToHost, stream_));
+    wait("ncclAllGather(i64)");
+    return std::vector<int64_t>(pinned_ + 1, pinned_ + 1 + world_);
+  }
+  void allreduce_min(double* buf, int64_t n) override {
+    NCCLT(ncclAllReduce(buf, buf, size_t(n), ncclFloat64, ncclMin, comm_, stream_));
+    wait("ncclAllReduce(min)");
+  }
+  void allreduce_max(double* buf, int64_t n) override {
+    NCCLT(ncclAllReduce(buf, buf, size_t(n), ncclFloat64, ncclMax, comm_, stream_));
+    wait("ncclAllReduce(max)");
+  }
+  void bcast(void* buf, int64_t bytes, int root) override {
+    if (bytes <= 0) return;
+    NCCLT(ncclBroadcast(buf, buf, size_t(bytes), ncclUint8, root, comm_, stream_));
+    wait("ncclBroadcast");
+  }
+  void gather(const void* send, int64_t bytes, void* recv, int root) override {
+    if (bytes <= 0) return;
+    NCCLT(ncclGather(send, recv, size_t(bytes), ncclUint8, root, comm_, stream_));
+    wait("ncclGather");
+  }
+  void send_i64(int64_t v, int peer) override {
+    pinned_[2] = v;
+    HIPT(hipMemcpyAsync(scratch_ + 2, pinned_ + 2, 8, hipMemcpyHostToDevice, stream_));
+    NCCLT(ncclSend(scratch_ + 2, 1, ncclInt64, peer, comm_, stream_));
+    wait("ncclSend(i64)");
+  }
+  int64_t recv_i64(int peer) override {
+    NCCLT(ncclRecv(scratch_ + 3, 1, ncclInt64, peer, comm_, stream_));
+    HIPT(hipMemcpyAsync(pinned_ + 3, scratch_ + 3, 8, hipMemcpyDeviceToHost, stream_));
+    wait("ncclRecv(i64)");
+    return pinned_[3];
+  }
+  void send(const void* buf, int64_t bytes, int peer) override {
+    if (bytes <= 0) return;
+    NCCLT(ncclSend(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
+    wait("ncclSend");
+  }
+  void recv(void* buf, int64_t bytes, int peer) override {
+    if (bytes <= 0) return;
+    NCCLT(ncclRecv(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
+    wait("ncclRecv");
+  }
+  void barrier() override {
+    NCCLT(ncclAllReduce(scratch_ + 4, scratch_ + 4, 1, ncclInt64, ncclSum, comm_, stream_));
+    wait("ncclAllReduce(barrier)");
+  }
+  void abort() override {
+    if (aborted_ || !comm_) return;
+    aborted_ = true;
+    (void)ncclCommAbort(comm_);  // frees the communicator; in-flight kernels are torn down
+  }
+
+ private:
+  // Poll instead of hipStreamSynchronize: a peer that never arrives must not hang this thread.
+  void wait(const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+      const hipError_t e = hipStreamQuery(stream_);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) throw TransportError(std::string(what) + ": " + hipGetErrorString(e));
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        throw TransportError(std::string(what) + ": " + ncclGetErrorString(ae));
+      wp_.check(t0, what);
+      if (spin < 2000)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+  ncclComm_t comm_;
+  int device_, rank_ = 0, world_ = 1;
+  hipStream_t stream_;
+  WaitPolicy wp_;
+  int64_t* scratch_ = nullptr;
+  int64_t* pinned_ = nullptr;
+  bool aborted_ = false;
+};
+
+double timeout_or_default(double s) { return s > 0 ? s : 600.0; }
+
+// ------------------------------------------------------------------------- thread-rank group
+struct Group {
+  int world = 0;
+  bool rccl = false;
+  bool broken = false;
+  double timeout_s = 600.0;
+  std::vector<int> devices;
+  std::vector<std::unique_ptr<HipBackend>> be;
+  std::vector<ncclComm_t> comms;
+  std::mutex mu;  // one fit at a time
+};
+
+// ----------------------------------------------------------------------------- process rank
+struct ProcRank {
+  int device = 0;
+  bool broken = false;
+  double timeout_s = 600.0;
+  std::unique_ptr<HipBackend> be;
+  ncclComm_t comm = nullptr;
+  std::unique_ptr<RcclTransport> tr;
+};
+
+}  // namespace
+}  // namespace svm355
+
+using namespace svm355;
+
+extern "C" {
+
+SVM_API void* svmd_cascade_group_create(int32_t world, const char* transport, double comm_timeout_s) {
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (world < 1) throw CascadeError("world must be >= 1");
+    if (ndev < 1) throw CascadeError("no HIP device visible");
+    std::string tr = transport ? transport : "auto";
+    if (tr == "auto") tr = world <= ndev ? "rccl" : "loopback";
+    if (tr != "rccl" && tr != "loopback") throw CascadeError("transport must be auto, rccl or loopback");
+    if (tr == "rccl" && world > ndev)
+      throw CascadeError("rccl transport needs one GPU per rank (" + std::to_string(world) + " ranks, " +
+                         std::to_string(ndev) + " GPUs visible)");
+    auto g = std::make_unique<Group>();
+    g->world = world;
+    g->rccl = tr == "rccl";
+    g->timeout_s = timeout_or_default(comm_timeout_s);
+    for (int r = 0; r < world; ++r) {
+      g->devices.push_back(g->rccl ? r : r % ndev);
+      g->be.push_back(std::make_unique<HipBackend>(g->devices.back()));
+    }
+    if (g->rccl) {
+      g->comms.resize(size_t(world));
+      const ncclResult_t rc = ncclCommInitAll(g->comms.data(), world, g->devices.data());
+      if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitAll: ") + ncclGetErrorString(rc));
+    }
+    return g.release();
+  } catch (const std::exception& e) {
+    set_error("svmd_cascade_group_create: %s", e.what());
+    return nullptr;
+  }
+}
+
+SVM_API void svmd_cascade_group_destroy(void* h) {
+  auto* g = static_cast<Group*>(h);
+  if (!g) return;
+  if (!g->broken)
+    for (auto c : g->comms) (void)ncclCommDestroy(c);
+  g->be.clear();
+  delete g;
+}
+
+SVM_API int svmd_cascade_group_world(void* h) { return h ? static_cast<Group*>(h)->world : 0; }
+
+SVM_API svm_cascade_out* svmd_cascade_group_fit(void* h, const void* X, int32_t u8, const int32_t* y, int64_t n,
+                                                int64_t d, const svm_cascade_cfg* c) {
+  auto* g = static_cast<Group*>(h);
+  if (!g || n < 0 || d <= 0 || (n && (!X || !y))) {
+    set_error("svmd_cascade_group_fit: bad arguments");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->broken) {
+    set_error("svmd_cascade_group_fit: the group's communicators were aborted by an earlier failure; create a new group");
+    return nullptr;
+  }
+  try {
+    const CascadeConfig cfg = config_from(c);
+    const int P = g->world;
+    auto token = std::make_shared<AbortToken>();
+    const WaitPolicy wp{token, (c && c->comm_timeout_s > 0) ? c->comm_timeout_s : g->timeout_s};
+    std::vector<std::unique_ptr<Transport>> tr(static_cast<size_t>(P));
+    std::shared_ptr<LoopbackGroup> lg = g->rccl ? nullptr : std::make_shared<LoopbackGroup>(P, wp);
+    for (int r = 0; r < P; ++r) {
+      if (g->rccl) {
+        tr[size_t(r)] = std::make_unique<RcclTransport>(g->comms[size_t(r)], g->devices[size_t(r)],
+                                                        g->be[size_t(r)]->stream(), wp);
+      } else {
+        tr[size_t(r)] = std::make_unique<LoopbackTransport>(lg, r, g->be[size_t(r)].get());
+      }
+    }
+    const size_t row_bytes = u8 ? size_t(d) : size_t(d) * 8;
+    std::vector<CascadeOutput> outs(static_cast<size_t>(P));
+    try {
+      run_rank_threads(
+          P, token,
+          [&](int r) {
+            if (hipSetDevice(g->devices[size_t(r)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
+            int64_t lo = 0, hi = 0;
+            const std::vector<int64_t> ids = partition_ids(n, P, r, &lo, &hi);
+            outs[size_t(r)] = run_cascade(*tr[size_t(r)], *g->be[size_t(r)],
+                                          static_cast<const char*>(X) + size_t(lo) * row_bytes, u8 != 0, y + lo,
+                                          ids.data(), hi - lo, d, n, cfg);
+          },
+          [&](int r) {
+            (void)hipSetDevice(g->devices[size_t(r)]);
+            tr[size_t(r)]->abort();
+          });
+    } catch (...) {
+      if (g->rccl) g->broken = true;  // ncclCommAbort released the communicators
+      throw;
+    }
+    std::vector<const CascadeOutput*> ptrs;
+    for (const auto& o : outs) ptrs.push_back(&o);
+    (void)hipSetDevice(g->devices[0]);
+    return build_cascade_out(ptrs, *g->be[0], P, 0, g->rccl ? "rccl" : "loopback", "hip");
+  } catch (const std::exception& e) {
+    set_error("cascade: %s", e.what());
+    return nullptr;
+  }
+}
+
+SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap) {
+  if (!out || cap < int64_t(sizeof(ncclUniqueId))) {
+    set_error("svmd_nccl_unique_id: need %zu bytes", sizeof(ncclUniqueId));
+    return SVM_ERR_ARG;
+  }
+  ncclUniqueId id;
+  const ncclResult_t rc = ncclGetUniqueId(&id);
+  if (rc != ncclSuccess) {
+    set_error("ncclGetUniqueId: %s", ncclGetErrorString(rc));
+    return SVM_ERR_DEVICE;
+  }
+  std::memcpy(out, &id, sizeof(id));
+  return SVM_OK;
+}
+
+SVM_API int64_t svmd_nccl_unique_id_bytes(void) { return int64_t(sizeof(ncclUniqueId)); }
+
+SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32_t world, int32_t rank,
+                                       double comm_timeout_s) {
+  try {
+    if (!uid || world < 1 || rank < 0 || rank >= world) throw CascadeError("bad arguments");
+    auto p = std::make_unique<ProcRank>();
+    p->device = device;
+    p->timeout_s = timeout_or_default(comm_timeout_s);
+    if (hipSetDevice(device) != hipSuccess) throw CascadeError("hipSetDevice(" + std::to_string(device) + ") failed");
+    p->be = std::make_unique<HipBackend>(device);
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    const ncclResult_t rc = ncclCommInitRank(&p->comm, world, id, rank);
+    if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
+    return p.release();
+  } catch (const std::exception& e) {
+    set_error("svmd_cascade_rank_create: %s", e.what());
+    return nullptr;
+  }
+}
+
+SVM_API void svmd_cascade_rank_destroy(void* h) {
+  auto* p = static_cast<ProcRank*>(h);
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  const bool aborted = p->broken;
+  p->tr.reset();
+  if (p->comm && !aborted) (void)ncclCommDestroy(p->comm);
+  p->be.reset();
+  delete p;
+}
+
+SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* h, const void* X, int32_t u8, const int32_t* y,
+                                               const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
+                                               const svm_cascade_cfg* c) {
+  auto* p = static_cast<ProcRank*>(h);
+  if (!p || n_part < 0 || d <= 0 || (n_part && (!X || !y || !ids))) {
+    set_error("svmd_cascade_rank_fit: bad arguments");
+    return nullptr;
+  }
+  if (p->broken) {
+    set_error("svmd_cascade_rank_fit: the communicator was aborted by an earlier failure");
+    return nullptr;
+  }
+  try {
+    (void)hipSetDevice(p->device);
+    const CascadeConfig cfg = config_from(c);
+    const WaitPolicy wp{nullptr, (c && c->comm_timeout_s > 0) ? c->comm_timeout_s : p->timeout_s};
+    p->tr = std::make_unique<RcclTransport>(p->comm, p->device, p->be->stream(), wp);
+    CascadeOutput o;
+    try {
+      o = run_cascade(*p->tr, *p->be, X, u8 != 0, y, ids, n_part, d, n_total, cfg);
+    } catch (...) {
+      p->tr->abort();  // MPI_Abort equivalent: release the communicator so the peers' waits fail
+      p->broken = true;
+      throw;
+    }
+    return build_cascade_out({&o}, *p->be, p->tr->world(), p->tr->rank(), "rccl", "hip");
+  } catch (const std::exception& e) {
+    set_error("cascade: %s", e.what());
+    return nullptr;
+  }
+}
+
+SVM_API int svmd_cascade_rank_barrier(void* h) {
+  auto* p = static_cast<ProcRank*>(h);
+  if (!p || p->broken) {
+    set_error("svmd_cascade_rank_barrier: no usable communicator");
+    return SVM_ERR_ARG;
+  }
+  try {
+    (void)hipSetDevice(p->device);
+    if (!p->tr) p->tr = std::make_unique<RcclTransport>(p->comm, p->device, p->be->stream(),
+                                                        WaitPolicy{nullptr, p->timeout_s});
+    p->tr->barrier();
+    return SVM_OK;
+  } catch (const std::exception& e) {
+    set_error("svmd_cascade_rank_barrier: %s", e.what());
+    return SVM_ERR_DEVICE;
+  }
+}
+
+}  // extern "C"

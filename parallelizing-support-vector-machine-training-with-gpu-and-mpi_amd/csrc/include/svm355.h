@@ -117,6 +117,59 @@ SVM_API int64_t svm_sv_indices(const double* alpha, int64_t n, double tol, int64
 SVM_API int svm_model_save(const char* dir, const int64_t* ids, const int32_t* labels,
                            const double* alphas, int64_t nsv, double b);
 
+// ---------------------------------------------------------------- Cascade SVM (L5)
+// One native driver (csrc/cascade) for the classical tree (mpi_svm_main3.cpp) and the modified
+// two-layer star (mpi_svm_main2.cpp) cascades; see cascade.h for the round semantics.
+typedef struct svm_cascade_cfg {
+  int32_t tree;            // 0 = star (modified two-layer), 1 = tree (classical, P a power of 2)
+  int32_t max_rounds;      // 50 (mpi_svm_main3.cpp:544)
+  svm_params params;
+  int32_t log;             // rank 0 prints the reference's [rank 0] lines
+  int32_t resume;          // start from <checkpoint_dir>/cascade_state.bin if present
+  const char* checkpoint_dir;  // NULL or "" = no per-round checkpoint
+  double comm_timeout_s;   // deadline of one blocking exchange (<= 0: 600 s)
+  int32_t fail_rank;       // fault injection: this rank fails at the start of fail_round (-1 = off):
+  int32_t fail_round;      //   it throws, or with fail_stall_s > 0 it stops responding for that long
+  double fail_stall_s;     //   (the others then hit comm_timeout_s)
+} svm_cascade_cfg;
+
+// Result of a cascade fit (allocated by the library, release with svm_cascade_free).
+typedef struct svm_cascade_out {
+  int32_t world, rank, rounds, converged;
+  double b;
+  double train_ms;         // max over the ranks this call drove (after the data distribution)
+  int64_t d, n_sv;
+  int64_t* ids;            // n_sv global sample ids of the final SVs (rank 0's SV order)
+  int32_t* y;              // n_sv labels
+  double* alpha;           // n_sv alphas
+  double* sv_rows;         // n_sv x d scaled rows
+  double* mn;              // d: global column min / max the rows were scaled with
+  double* mx;
+  int64_t n_hist;          // rounds recorded on rank 0
+  int64_t* sv_history;     // n_hist global SV counts
+  double* round_ms;        // n_hist round wall times (rank 0)
+  int64_t n_merged;
+  int64_t* merged_history; // star: rank 0's merged set sizes
+  int64_t n_solves;
+  double* solves;          // n_solves x 9: rank, round, layer (star 0 local / -1 merge, tree step),
+                           //   rows, SMO iterations, ms, b, stop reason, of ms the kernel matrix
+  int64_t n_ranks;
+  double* rank_train_ms;   // train_ms of each rank this call drove
+  char transport[16];
+  char backend[16];
+  // Lowest driven rank's wall time per driver phase (cascade.h CascadePhase): upload, scale, bcast,
+  // assemble, solve, select, gather, sendrecv, checkpoint, final.
+  double phase_ms[10];
+} svm_cascade_out;
+
+SVM_API void svm_cascade_default_cfg(svm_cascade_cfg* c);
+// world thread-ranks in this process on the CPU oracle backend, loopback transport; rows X (n x d,
+// float64) are partitioned into contiguous chunks of ceil(n / world) with global ids.
+// Returns NULL on failure (svm_last_error(); a failed rank makes every rank leave its exchange).
+SVM_API svm_cascade_out* svm_cascade_fit_cpu(const double* X, const int32_t* y, int64_t n, int64_t d,
+                                             int32_t world, const svm_cascade_cfg* cfg);
+SVM_API void svm_cascade_free(svm_cascade_out* o);
+
 #ifdef __cplusplus
 }
 #endif

@@ -131,6 +131,28 @@ SVM_API int svmd_count_correct(void* ctx, const double* dec_d, const int32_t* y_
 SVM_API int svmd_gather_rows(void* ctx, const double* src_d, int64_t ld, const int64_t* idx_d,
                              int64_t k, double* dst_d);
 
+// ---- Cascade SVM on MI355X GPUs (csrc/hip/cascade_dev.hip; round logic in csrc/cascade).
+// Thread-rank group of this process: world ranks on GPUs 0..world-1 with one RCCL communicator each
+// (ncclCommInitAll over xGMI, transport "rccl"), or world ranks sharing the visible GPUs with
+// host-staged exchanges ("loopback", a rehearsal of any P on one GPU); "auto" = rccl when world
+// GPUs are visible.  fit partitions X (n x d, float64 or uint8 pixels when u8) into contiguous
+// ceil(n / world) chunks with global ids; the group keeps its contexts / buffers between fits.
+SVM_API void* svmd_cascade_group_create(int32_t world, const char* transport, double comm_timeout_s);
+SVM_API int svmd_cascade_group_world(void* group);
+SVM_API svm_cascade_out* svmd_cascade_group_fit(void* group, const void* X, int32_t u8, const int32_t* y, int64_t n,
+                                                int64_t d, const svm_cascade_cfg* cfg);
+SVM_API void svmd_cascade_group_destroy(void* group);
+// One rank per process (e.g. torchrun): rank 0 makes the id, the launcher distributes it.
+SVM_API int64_t svmd_nccl_unique_id_bytes(void);
+SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap);
+SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32_t world, int32_t rank,
+                                       double comm_timeout_s);
+SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* rank, const void* X, int32_t u8, const int32_t* y,
+                                               const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
+                                               const svm_cascade_cfg* cfg);
+SVM_API int svmd_cascade_rank_barrier(void* rank);
+SVM_API void svmd_cascade_rank_destroy(void* rank);
+
 // roctx ranges (rocprofv3 --marker-trace); the library already brackets preprocess / gram / smo /
 // decision, these let callers mark their own phases (e.g. cascade rounds and exchanges).
 SVM_API void svmd_trace_push(const char* name);

@@ -1,5 +1,6 @@
-"""Distributed Cascade SVM (classical tree + modified two-layer star) and its transports."""
-from .cascade import CascadeSVM, CascadeResult
+"""Distributed training: the native Cascade SVM (classical tree + modified two-layer star) with its
+RCCL bootstraps, and the rank transports of the one-vs-rest trainer."""
+from .cascade import CascadeResult, CascadeSVM, partition_bounds
 from .transport import ThreadTransport, TorchDistTransport, Transport
 
-__all__ = ["CascadeSVM", "CascadeResult", "Transport", "ThreadTransport", "TorchDistTransport"]
+__all__ = ["CascadeSVM", "CascadeResult", "partition_bounds", "Transport", "ThreadTransport", "TorchDistTransport"]

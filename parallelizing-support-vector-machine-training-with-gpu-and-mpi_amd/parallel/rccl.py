@@ -1,0 +1,92 @@
+"""RCCL bootstraps of the native cascade.
+
+``DeviceGroup``  P thread-ranks over GPUs 0..P-1 of THIS process: one ``ncclCommInitAll``, one
+                 communicator + device context per GPU, kept between fits (buffers stay warm).
+                 ``transport="loopback"`` runs the same ranks on fewer GPUs with host-staged
+                 exchanges (rehearsals on one GPU).
+``RcclRank``     one rank per process (torchrun): rank 0 draws the ncclUniqueId, the launcher's
+                 store (``torch.distributed``, any backend, e.g. gloo) distributes it, every process
+                 calls ``ncclCommInitRank`` on its own GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _native as N
+
+
+class DeviceGroup:
+    _shared: dict = {}
+
+    def __init__(self, world: int, transport: str = "auto", comm_timeout_s: float = 600.0):
+        self.world = world
+        self.handle = N.hip().svmd_cascade_group_create(int(world), transport.encode(), float(comm_timeout_s))
+        if not self.handle:
+            raise N.NativeError(N.last_error())
+        self.transport = transport
+
+    @classmethod
+    def shared(cls, world: int, transport: str = "auto") -> "DeviceGroup":
+        """A process-wide group per (world, transport): communicators are created once."""
+        g = cls._shared.get((world, transport))
+        if g is None:
+            g = cls._shared[(world, transport)] = cls(world, transport)
+        return g
+
+    @classmethod
+    def release_shared(cls) -> None:
+        for g in cls._shared.values():
+            g.close()
+        cls._shared.clear()
+
+    def close(self) -> None:
+        if self.handle:
+            N.hip().svmd_cascade_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RcclRank:
+    def __init__(self, device: int, uid: bytes, world: int, rank: int, comm_timeout_s: float = 600.0):
+        self.device, self.world, self.rank = device, world, rank
+        buf = np.frombuffer(uid, dtype=np.uint8).copy()
+        self.handle = N.hip().svmd_cascade_rank_create(int(device), N.ptr(buf), int(world), int(rank),
+                                                      float(comm_timeout_s))
+        if not self.handle:
+            raise N.NativeError(N.last_error())
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = N.hip()
+        n = int(lib.svmd_nccl_unique_id_bytes())
+        buf = np.zeros(n, dtype=np.uint8)
+        N.check(lib.svmd_nccl_unique_id(N.ptr(buf), n), "svmd_nccl_unique_id")
+        return buf.tobytes()
+
+    @classmethod
+    def from_torch_dist(cls, device: int, comm_timeout_s: float = 600.0) -> "RcclRank":
+        """Every rank of an initialised torch.distributed group calls this collectively."""
+        import torch.distributed as dist
+
+        obj = [cls.unique_id() if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(device, obj[0], dist.get_world_size(), dist.get_rank(), comm_timeout_s)
+
+    def barrier(self) -> None:
+        N.check(N.hip().svmd_cascade_rank_barrier(self.handle), "svmd_cascade_rank_barrier")
+
+    def close(self) -> None:
+        if self.handle:
+            N.hip().svmd_cascade_rank_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,19 +1,22 @@
-"""Cascade SVM on CPU ranks: thread-ranks (ThreadTransport) and a real
-multi-process gloo group (TorchDistTransport), both topologies."""
-import os
-import socket
+"""Cascade SVM on CPU thread-ranks: the ONE native driver (csrc/cascade) on the
+C++ oracle backend with the loopback transport — the same round code the GPUs run.
+
+Parity is pinned against an independent Python transcription of the reference round loops
+(mpi_svm_main2.cpp:439-769 star, mpi_svm_main3.cpp:565-828 tree) on the same oracle SMO: rounds,
+SV ids and b must be bit-identical."""
+import time
 
 import numpy as np
 import pytest
-import torch
 
 from svm355 import SVMParams
+from svm355._native import NativeError
 from svm355.ops import cpu as C
-from svm355.parallel.cascade import CascadeSVM, SVSet, merge_unseen, partition_bounds, _CpuBackend
-from svm355.parallel.transport import run_threads
+from svm355.parallel.cascade import CascadeSVM, partition_bounds
 from svm355.utils.data import MinMaxScaler, synthetic_mnist
 
 N_TRAIN = 1500
+P2 = SVMParams(n_threads=2)
 
 
 @pytest.fixture(scope="module")
@@ -21,133 +24,148 @@ def data():
     return synthetic_mnist(N_TRAIN, seed=11), synthetic_mnist(500, seed=11, offset=N_TRAIN)
 
 
-def _single(tr):
-    p = SVMParams(n_threads=4)
-    X = MinMaxScaler().fit_transform(tr.X)
-    a, res, _ = C.smo_train(X, tr.y, p)
-    return set(np.flatnonzero(a > p.sv_tol).tolist()), res.b
+# ------------------------------------------------------------------ independent transcription
+def _solve(X, y, a):
+    a2, res, _ = C.smo_train(X, y, P2, alpha=a.copy(), warm=True)
+    keep = np.flatnonzero(a2 > P2.sv_tol)
+    return (X[keep], y[keep], a2[keep]), res.b, keep
 
 
-def _run(world, topology, tr, te, **kw):
-    def fn(t):
-        lo, hi = partition_bounds(tr.n, t.world, t.rank)
-        c = CascadeSVM(t, SVMParams(n_threads=2), topology=topology, verbose=0, **kw)
-        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=tr.n)
-        return c.summary(), c.score(te.X, te.y), set(c.result.sv.ids.tolist())
-
-    return run_threads(world, fn)
+def _merge_unseen(warm, extra):  # M3 :629-655 / M2 :474-502
+    (Xw, yw, aw, iw), (Xe, ye, _, ie) = warm, extra
+    keep = np.flatnonzero(~np.isin(ie, iw))
+    return (np.concatenate([Xw, Xe[keep]]), np.concatenate([yw, ye[keep]]),
+            np.concatenate([aw, np.zeros(len(keep))]), np.concatenate([iw, ie[keep]]))
 
 
+def _py_cascade(tr, P, topology):
+    Xs = MinMaxScaler().fit_transform(tr.X)  # global min/max (M3 :529-539)
+    parts = []
+    for r in range(P):
+        lo, hi = partition_bounds(tr.n, P, r)
+        parts.append((Xs[lo:hi], tr.y[lo:hi], np.zeros(hi - lo), np.arange(lo, hi)))
+    G = (np.empty((0, tr.d)), np.empty(0, np.int32), np.empty(0), np.empty(0, np.int64))
+    prev, b, rounds, hist = None, 0.0, 0, []
+    while rounds < 50:
+        rounds += 1
+        if topology == "star":
+            local = []
+            for r in range(P):
+                S = _merge_unseen(G, parts[r])
+                (Xk, yk, ak), _, keep = _solve(*S[:3])
+                local.append((Xk, yk, ak, S[3][keep]))
+            merged = local[0]
+            for w in local[1:]:  # worker alphas reset to 0 (M2 :600-601), source order (M2 :578)
+                merged = _merge_unseen(merged, (w[0], w[1], np.zeros(len(w[1])), w[3]))
+            (Xk, yk, ak), b, keep = _solve(*merged[:3])
+            G = (Xk, yk, ak, merged[3][keep])
+        else:
+            cur = {}
+            recv = {0: G}
+            step = 1
+            while step <= P:
+                for r in range(0, P, step):
+                    S = _merge_unseen(recv.get(r, G) if step > 1 else G, cur.get(r, parts[r]))
+                    (Xk, yk, ak), bl, keep = _solve(*S[:3])
+                    cur[r] = (Xk, yk, ak, S[3][keep])
+                    if r == 0:
+                        b = bl
+                recv = {r: cur[r + step] for r in range(0, P, 2 * step) if r + step < P}
+                step *= 2
+            G = cur[0]
+        hist.append(len(G[3]))
+        ids = set(G[3].tolist())
+        if ids == prev:
+            break
+        prev = ids
+    return rounds, sorted(G[3].tolist()), b, hist
+
+
+# ------------------------------------------------------------------------------------ tests
 def test_partition_bounds():
     assert [partition_bounds(10, 4, r) for r in range(4)] == [(0, 3), (3, 6), (6, 9), (9, 10)]
     assert partition_bounds(2, 4, 3) == (2, 2)
 
 
-def test_merge_unseen_keeps_warm_alpha_and_order():
-    be = _CpuBackend(SVMParams(), 2)
-    warm = SVSet(torch.tensor([[1.0, 1.0], [2.0, 2.0]]), np.array([1, -1], np.int32), np.array([0.5, 0.7]),
-                 np.array([10, 20]))
-    extra = SVSet(torch.tensor([[3.0, 3.0], [2.0, 2.0], [4.0, 4.0]]), np.array([1, -1, 1], np.int32),
-                  np.array([9.0, 9.0, 9.0]), np.array([30, 20, 40]))
-    m = merge_unseen(be, warm, extra)
-    assert m.ids.tolist() == [10, 20, 30, 40]
-    assert m.alpha.tolist() == [0.5, 0.7, 0.0, 0.0]
-    assert m.X[:, 0].tolist() == [1, 2, 3, 4]
-
-
-def test_svset_pack_roundtrip():
-    s = SVSet(torch.arange(6, dtype=torch.float64).reshape(2, 3), np.array([1, -1], np.int32),
-              np.array([0.25, 3.5]), np.array([7, 2 ** 40]))
-    u = SVSet.unpack(s.pack(), 3)
-    assert torch.equal(u.X, s.X) and u.y.tolist() == [1, -1] and u.alpha.tolist() == [0.25, 3.5]
-    assert u.ids.tolist() == [7, 2 ** 40]
+@pytest.mark.parametrize("topology,world", [("star", 2), ("star", 3), ("tree", 2), ("tree", 4)])
+def test_native_driver_bit_identical_to_transcription(data, topology, world):
+    tr, _ = data
+    nat = CascadeSVM(P2, topology=topology).fit(tr.X, tr.y, world=world).result
+    rounds, ids, b, hist = _py_cascade(tr, world, topology)
+    assert nat.rounds == rounds and nat.sv_history == hist
+    assert sorted(nat.ids.tolist()) == ids
+    assert nat.b == b
 
 
 @pytest.mark.parametrize("topology,world", [("star", 1), ("star", 2), ("star", 3), ("tree", 2), ("tree", 4)])
 def test_cascade_threads_converge_to_single_solve(data, topology, world):
     tr, te = data
-    single_ids, single_b = _single(tr)
-    out = _run(world, topology, tr, te)
-    s0, acc0, ids0 = out[0]
-    assert s0["converged"]
-    assert s0["rounds"] <= 10
-    # every rank holds the same final model
-    for s, acc, ids in out[1:]:
-        assert ids == ids0 and s["b"] == s0["b"] and acc == acc0
-    # same optimum as one global SMO within the stopping tolerance
-    assert len(ids0 ^ single_ids) <= max(3, len(single_ids) // 50)
-    assert abs(s0["b"] - single_b) < 5e-3 * max(1.0, abs(single_b))
-    assert acc0 > 0.95
+    p = SVMParams(n_threads=4)
+    a, res, _ = C.smo_train(MinMaxScaler().fit_transform(tr.X), tr.y, p)
+    single = set(np.flatnonzero(a > p.sv_tol).tolist())
+    c = CascadeSVM(P2, topology=topology).fit(tr.X, tr.y, world=world)
+    r = c.result
+    assert r.converged and r.rounds <= 10 and r.backend == "cpu" and r.transport == "loopback"
+    assert len(set(r.ids.tolist()) ^ single) <= max(3, len(single) // 50)
+    assert abs(r.b - res.b) < 5e-3 * max(1.0, abs(res.b))
+    assert c.score(te.X, te.y) > 0.95
+    # per-solve log: every rank's solves with rows / iterations
+    assert {s["rank"] for s in r.solves} == set(range(world))
+    assert all(s["iterations"] >= 1 and s["n"] > 0 for s in r.solves)
 
 
 def test_fit_and_score_do_not_mutate_inputs(data):
     tr, te = data
     X0, T0 = tr.X.copy(), te.X.copy()
-    _run(2, "star", tr, te)
+    CascadeSVM(P2).fit(tr.X, tr.y, world=2).score(te.X, te.y)
     np.testing.assert_array_equal(tr.X, X0)
     np.testing.assert_array_equal(te.X, T0)
 
 
 def test_tree_rejects_non_power_of_two(data):
-    tr, te = data
+    tr, _ = data
     with pytest.raises(ValueError, match="power-of-2"):
-        _run(3, "tree", tr, te)
+        CascadeSVM(P2, topology="tree").fit(tr.X, tr.y, world=3)
 
 
-def test_checkpoint_resume(tmp_path, data):
-    tr, te = data
-    full = _run(2, "star", tr, te, checkpoint_dir=str(tmp_path))[0][0]
-    assert (tmp_path / "cascade_state.npz").exists()
-    # Resume from the final state: converges in one more round with the same model.
-    res = _run(2, "star", tr, te, checkpoint_dir=str(tmp_path), resume=True)[0][0]
-    assert res["converged"] and res["n_sv"] == full["n_sv"]
-    assert abs(res["b"] - full["b"]) < 1e-9 * max(1, abs(full["b"]))
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _gloo_worker(rank, world, port, topology, q):
-    import torch.distributed as dist
-
-    from svm355.parallel.transport import TorchDistTransport
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        tr = synthetic_mnist(N_TRAIN, seed=11)
-        te = synthetic_mnist(500, seed=11, offset=N_TRAIN)
-        lo, hi = partition_bounds(tr.n, world, rank)
-        t = TorchDistTransport(torch.device("cpu"))
-        c = CascadeSVM(t, SVMParams(n_threads=2), topology=topology, verbose=0)
-        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=tr.n)
-        q.put((rank, c.summary(), c.score(te.X, te.y), sorted(c.result.sv.ids.tolist())))
-    finally:
-        dist.destroy_process_group()
+def test_empty_data_is_an_error():
+    with pytest.raises(NativeError, match="No data read"):
+        CascadeSVM(P2).fit(np.empty((0, 4)), np.empty(0, np.int32), world=2)
 
 
 @pytest.mark.parametrize("topology", ["star", "tree"])
-def test_cascade_gloo_two_processes_matches_threads(data, topology):
-    import torch.multiprocessing as mp
+def test_checkpoint_resume_bit_identical(tmp_path, data, topology):
+    tr, _ = data
+    full = CascadeSVM(P2, topology=topology).fit(tr.X, tr.y, world=2).result
+    ck = str(tmp_path / topology)
+    part = CascadeSVM(P2, topology=topology, max_rounds=1, checkpoint_dir=ck).fit(tr.X, tr.y, world=2).result
+    assert part.rounds == 1 and not part.converged and (tmp_path / topology / "cascade_state.bin").exists()
+    res = CascadeSVM(P2, topology=topology, checkpoint_dir=ck, resume=True).fit(tr.X, tr.y, world=2).result
+    assert res.converged and res.rounds == full.rounds
+    assert sorted(res.ids.tolist()) == sorted(full.ids.tolist()) and res.b == full.b
 
-    tr, te = data
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, topology, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    res.sort()
-    thr = _run(2, topology, tr, te)[0]
-    for _, s, acc, ids in res:
-        assert s["converged"] and s["rounds"] == thr[0]["rounds"]
-        assert s["b"] == thr[0]["b"]  # identical arithmetic, identical transport payloads
-        assert ids == sorted(thr[2])
-        assert acc == thr[1]
+
+def test_checkpoint_of_other_topology_is_rejected(tmp_path, data):
+    tr, _ = data
+    CascadeSVM(P2, topology="star", max_rounds=1, checkpoint_dir=str(tmp_path)).fit(tr.X, tr.y, world=2)
+    with pytest.raises(NativeError, match="does not match"):
+        CascadeSVM(P2, topology="tree", checkpoint_dir=str(tmp_path), resume=True).fit(tr.X, tr.y, world=2)
+
+
+@pytest.mark.parametrize("world,fail_rank,fail_round", [(2, 1, 1), (3, 0, 0), (4, 2, 1)])
+def test_failing_rank_ends_every_rank(data, world, fail_rank, fail_round):
+    """One rank throws mid-run: the others leave their exchanges and the call reports that rank."""
+    tr, _ = data
+    t0 = time.perf_counter()
+    with pytest.raises(NativeError, match=f"rank {fail_rank}: injected failure at round {fail_round}"):
+        CascadeSVM(P2, comm_timeout_s=60, fail_rank=fail_rank, fail_round=fail_round).fit(tr.X, tr.y, world=world)
+    assert time.perf_counter() - t0 < 30  # no deadline was needed: the abort token ended the waits
+
+
+def test_stalled_rank_hits_the_deadline(data):
+    """A rank that stops responding: its peers' exchanges time out instead of hanging."""
+    tr, _ = data
+    t0 = time.perf_counter()
+    with pytest.raises(NativeError, match="no progress for 0.5 s"):
+        CascadeSVM(P2, comm_timeout_s=0.5, fail_rank=1, fail_round=1, fail_stall_s=3.0).fit(tr.X, tr.y, world=2)
+    assert time.perf_counter() - t0 < 30

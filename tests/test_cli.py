@@ -45,13 +45,17 @@ def test_cli_cascade_single_rank_cpu(tmp_path, topology):
     assert s["converged"] and s["world"] == 1 and s["accuracy"] > 0.9
 
 
-def test_cli_cascade_two_ranks_gloo(tmp_path):
+def test_cli_cascade_two_ranks_cpu(tmp_path):
     js = tmp_path / "c2.json"
-    out = _run(["cascade", "--synthetic", "900,200", "--cpu", "--gpus", "2", "--backend", "gloo",
-                "--json", str(js)], tmp_path, timeout=900)
+    out = _run(["cascade", "--synthetic", "900,200", "--cpu", "--gpus", "2", "--json", str(js),
+                "--model-dir", str(tmp_path / "m")], tmp_path, timeout=900)
     assert "[rank 0] Running modified CascadeSVM with 2 processes" in out
+    assert "[rank 0] merged unique SV count from workers = " in out and "=== Round 0 ===" in out
     s = json.loads(js.read_text())
-    assert s["converged"] and s["world"] == 2
+    assert s["converged"] and s["world"] == 2 and s["backend"] == "cpu"
+    assert {x["rank"] for x in s["solves"]} == {0, 1}
+    for f in ("final_sv_ids.txt", "final_sv_labels.txt", "final_sv_alphas.txt", "final_b.txt"):
+        assert (tmp_path / "m" / f).exists()
 
 
 def test_native_cascade_rejects_non_power_of_two_tree():

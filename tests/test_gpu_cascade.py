@@ -1,76 +1,148 @@
-"""Cascade SVM with the gfx950 device solver: multi-process SPMD ranks sharing one GPU (gloo group
-for the exchanges, HIP for every solve), compared with the CPU-oracle cascade."""
-import os
-import socket
+"""Cascade SVM on the gfx950 backend (csrc/hip/cascade_dev.hip) driven by the one native driver.
+
+* HIP backend vs the CPU-oracle backend on the same partitions (kernel values differ in the last
+  ulps between the MFMA norm form and the direct sum, so tolerances);
+* RCCL transport (group of one GPU, and a per-process rank bootstrapped from an ncclUniqueId) vs
+  the loopback transport: bit-identical;
+* the native CLI bin/svm_cascade: reference stdout lines, checkpoint/resume, fault injection.
+
+RCCL refuses two ranks on one GPU, so multi-rank runs on the one-GPU box use the loopback
+transport; RCCL itself runs here with one rank (ncclCommInitAll and ncclCommInitRank)."""
+import json
+import subprocess
+from pathlib import Path
 
 import numpy as np
 import pytest
-import torch
 
-from svm355 import SVMParams
-from svm355.parallel.cascade import CascadeSVM, partition_bounds
-from svm355.parallel.transport import run_threads
+from svm355 import SVC, SVMParams
+from svm355._native import NativeError
+from svm355.parallel.cascade import CascadeSVM
+from svm355.parallel.rccl import DeviceGroup, RcclRank
 from svm355.utils.data import synthetic_mnist
 
 pytestmark = pytest.mark.gpu
 
-N = 2000
+EXE = Path(__file__).resolve().parents[1] / "svm355" / "bin" / "svm_cascade"
+N, M = 2000, 500
 
 
-def _worker(rank, world, port, topology, q):
-    import torch.distributed as dist
+@pytest.fixture(scope="module")
+def data():
+    return synthetic_mnist(N, seed=21), synthetic_mnist(M, seed=21, offset=N)
 
-    from svm355.parallel.transport import TorchDistTransport
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        tr = synthetic_mnist(N, seed=21)
-        te = synthetic_mnist(500, seed=21, offset=N)
-        lo, hi = partition_bounds(N, world, rank)
-        t = TorchDistTransport(torch.device("cpu"))
-        c = CascadeSVM(t, SVMParams(), topology=topology, verbose=0, device=torch.device("cuda:0"))
-        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=N)
-        q.put((rank, c.summary(), c.score(te.X, te.y), sorted(c.result.sv.ids.tolist())))
-    except BaseException as e:  # report instead of hanging the parent
-        q.put((rank, {"error": repr(e)}, 0.0, []))
-        raise
-    finally:
-        dist.destroy_process_group()
+@pytest.mark.parametrize("topology,world", [("star", 1), ("star", 2), ("star", 3), ("tree", 2), ("tree", 4)])
+def test_hip_cascade_matches_cpu_cascade(data, topology, world):
+    tr, te = data
+    g = CascadeSVM(SVMParams(), topology=topology).fit(tr.compact().X, tr.y, world=world, device="cuda",
+                                                       transport="loopback")
+    c = CascadeSVM(SVMParams(n_threads=4), topology=topology).fit(tr.X, tr.y, world=world)
+    rg, rc = g.result, c.result
+    assert rg.backend == "hip" and rg.transport == "loopback" and rg.converged
+    assert abs(rg.b - rc.b) < 1e-5 * max(1.0, abs(rc.b))
+    assert len(set(rg.ids.tolist()) ^ set(rc.ids.tolist())) <= 2
+    assert abs(g.score(te.X, te.y) - c.score(te.X, te.y)) <= 0.002
+    assert {s["rank"] for s in rg.solves} == set(range(world))
+
+
+def test_hip_cascade_one_rank_finds_the_single_gpu_svs(data):
+    tr, _ = data
+    g = CascadeSVM(SVMParams()).fit(tr.compact().X, tr.y, world=1, device="cuda", transport="loopback")
+    s = SVC(device="cuda:0").fit(tr.compact().X, tr.y)
+    assert sorted(g.result.ids.tolist()) == sorted(s.support_.tolist())
+    first = g.result.solves[0]
+    assert first["layer"] == "local" and first["iterations"] == s.n_iter_  # same trajectory as the SVC fit
 
 
 @pytest.mark.parametrize("topology", ["star", "tree"])
-def test_multiprocess_hip_cascade_matches_cpu_cascade(topology):
-    import torch.multiprocessing as mp
+def test_rccl_group_equals_loopback(data, topology):
+    tr, _ = data
+    X = tr.compact().X
+    a = CascadeSVM(SVMParams(), topology=topology).fit(X, tr.y, world=1, device="cuda", transport="rccl").result
+    b = CascadeSVM(SVMParams(), topology=topology).fit(X, tr.y, world=1, device="cuda", transport="loopback").result
+    assert a.transport == "rccl" and b.transport == "loopback"
+    assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
+    np.testing.assert_array_equal(a.alpha, b.alpha)
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, topology, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=600) for _ in procs)
-    for p in procs:
-        p.join(timeout=120)
-    for _, s, _, _ in res:
-        assert "error" not in s, s
-    assert all(p.exitcode == 0 for p in procs)
-    (_, s0, acc0, ids0), (_, s1, acc1, ids1) = res
-    assert s0["converged"] and ids0 == ids1 and s0["b"] == s1["b"]
 
+def test_rccl_rank_bootstrap_equals_group(data):
+    """The per-process path (ncclUniqueId -> ncclCommInitRank) with a world of one."""
+    tr, _ = data
+    X = tr.compact().X
+    rank = RcclRank(0, RcclRank.unique_id(), 1, 0, comm_timeout_s=60)
+    try:
+        rank.barrier()
+        a = CascadeSVM(SVMParams()).fit_rank(rank, X, tr.y, np.arange(N), N).result
+    finally:
+        rank.close()
+    b = CascadeSVM(SVMParams()).fit(X, tr.y, world=1, device="cuda", transport="rccl").result
+    assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
+
+
+def test_group_keeps_working_after_a_loopback_failure(data):
+    tr, _ = data
+    X = tr.compact().X
+    g = DeviceGroup(2, "loopback")
+    try:
+        with pytest.raises(NativeError, match="rank 1: injected failure"):
+            CascadeSVM(SVMParams(), fail_rank=1, fail_round=1).fit(X, tr.y, world=2, device="cuda", group=g)
+        r = CascadeSVM(SVMParams()).fit(X, tr.y, world=2, device="cuda", group=g).result
+        assert r.converged
+    finally:
+        g.close()
+
+
+def test_rccl_failure_aborts_the_communicator(data):
+    tr, _ = data
+    X = tr.compact().X
+    g = DeviceGroup(1, "rccl")
+    try:
+        with pytest.raises(NativeError, match="rank 0: injected failure"):
+            CascadeSVM(SVMParams(), fail_rank=0, fail_round=0).fit(X, tr.y, world=1, device="cuda", group=g)
+        with pytest.raises(NativeError, match="aborted"):
+            CascadeSVM(SVMParams()).fit(X, tr.y, world=1, device="cuda", group=g)
+    finally:
+        g.close()
+
+
+def _cli(tmp_path, name, *extra):
+    out = tmp_path / name
+    r = subprocess.run([str(EXE), "--synthetic", f"{N},{M}", "--seed", "21", "--json", str(out), "--quiet", *extra],
+                       capture_output=True, text=True, timeout=240)
+    return r, (json.loads(out.read_text()) if out.exists() else None)
+
+
+@pytest.mark.parametrize("topology,world", [("star", 2), ("tree", 2)])
+def test_native_cli_matches_python_binding(tmp_path, topology, world):
+    r, nat = _cli(tmp_path, "n.json", "--topology", topology, "--gpus", str(world), "--transport", "loopback")
+    assert r.returncode == 0, r.stdout + r.stderr
     tr = synthetic_mnist(N, seed=21)
-    te = synthetic_mnist(500, seed=21, offset=N)
+    py = CascadeSVM(SVMParams(), topology=topology).fit(tr.X, tr.y, world=world, device="cuda",
+                                                        transport="loopback").result
+    assert nat["sv_ids"] == sorted(py.ids.tolist()) and nat["b"] == py.b and nat["rounds"] == py.rounds
+    head = "modified CascadeSVM" if topology == "star" else "CascadeSVM"
+    assert f"[rank 0] Running {head} with {world} processes" in r.stdout
+    assert f"[rank 0] total samples = {N}, features = 784" in r.stdout
+    assert "[rank 0] Final b = " in r.stdout and f"[rank 0] Cascade finished in {nat['rounds']} rounds" in r.stdout
 
-    def fn(t):
-        lo, hi = partition_bounds(N, t.world, t.rank)
-        c = CascadeSVM(t, SVMParams(n_threads=4), topology=topology, verbose=0)
-        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=N)
-        return c.summary(), c.score(te.X, te.y), sorted(c.result.sv.ids.tolist())
 
-    cpu = run_threads(2, fn)[0]
-    # Same cascade, kernel values differ in the last ulps (MFMA norm form vs direct sum).
-    assert abs(s0["b"] - cpu[0]["b"]) < 1e-5 * max(1.0, abs(cpu[0]["b"]))
-    assert len(set(ids0) ^ set(cpu[2])) <= 2
-    assert abs(acc0 - cpu[1]) <= 0.002
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_native_cli_checkpoint_resume(tmp_path, topology):
+    base = ["--topology", topology, "--gpus", "2", "--transport", "loopback"]
+    r, full = _cli(tmp_path, "full.json", *base)
+    assert r.returncode == 0, r.stderr
+    ck = str(tmp_path / f"ck_{topology}")
+    r, part = _cli(tmp_path, "part.json", *base, "--max-rounds", "1", "--checkpoint-dir", ck)
+    assert r.returncode == 0 and part["rounds"] == 1 and not part["converged"]
+    r, res = _cli(tmp_path, "res.json", *base, "--checkpoint-dir", ck, "--resume")
+    assert r.returncode == 0 and "[rank 0] resumed from checkpoint at round 1" in r.stdout
+    assert res["converged"] and res["rounds"] == full["rounds"]
+    assert res["sv_ids"] == full["sv_ids"] and res["b"] == full["b"]
+
+
+def test_native_cli_failed_rank_exits_nonzero(tmp_path):
+    r, js = _cli(tmp_path, "f.json", "--gpus", "3", "--transport", "loopback", "--fail-rank", "2", "--fail-round", "1",
+                 "--comm-timeout", "60")
+    assert r.returncode == 1 and js is None
+    assert "rank 2: injected failure at round 1" in r.stderr

@@ -3,8 +3,6 @@
 Numerics tests compare each HIP kernel with a PyTorch/numpy fp64 computation of the same op; the
 device SMO is checked bit-for-bit against the CPU oracle when both run on the same kernel matrix.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -284,49 +282,6 @@ def test_svc_cuda_save_load(tmp_path, dev, mn_data):
     g.save(tmp_path / "m")
     g2 = SVC.load(tmp_path / "m", device="cuda")
     np.testing.assert_allclose(g2.decision_function(te.X), g.decision_function(te.X), atol=1e-12)
-
-
-def test_cascade_thread_ranks_on_one_gpu(dev, mn_data):
-    from svm355.parallel.cascade import CascadeSVM, partition_bounds
-    from svm355.parallel.transport import run_threads
-
-    tr, te = mn_data
-
-    def fn(t):
-        lo, hi = partition_bounds(tr.n, t.world, t.rank)
-        c = CascadeSVM(t, SVMParams(), topology="star", verbose=0)
-        c.fit(tr.X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), n_total=tr.n)
-        return c.summary(), c.score(te.X, te.y)
-
-    out = run_threads(2, fn, device_for_rank=lambda r: dev)
-    assert out[0][0]["converged"] and out[0][0]["n_sv"] == out[1][0]["n_sv"]
-    single = SVC(device="cuda").fit(tr.X, tr.y)
-    assert abs(out[0][0]["n_sv"] - len(single.support_)) <= max(3, len(single.support_) // 50)
-    assert out[0][1] >= single.score(te.X, te.y) - 0.01
-
-
-def test_cascade_rccl_single_rank_group(dev, mn_data):
-    """TorchDistTransport over the nccl (= RCCL) backend, world size 1, both topologies."""
-    import torch.distributed as dist
-
-    from svm355.parallel.cascade import CascadeSVM
-    from svm355.parallel.transport import TorchDistTransport
-
-    tr, te = mn_data
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    try:
-        t = TorchDistTransport(dev)
-        for topo in ("star", "tree"):
-            c = CascadeSVM(t, SVMParams(), topology=topo, verbose=0)
-            c.fit(tr.X, tr.y, np.arange(tr.n), n_total=tr.n)
-            assert c.result.converged
-            assert c.score(te.X, te.y) > 0.95
-    finally:
-        dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------- exact-integer Gram (igram.hip)
