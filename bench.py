@@ -214,6 +214,7 @@ def main(argv=None):
                  "driver_train_ms": round(r.train_ms, 3), "rank0_phase_ms": r.phase_ms,
                  "per_round_critical_path": crit, "critical_path_solve_ms": crit_ms,
                  "rank0_smo_iterations": int(sum(s["iterations"] for s in r0)),
+                 "skipped_solves": int(sum(s["skipped"] for s in solves)),
                  "max_rank_smo_iterations": max(sum(s["iterations"] for s in solves if s["rank"] == q)
                                                 for q in range(max(1, r.world))),
                  "note": "per_round_critical_path = [round, slowest local solve ms (tree: first layer), rank-0 "

@@ -112,12 +112,13 @@ class SvmCascadeOut(ctypes.Structure):
         ("rank_train_ms", POINTER(c_double)),
         ("transport", ctypes.c_char * 16),
         ("backend", ctypes.c_char * 16),
-        ("phase_ms", c_double * 10),
+        ("phase_ms", c_double * 11),
     ]
 
 
+SOLVE_COLS = 10  # svm355.h SVM_CASCADE_SOLVE_COLS
 CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
-                  "final")
+                  "final", "setup")
 
 
 _P = c_void_p  # raw pointers are passed as integers / c_void_p

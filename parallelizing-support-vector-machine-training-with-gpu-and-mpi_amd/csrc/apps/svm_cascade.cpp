@@ -188,9 +188,9 @@ int main(int argc, char** argv) {
   printf("[rank 0] elapsed time = %d ms\n", int(R->train_ms + pred_ms));
   int64_t r0_solves = 0, r0_iters = 0;
   for (int64_t i = 0; i < R->n_solves; ++i)
-    if (R->solves[9 * i] == 0.0) {
+    if (R->solves[SVM_CASCADE_SOLVE_COLS * i] == 0.0) {
       ++r0_solves;
-      r0_iters += int64_t(R->solves[9 * i + 4]);
+      r0_iters += int64_t(R->solves[SVM_CASCADE_SOLVE_COLS * i + 4]);
     }
   if (!o.quiet)
     fprintf(stderr, "[svm_cascade] transport %s, %lld solves on rank 0, %lld SMO iterations on rank 0\n", R->transport,

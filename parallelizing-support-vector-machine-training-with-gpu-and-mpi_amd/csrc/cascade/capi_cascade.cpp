@@ -78,11 +78,12 @@ svm_cascade_out* build_cascade_out(const std::vector<const CascadeOutput*>& outs
     tms.push_back(x->train_ms);
     for (const SolveLog& s : x->solves)
       solves.insert(solves.end(), {double(s.rank), double(s.round), double(s.layer), double(s.rows),
-                                   double(s.iterations), s.ms, s.b, double(s.stop), s.gram_ms});
+                                   double(s.iterations), s.ms, s.b, double(s.stop), s.gram_ms,
+                                   s.skipped ? 1.0 : 0.0});
   }
   static_assert(kNumPhases == sizeof(o->phase_ms) / sizeof(double), "svm_cascade_out.phase_ms size");
   std::copy(R.phase_ms, R.phase_ms + kNumPhases, o->phase_ms);
-  o->n_solves = int64_t(solves.size() / 9);
+  o->n_solves = int64_t(solves.size() / SVM_CASCADE_SOLVE_COLS);
   o->solves = dup(solves);
   o->n_ranks = int64_t(tms.size());
   o->rank_train_ms = dup(tms);

@@ -89,6 +89,69 @@ void run_rank_threads(int P, const std::shared_ptr<AbortToken>& token, const std
   }
 }
 
+RankPool::RankPool(int P) : P_(P) {
+  th_.reserve(size_t(P));
+  for (int r = 0; r < P; ++r) th_.emplace_back([this, r] { loop(r); });
+}
+
+RankPool::~RankPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+    ++gen_;
+  }
+  cv_.notify_all();
+  for (auto& t : th_) t.join();
+}
+
+void RankPool::loop(int r) {
+  uint64_t seen = 0;
+  for (;;) {
+    const std::function<void(int)>* job;
+    std::shared_ptr<AbortToken> token;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+      job = job_;
+      token = token_;
+    }
+    try {
+      (*job)(r);
+    } catch (const CascadeAborted&) {
+    } catch (const std::exception& e) {
+      token->raise("rank " + std::to_string(r) + ": " + e.what());
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+}
+
+void RankPool::run(const std::shared_ptr<AbortToken>& token, const std::function<void(int)>& fn,
+                   const std::function<void(int)>& on_abort) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    job_ = &fn;
+    token_ = token;
+    pending_ = P_;
+    ++gen_;
+  }
+  cv_.notify_all();
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+    token_.reset();
+  }
+  if (token->raised()) {
+    for (int r = 0; r < P_; ++r) on_abort(r);
+    throw CascadeError(token->why());
+  }
+}
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
@@ -135,6 +198,7 @@ class Rank {
   std::vector<double> mn_h, mx_h;
   std::vector<SolveLog> log;
   double phase[kNumPhases] = {};
+  int64_t skipped = 0;  // solves whose warm start already met the stop test
   PhaseTimer timer(CascadePhase p) { return PhaseTimer(B_, phase[p], prof_); }
 
   DSet make(int64_t k) {
@@ -216,15 +280,27 @@ class Rank {
                      Segment{&extra, nullptr, 0, nullptr, &keep, true}});
   }
 
-  // Warm-start SMO on S; returns (its SVs with alpha > sv_tol, in S order, b).
-  std::pair<DSet, double> solve(DSet& S, int rnd, int layer) {
+  // Warm-start SMO on S; returns (its SVs with alpha > sv_tol, in S order, b).  warm_rows: S's
+  // leading rows that carry the warm alphas; skippable: the solve's b is not part of the model, so
+  // a warm start that provably meets the stop test may skip the solve (Backend::warm_start_converged:
+  // the solve would have stopped at its first selection with the same alphas).
+  std::pair<DSet, double> solve(DSet& S, int rnd, int layer, int64_t warm_rows = 0, bool skippable = false) {
     if (S.k == 0) return {make(0), 0.0};
     Range tr(B_, "cascade:solve");
     const auto t0 = Clock::now();
     SolveStats st;
+    bool skipped_now = false;
     {
       auto tm = timer(kPhSolve);
-      st = B_.solve(S, d_, cfg_.params, mn_h.data(), mx_h.data());
+      if (skippable && warm_rows > 0 && B_.warm_start_converged(S, warm_rows, d_, cfg_.params)) {
+        st.iterations = 1;  // what the solve reports when it stops at its first selection
+        st.stop = SVM_STOP_CONVERGED;
+        st.b = 0.0;         // not part of the model (skippable)
+        ++skipped;
+        skipped_now = true;
+      } else {
+        st = B_.solve(S, d_, cfg_.params, mn_h.data(), mx_h.data());
+      }
     }
     auto tm = timer(kPhSelect);
     std::vector<double> a(size_t(S.k));
@@ -234,7 +310,8 @@ class Rank {
       if (a[size_t(i)] > cfg_.params.sv_tol) keep.push_back(i);
     DSet out = assemble({Segment{&S, nullptr, 0, nullptr, &keep, false}});
     log.push_back(
-        SolveLog{t_.rank(), rnd, layer, S.k, st.iterations, ms_between(t0, Clock::now()), st.b, st.stop, st.gram_ms});
+        SolveLog{t_.rank(), rnd, layer, S.k, st.iterations, ms_between(t0, Clock::now()), st.b, st.stop, st.gram_ms,
+                              skipped_now});
     return {std::move(out), st.b};
   }
 
@@ -407,6 +484,7 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
                           int64_t n_part, int64_t d, int64_t n_total, const CascadeConfig& cfg) {
   const int P = t.world(), me = t.rank();
   const bool log = cfg.log && me == 0;
+  const auto t_entry = Clock::now();
   if (cfg.tree && (P & (P - 1)))  // mpi_svm_main3.cpp:420-428 aborts on a non-power-of-2 world
     throw CascadeError("classical (tree) cascade needs a power-of-2 number of ranks, got " + std::to_string(P));
   const int64_t d0 = t.bcast_i64(d, 0);
@@ -419,12 +497,19 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
     printf("[rank 0] total samples = %lld, features = %lld\n", (long long)n_total, (long long)d);
     fflush(stdout);
   }
+  const auto t_bc = Clock::now();
   DSet part = R.upload(X, u8, y, ids, n_part);  // data distribution (not timed, M3 :526)
+  const auto t_up = Clock::now();
   B.sync();
+  const auto t_sy = Clock::now();
   t.barrier();
+  if (const char* e = getenv("SVM355_CASCADE_PROFILE"); e && atoi(e) >= 2)
+    fprintf(stderr, "[cascade rank %d] setup: bcasts %.3f ms, upload %.3f ms, sync %.3f ms, barrier %.3f ms\n", me,
+            ms_between(t_entry, t_bc), ms_between(t_bc, t_up), ms_between(t_up, t_sy), ms_between(t_sy, Clock::now()));
 
   CascadeOutput out;
   const auto t0 = Clock::now();
+  R.phase[kPhSetup] = ms_between(t_entry, t0) - R.phase[kPhUpload];
   R.scale_global(part);
   DSet G = R.make(0);  // global SV set (meaningful on rank 0; broadcast each round)
   std::unordered_set<int64_t> global_ids;
@@ -456,7 +541,7 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
     int64_t same = 0;
     if (!cfg.tree) {
       DSet S = R.merge_unseen(Gb, part);
-      DSet local = R.solve(S, shown, 0).first;
+      DSet local = R.solve(S, shown, 0, Gb.k, true).first;
       const auto g = R.gather_sets(local);
       if (me == 0) {
         // merged = own SVs (alphas kept) U unseen worker SVs in source order 1..P-1 with their
@@ -501,7 +586,7 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
       for (int step = 1; step <= P; step *= 2) {
         if (me % step == 0) {  // receiver's SVs warm, own rows not among them cold (M3 :629-660)
           DSet S = R.merge_unseen(recv, *cur);
-          auto res = R.solve(S, shown, step);
+          auto res = R.solve(S, shown, step, recv.k, !(me == 0 && step == P));
           own = std::move(res.first);
           cur = &own;
           if (me == 0) b = res.second;

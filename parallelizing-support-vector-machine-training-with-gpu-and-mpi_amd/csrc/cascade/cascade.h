@@ -29,6 +29,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "svm355.h"
@@ -156,6 +157,11 @@ class Backend {
   // Warm-start SMO (SMO_train(..., init=false), mpi_svm_main3.cpp:155-290) on S: alphas in S.a
   // are updated in place.  mn_h/mx_h: the global scaling statistics (host, d values).
   virtual SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) = 0;
+  // True when the warm start of S (rows [0, nz) carry every nonzero alpha) provably meets the stop
+  // test b_low <= b_high + 2 tau already -- i.e. the solve would end at its first selection without
+  // an update -- checked from a cross-kernel K(S, S[0:nz]) only, before any Gram work.  The margin
+  // covers the check's own rounding, so a true answer never changes a result.  Default: never.
+  virtual bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) { return false; }
   virtual void trace_push(const char*) {}  // roctx ranges (HIP backend)
   virtual void trace_pop() {}
 };
@@ -273,6 +279,7 @@ struct SolveLog {
   double ms = 0.0, b = 0.0;
   int32_t stop = 0;
   double gram_ms = 0.0;  // of ms: the kernel matrix (device backend)
+  bool skipped = false;  // warm start already met the stop test (Backend::warm_start_converged)
 };
 
 // Wall time of this rank per driver phase (host clock; with SVM355_CASCADE_PROFILE=1 every phase
@@ -288,6 +295,7 @@ enum CascadePhase {
   kPhSendRecv,     // tree: pairwise exchanges
   kPhCheckpoint,   // per-round state file
   kPhFinal,        // final b / SV broadcast and the host copy of the model
+  kPhSetup,        // driver entry to the start of the timed region, without the upload
   kNumPhases
 };
 
@@ -326,6 +334,31 @@ inline void partition_bounds(int64_t n, int P, int r, int64_t* lo, int64_t* hi) 
 // rethrown as CascadeError with the rank that failed.  Returns when every thread has ended.
 void run_rank_threads(int P, const std::shared_ptr<AbortToken>& token, const std::function<void(int)>& fn,
                       const std::function<void(int)>& on_abort);
+
+// Persistent rank threads (one per rank, kept by a device group between fits, so no fit pays
+// thread creation / per-thread runtime set-up and teardown).  run() has run_rank_threads semantics.
+class RankPool {
+ public:
+  explicit RankPool(int P);
+  ~RankPool();
+  RankPool(const RankPool&) = delete;
+  RankPool& operator=(const RankPool&) = delete;
+  int size() const { return P_; }
+  void run(const std::shared_ptr<AbortToken>& token, const std::function<void(int)>& fn,
+           const std::function<void(int)>& on_abort);
+
+ private:
+  void loop(int r);
+  int P_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+  const std::function<void(int)>* job_ = nullptr;
+  std::shared_ptr<AbortToken> token_;
+};
 
 std::unique_ptr<Backend> make_cpu_backend();
 

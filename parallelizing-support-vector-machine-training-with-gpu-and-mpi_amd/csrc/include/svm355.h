@@ -133,6 +133,7 @@ typedef struct svm_cascade_cfg {
   double fail_stall_s;     //   (the others then hit comm_timeout_s)
 } svm_cascade_cfg;
 
+#define SVM_CASCADE_SOLVE_COLS 10
 // Result of a cascade fit (allocated by the library, release with svm_cascade_free).
 typedef struct svm_cascade_out {
   int32_t world, rank, rounds, converged;
@@ -151,15 +152,16 @@ typedef struct svm_cascade_out {
   int64_t n_merged;
   int64_t* merged_history; // star: rank 0's merged set sizes
   int64_t n_solves;
-  double* solves;          // n_solves x 9: rank, round, layer (star 0 local / -1 merge, tree step),
-                           //   rows, SMO iterations, ms, b, stop reason, of ms the kernel matrix
+  double* solves;          // n_solves x SVM_CASCADE_SOLVE_COLS: rank, round, layer (star 0 local /
+                           //   -1 merge, tree step), rows, SMO iterations, ms, b, stop reason, of ms
+                           //   the kernel matrix, skipped (warm start already optimal)
   int64_t n_ranks;
   double* rank_train_ms;   // train_ms of each rank this call drove
   char transport[16];
   char backend[16];
   // Lowest driven rank's wall time per driver phase (cascade.h CascadePhase): upload, scale, bcast,
-  // assemble, solve, select, gather, sendrecv, checkpoint, final.
-  double phase_ms[10];
+  // assemble, solve, select, gather, sendrecv, checkpoint, final, setup.
+  double phase_ms[11];
 } svm_cascade_out;
 
 SVM_API void svm_cascade_default_cfg(svm_cascade_cfg* c);

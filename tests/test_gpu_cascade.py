@@ -55,6 +55,28 @@ def test_hip_cascade_one_rank_finds_the_single_gpu_svs(data):
     assert first["layer"] == "local" and first["iterations"] == s.n_iter_  # same trajectory as the SVC fit
 
 
+@pytest.mark.parametrize("topology,world", [("star", 1), ("star", 3), ("tree", 2)])
+def test_optimal_warm_start_skip_changes_nothing(data, monkeypatch, topology, world):
+    """A solve whose warm start already meets the stop test is skipped (no Gram); the model is the
+    same bit for bit as with every solve run."""
+    tr, _ = data
+    X = tr.compact().X
+    fit = lambda: CascadeSVM(SVMParams(), topology=topology).fit(X, tr.y, world=world, device="cuda",
+                                                                 transport="loopback").result
+    a = fit()
+    monkeypatch.setenv("SVM355_CASCADE_SKIP", "0")
+    b = fit()
+    assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
+    np.testing.assert_array_equal(a.alpha, b.alpha)
+    assert not any(s["skipped"] for s in b.solves)
+    skipped = [s for s in a.solves if s["skipped"]]
+    if topology == "star" and world == 1:  # round 1's local solve restarts from the optimum
+        assert skipped and all(s["layer"] == "local" and s["iterations"] == 1 for s in skipped)
+    # every skipped solve really would have stopped at its first selection
+    ref = {(s["rank"], s["round"], s["layer"]): s["iterations"] for s in b.solves}
+    assert all(ref[(s["rank"], s["round"], s["layer"])] == 1 for s in skipped)
+
+
 @pytest.mark.parametrize("topology", ["star", "tree"])
 def test_rccl_group_equals_loopback(data, topology):
     tr, _ = data
