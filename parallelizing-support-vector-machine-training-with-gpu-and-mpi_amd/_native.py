@@ -14,7 +14,7 @@ import threading
 from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_uint64, c_void_p
 from pathlib import Path
 
-LIB_DIR = Path(__file__).resolve().parent / "lib"
+LIB_DIR = Path(os.environ.get("SVM355_LIB_DIR") or Path(__file__).resolve().parent / "lib")  # override: A/B builds
 
 _lock = threading.Lock()
 _core = None

@@ -76,9 +76,11 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
       const int j = perm[k];
       int qq = 0;
       if (j >= 0) {
+        // x = q / r rounded once, so x * r recovers the integer q to within 2 ulp(q) <= 6e-14;
+        // anything farther off is not an integer pixel (e.g. 3.0000004) and takes the FP64 Gram.
         const double v = xr[j] * rmul[k];
         const double q = rint(v);
-        bad |= !(fabs(v - q) <= 1e-6) || q < 0.0 || q > 255.0;
+        bad |= !(fabs(v - q) <= 64.0 * __DBL_EPSILON__ * fmax(1.0, rmul[k])) || q < 0.0 || q > 255.0;
         qq = int(q - off[k]);
         if (k >= main0)
           nacc += qq * qq;

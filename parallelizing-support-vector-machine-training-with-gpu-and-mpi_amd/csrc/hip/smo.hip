@@ -523,7 +523,17 @@ __device__ __forceinline__ uint32_t persist_solve(
         pay = lane == 7 ? b.i : pay;
         pay = lane == 8 ? lo32(ba) : pay;
         pay = lane == 9 ? hi32(ba) : pay;
-        if constexpr (XLOCAL)  // stays in the XCD's L2, where every participant's sc1 loads look
+        // Memory-model note (XLOCAL).  The readers are other workgroups, but every participant runs
+        // on XCD 0 (xcd_register checks HW_REG_XCC_ID), and HIP has no scope between workgroup and
+        // agent.  On gfx950 the scopes differ only in the store's cache-coherence bits: workgroup
+        // scope emits `global_store_dwordx2 ... sc0` (through the write-through vL1D into the
+        // XCD's L2), agent scope `... sc1` (written through past the XCD-local L2 to the
+        // device-coherent level, because the eight XCD L2s are not coherent with each other).  The
+        // pollers' agent-scope loads (`global_load_dwordx2 ... sc1`) miss the vL1D and are served by
+        // that same L2, the single point of coherence of one XCD, so the sc0 store is visible to
+        // them.  Agent scope costs 16 % at the headline shape (3.42 -> 3.95 us/iter at n = 60k,
+        // profiles/r2_psmo_store_scope_ab.txt); tests/test_isa_pins.py pins both encodings.
+        if constexpr (XLOCAL)
           __hip_atomic_store(rec + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
         else

@@ -42,10 +42,10 @@ class SMOResult:
 
 class DeviceContext:
     """One native device context (private HIP stream + workspace) per GPU per host thread
-    (thread-ranks of ``ThreadTransport`` sharing a GPU must not share a workspace)."""
+    (thread-ranks sharing a GPU must not share a workspace).  Contexts live in thread-local storage:
+    when a worker thread ends, its contexts (and their library-owned Gram) are destroyed with it."""
 
-    _ctxs: dict = {}
-    _lock = threading.Lock()
+    _tls = threading.local()
 
     def __init__(self, index: int):
         self.index = index
@@ -55,16 +55,25 @@ class DeviceContext:
         if not self.handle:
             raise N.NativeError(f"svmd_create({index}) failed: {N.last_error()}")
 
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h:
+            try:
+                self.lib.svmd_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
     @classmethod
     def get(cls, device) -> "DeviceContext":
         index = torch.device(device).index
         if index is None:
             index = torch.cuda.current_device()
-        key = (index, threading.get_ident())
-        with cls._lock:
-            ctx = cls._ctxs.get(key)
-            if ctx is None:
-                ctx = cls._ctxs[key] = DeviceContext(index)
+        ctxs = getattr(cls._tls, "ctxs", None)
+        if ctxs is None:
+            ctxs = cls._tls.ctxs = {}
+        ctx = ctxs.get(index)
+        if ctx is None:
+            ctx = ctxs[index] = DeviceContext(index)
         return ctx
 
     def bind(self) -> int:
@@ -228,29 +237,38 @@ def _host_stats(mn, mx):
     return a, b, int(a.shape[0])
 
 
-_GRAM_BUFS: dict = {}
+_GRAM_TLS = threading.local()  # per host thread: {device index: grow-only Gram buffer}
+
+
+def _gram_bufs() -> dict:
+    bufs = getattr(_GRAM_TLS, "bufs", None)
+    if bufs is None:
+        bufs = _GRAM_TLS.bufs = {}
+    return bufs
 
 
 def gram_buffer(n: int, device) -> torch.Tensor:
-    """(n, ldk) float64 scratch Gram for the library's own transient use (SVC fit, one-vs-rest,
-    cascade solves): one grow-only buffer per (device, host thread), so repeated fits of the same or
-    smaller size never go back to the allocator — a fresh multi-GB device allocation can take
-    hundreds of milliseconds.  The view is overwritten by the next call on the same thread; free the
-    buffers with ``release_gram_buffers()``."""
+    """(n, ldk) float64 scratch Gram for the library's own transient use (SVC fit, one-vs-rest):
+    one grow-only buffer per device per host thread, so repeated fits of the same or smaller size
+    never go back to the allocator — a fresh multi-GB device allocation can take hundreds of
+    milliseconds.  The view is overwritten by the next call on the same thread.  Buffers live in
+    thread-local storage (released when the thread ends) and ``release_gram_buffers()`` drops the
+    calling thread's."""
     device = torch.device(device)
     ldk = (n + 1) // 2 * 2
-    key = (device.index if device.index is not None else torch.cuda.current_device(), threading.get_ident())
-    buf = _GRAM_BUFS.get(key)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    bufs = _gram_bufs()
+    buf = bufs.get(key)
     if buf is None or buf.numel() < n * ldk:
-        _GRAM_BUFS.pop(key, None)
+        bufs.pop(key, None)
         del buf
-        buf = _GRAM_BUFS[key] = torch.empty(n * ldk, dtype=torch.float64, device=device)
+        buf = bufs[key] = torch.empty(n * ldk, dtype=torch.float64, device=device)
     return buf[: n * ldk].view(n, ldk)
 
 
 def release_gram_buffers() -> None:
-    """Drop the cached Gram buffers of every thread (``gram_buffer``)."""
-    _GRAM_BUFS.clear()
+    """Drop the calling thread's cached Gram buffers (``gram_buffer``)."""
+    _gram_bufs().clear()
 
 
 def gram_fits(n: int, device, fraction: float = 0.8) -> bool:
@@ -285,8 +303,7 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
         import time as _t
 
         # the row cache sizes itself from the free HBM: hand this thread's scratch Gram back first
-        key = (X.device.index, threading.get_ident())
-        if _GRAM_BUFS.pop(key, None) is not None:
+        if _gram_bufs().pop(X.device.index, None) is not None:
             torch.cuda.empty_cache()
 
         t0 = _t.perf_counter()

@@ -1,27 +1,13 @@
-"""Transports for the Cascade SVM: the reference's MPI call sites re-expressed as
-collectives over ``torch.distributed`` (RCCL over xGMI on MI355X, gloo on CPUs) or over threads.
+"""Rank transports of the one-vs-rest trainer (models/multiclass.py): the classes are dealt over
+ranks and the per-class alphas / intercepts are all-reduced.  (The Cascade SVM has its own native
+transports, csrc/cascade: RCCL from C++ and a host-staged loopback.)
 
-| reference call site (mpi_svm_main*.cpp)            | Transport method                       |
-|----------------------------------------------------|----------------------------------------|
-| MPI_Bcast n_features / n_total (M3 :459-461)       | ``broadcast_int``                      |
-| MPI_Bcast min/max (M3 :534-535)                    | ``allreduce_`` MIN / MAX of local stats |
-| MPI_Bcast SV count + X/Y/alpha/ID (M3 :587-601)    | ``broadcast_int`` + ``broadcast_``     |
-|                                                    |   of ONE packed (k, w+3) float64 buffer |
-| tree MPI_Send/Recv count+4 arrays (M3 :689-716)    | ``send_rows`` / ``recv_rows``          |
-| star MPI_Send/Recv to rank 0 (M2 :578-607,748-760) | ``gather_rows`` (counts all-gathered,  |
-|                                                    |   max-padded ``dist.gather`` to rank 0) |
-| MPI_Bcast converged flag (M3 :824, M2 :764)        | ``broadcast_int``                      |
-
-Instead of four messages per SV set (X, Y, alpha, ID with tags 20-24), rows, labels, alphas and
-IDs travel as one packed float64 buffer (IDs < 2^53 and +-1 labels are exact in float64), so each
-exchange is a count plus one bulk transfer that stays on the device end to end.
-
-``ThreadTransport`` runs P ranks as threads of one process (the native solvers release the GIL),
-which gives CPU tests and single-GPU rehearsals of any P without a process group.
+``TorchDistTransport`` wraps a ``torch.distributed`` group (backend "nccl" = RCCL over xGMI on
+MI355X, or gloo); ``ThreadTransport`` runs P ranks as threads of one process (the native solvers
+release the GIL) — CPU tests and single-GPU rehearsals of any P without a process group.
 """
 from __future__ import annotations
 
-import queue
 import threading
 from abc import ABC, abstractmethod
 from typing import List, Optional
@@ -35,36 +21,13 @@ class Transport(ABC):
     device: torch.device
 
     @abstractmethod
-    def allreduce_(self, t: torch.Tensor, op: str) -> torch.Tensor: ...
+    def allreduce_(self, t: torch.Tensor, op: str) -> torch.Tensor: ...  # op: "min" | "max" | "sum"
 
     @abstractmethod
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor: ...
 
     @abstractmethod
-    def gather_rows(self, payload: torch.Tensor, dst: int = 0) -> Optional[List[torch.Tensor]]: ...
-
-    @abstractmethod
-    def send_rows(self, payload: torch.Tensor, dst: int) -> None: ...
-
-    @abstractmethod
-    def recv_rows(self, src: int, width: int) -> torch.Tensor: ...
-
-    @abstractmethod
     def barrier(self) -> None: ...
-
-    def broadcast_int(self, v: int, src: int = 0) -> int:
-        t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
-        self.broadcast_(t, src)
-        return int(t.item())
-
-    def broadcast_rows(self, payload: Optional[torch.Tensor], width: int, src: int = 0) -> torch.Tensor:
-        """Count, then one bulk broadcast of a (k, width) float64 buffer from src."""
-        k = self.broadcast_int(payload.shape[0] if self.rank == src else 0, src)
-        if self.rank != src:
-            payload = torch.empty((k, width), dtype=torch.float64, device=self.device)
-        if k:
-            self.broadcast_(payload, src)
-        return payload
 
 
 class TorchDistTransport(Transport):
@@ -89,39 +52,6 @@ class TorchDistTransport(Transport):
         self.dist.broadcast(t, src, group=self.group)
         return t
 
-    def gather_rows(self, payload, dst=0):
-        w = payload.shape[1]
-        cnt = torch.tensor([payload.shape[0]], dtype=torch.int64, device=self.device)
-        counts = torch.empty(self.world, dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(counts, cnt, group=self.group)
-        counts = counts.tolist()
-        kmax = max(counts)
-        if kmax == 0:
-            return [torch.empty((0, w), dtype=torch.float64, device=self.device) for _ in range(self.world)] \
-                if self.rank == dst else None
-        padded = torch.zeros((kmax, w), dtype=torch.float64, device=self.device)
-        padded[: payload.shape[0]] = payload
-        bufs = [torch.empty_like(padded) for _ in range(self.world)] if self.rank == dst else None
-        self.dist.gather(padded, bufs, dst=dst, group=self.group)
-        if self.rank != dst:
-            return None
-        return [b[:c] for b, c in zip(bufs, counts)]
-
-    def send_rows(self, payload, dst):
-        cnt = torch.tensor([payload.shape[0]], dtype=torch.int64, device=self.device)
-        self.dist.send(cnt, dst, group=self.group)
-        if payload.shape[0]:
-            self.dist.send(payload.contiguous(), dst, group=self.group)
-
-    def recv_rows(self, src, width):
-        cnt = torch.empty(1, dtype=torch.int64, device=self.device)
-        self.dist.recv(cnt, src, group=self.group)
-        k = int(cnt.item())
-        out = torch.empty((k, width), dtype=torch.float64, device=self.device)
-        if k:
-            self.dist.recv(out, src, group=self.group)
-        return out
-
     def barrier(self):
         if self.device.type == "cuda":
             self.dist.barrier(group=self.group, device_ids=[self.device.index])
@@ -134,7 +64,6 @@ class _ThreadGroup:
         self.world = world
         self.barrier = threading.Barrier(world)
         self.slots: List[Optional[torch.Tensor]] = [None] * world
-        self.queues = {(s, d): queue.Queue() for s in range(world) for d in range(world)}
 
 
 class ThreadTransport(Transport):
@@ -171,25 +100,14 @@ class ThreadTransport(Transport):
             t.copy_(vals[src])
         return t
 
-    def gather_rows(self, payload, dst=0):
-        vals = self._exchange(payload)
-        return [v.to(self.device) for v in vals] if self.rank == dst else None
-
-    def send_rows(self, payload, dst):
-        self.g.queues[(self.rank, dst)].put(payload.detach().clone())
-
-    def recv_rows(self, src, width):
-        out = self.g.queues[(src, self.rank)].get(timeout=3600)
-        assert out.shape[1] == width
-        return out.to(self.device)
-
     def barrier(self):
         self.g.barrier.wait()
 
 
 def run_threads(world: int, fn, device_for_rank=lambda r: torch.device("cpu")):
     """Run ``fn(transport)`` on ``world`` thread-ranks; returns the per-rank results in rank order.
-    Exceptions on any rank abort the group (broken barrier) and are re-raised."""
+    Exceptions on any rank abort the group (broken barrier) and are re-raised.  Per-thread device
+    state (contexts, scratch Grams; ops/device.py) is thread-local and released with the thread."""
     group = ThreadTransport.create_group(world)
     results: list = [None] * world
     errors: list = [None] * world
@@ -201,7 +119,7 @@ def run_threads(world: int, fn, device_for_rank=lambda r: torch.device("cpu")):
             errors[r] = e
             group.barrier.abort()
 
-    threads = [threading.Thread(target=body, args=(r,), name=f"cascade-rank{r}") for r in range(world)]
+    threads = [threading.Thread(target=body, args=(r,), name=f"rank{r}") for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:

@@ -193,6 +193,37 @@ def test_xcd_local_persistent_smo_matches_graph(dev, D, monkeypatch, n):
     np.testing.assert_array_equal(a1, a2)
 
 
+def test_headline_shape_60k_default_solver_equals_graph_replay(dev, D, monkeypatch):
+    """The bench's exact shape: n = 60000 MNIST-shaped rows, resident exact-integer Gram, the default
+    solver (XCD-local persistent, 512-thread workgroups x 4 elements) against the two-kernel graph
+    replay: identical (i_high, i_low) traces, alphas and b; and SVC.fit (what bench.py times)
+    reports that solve's iterations and b."""
+    n = 60000
+    tr = synthetic_mnist(n, seed=2024).compact()
+    Xd = D.upload_rows(tr.X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    K, path = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    assert path == "int8-exact"
+    yd = torch.from_numpy(tr.y).to(dev)
+    out = {}
+    for mode in ("auto", "graph"):
+        monkeypatch.setenv("SVM355_SMO", mode)
+        a = torch.zeros(n, dtype=torch.float64, device=dev)
+        r, trc = D.smo(K, yd, a, SVMParams(), n=n, trace_cap=20000)
+        out[mode] = (r, trc, a.cpu().numpy())
+    monkeypatch.delenv("SVM355_SMO")
+    (r1, t1, a1), (r2, t2, a2) = out["auto"], out["graph"]
+    assert r1.stop_reason == "converged" and r1.iterations == 12793  # the README / BENCH headline solve
+    assert r1.iterations == r2.iterations and r1.b == r2.b
+    assert len(t1) == r1.iterations - 1
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(a1, a2)
+    del K
+    m = SVC(device="cuda:0").fit(tr.X, tr.y)
+    assert m.n_iter_ == r1.iterations and m.b_ == r1.b
+    assert m.timings_["gram_path"] == "int8-exact" and m.timings_["kcache"] == "full"
+
+
 def test_device_smo_warm_start_bit_identical(dev, D, mn_data):
     tr, _ = mn_data
     X = MinMaxScaler().fit_transform(tr.X[:700])
@@ -341,6 +372,21 @@ def test_int_gram_falls_back_on_real_valued_data(dev, D):
     assert path == "fp64"
     with pytest.raises(Exception):
         D.rbf_gram_sym(Xd, sqn, 0.1, mn=mn, mx=mx, gram="int")
+
+
+def test_near_integer_rows_take_the_fp64_gram(dev, mn_data):
+    """Values a few 1e-7 off an integer are real-valued data: the auto Gram must not round them onto
+    the exact-integer path (igram.hip quantisation tolerance is ~64 ulp of the pixel range)."""
+    tr, _ = mn_data
+    X = tr.X[:600].copy()
+    col = int(np.argmax(X.max(0) - X.min(0)))
+    inner = np.flatnonzero((X[:, col] > X[:, col].min()) & (X[:, col] < X[:, col].max()))
+    assert len(inner) > 3
+    X[inner[::3], col] += 4e-7  # e.g. 3.0000004; min / max (and so the range plan) stay integers
+    a = SVC(device="cuda:0").fit(X, tr.y[:600])
+    assert a.timings_["gram_path"] == "fp64"
+    b = SVC(device="cuda:0").fit(tr.X[:600], tr.y[:600])
+    assert b.timings_["gram_path"] == "int8-exact"
 
 
 def test_svc_int_gram_matches_fp64_gram(dev, mn_data):
