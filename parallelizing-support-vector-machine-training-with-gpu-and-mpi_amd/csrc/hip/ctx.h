@@ -125,6 +125,13 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
                      svm_result* r, size_t cache_bytes, int64_t* trace, int64_t trace_cap, int32_t* used_int);
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap);
+// Persistent row-cache SMO (smo.hip): f / alpha initialised by the caller; kRcNotApplicable when no
+// persistent shape covers n (SVM355_RC_SMO=graph forces that answer).
+struct QRows;
+constexpr int kRcNotApplicable = -100;
+int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double* cache, int64_t ldc, int64_t nslots,
+                          const int32_t* y, double* alpha, double* f, int64_t n, const svm_params& p, svm_result* r,
+                          int64_t* trace, int64_t trace_cap);
 // nclass cold-start solves on one Gram (Y, A: nclass x n, class-major): XCD teams (smo.hip).
 // exp self-test (igram.hip): device libm exp and the Gram epilogue's batched exp of x[0..n).
 int exp_selftest(hipStream_t s, const double* x, int64_t n, double* out_lib, double* out_batch);

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "qrows.h"
 
 namespace svm355 {
 namespace {
@@ -50,61 +51,14 @@ struct KcPartial {
   int64_t imax;
 };
 
-// Quantised-row kernel description (igram.hip layout).
-struct QRows {
-  const int8_t* Q;
-  const int32_t* N0;
-  const double* WN;
-  const double* step_w;
-  int kq, main_step0;
-  double w0;
-  // FP64 mode (INT = false)
-  const double* X;
-  const double* sqn;
-  int64_t ld, d;
-};
-
-template <bool INT>
-__device__ __forceinline__ double kval(const QRows& q, int64_t a, int64_t b, double neg_gamma) {
-  if (a == b) return 1.0;
-  if constexpr (INT) {
-    const int4* pa = reinterpret_cast<const int4*>(q.Q + a * int64_t(q.kq));
-    const int4* pb = reinterpret_cast<const int4*>(q.Q + b * int64_t(q.kq));
-    const int nsteps = q.kq / 32;
-    int32_t acc = 0;
-    double x = 0.0;
-    for (int s = 0; s < nsteps; ++s) {
-      const int4 a0 = pa[2 * s], a1 = pa[2 * s + 1], b0 = pb[2 * s], b1 = pb[2 * s + 1];
-      acc = __builtin_amdgcn_sdot4(a0.x, b0.x, acc, false);
-      acc = __builtin_amdgcn_sdot4(a0.y, b0.y, acc, false);
-      acc = __builtin_amdgcn_sdot4(a0.z, b0.z, acc, false);
-      acc = __builtin_amdgcn_sdot4(a0.w, b0.w, acc, false);
-      acc = __builtin_amdgcn_sdot4(a1.x, b1.x, acc, false);
-      acc = __builtin_amdgcn_sdot4(a1.y, b1.y, acc, false);
-      acc = __builtin_amdgcn_sdot4(a1.z, b1.z, acc, false);
-      acc = __builtin_amdgcn_sdot4(a1.w, b1.w, acc, false);
-      if (s < q.main_step0) {
-        const double wg = q.step_w[s];
-        if (wg != 0.0) {  // igram_tri_kernel's group flush, same order and expression
-          x += wg * double(acc);
-          acc = 0;
-        }
-      }
-    }
-    const int32_t D0 = q.N0[a] + q.N0[b] - 2 * acc;
-    double dist = q.w0 * double(D0);
-    if (q.main_step0 > 0) dist += (q.WN[a] + q.WN[b]) - 2.0 * x;
-    dist = dist > 0.0 ? dist : 0.0;
-    return exp(neg_gamma * dist);
-  } else {
-    const double* xa = q.X + a * q.ld;
-    const double* xb = q.X + b * q.ld;
-    double dot = 0.0;
-    for (int64_t k = 0; k < q.d; ++k) dot += xa[k] * xb[k];
-    double dist = q.sqn[a] + q.sqn[b] - 2.0 * dot;
-    dist = dist > 0.0 ? dist : 0.0;
-    return exp(neg_gamma * dist);
-  }
+// Chunk-interleaved copy of the quantised rows (QRows::Qt): thread (c, i) moves 16-byte chunk c of
+// row i; consecutive threads write consecutive rows of one chunk.
+__global__ void interleave_rows_kernel(const int8_t* __restrict__ Q, int64_t n, int kq, int8_t* __restrict__ Qt) {
+  const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t nc = kq / 16;
+  if (idx >= n * nc) return;
+  const int64_t c = idx / n, i = idx - c * n;
+  reinterpret_cast<int4*>(Qt)[c * n + i] = reinterpret_cast<const int4*>(Q + i * int64_t(kq))[c];
 }
 
 __global__ void kc_init_cold_kernel(const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f,
@@ -506,6 +460,25 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
     release();
     set_error("row cache: init launch failed");
     return SVM_ERR_DEVICE;
+  }
+  // Default: the persistent solver (one launch, register-resident state, directory in LDS), whose
+  // misses walk each element's quantised row: give it the coalesced interleaved copy.
+  if (int_ok) {
+    auto* Qt = static_cast<int8_t*>(dalloc(size_t(n) * size_t(q.kq)));
+    if (Qt) {
+      const int64_t work = n * (q.kq / 16);
+      hipLaunchKernelGGL(interleave_rows_kernel, dim3(unsigned((work + 255) / 256)), dim3(256), 0, s, q.Q, n, q.kq,
+                         Qt);
+      if (hipGetLastError() == hipSuccess) {
+        q.Qt = Qt;
+        q.n_rows = n;
+      }
+    }
+  }
+  rc = run_smo_rc_persistent(ctx, q, int_ok, cache, ldc, C, y, alpha, f, n, p, r, trace, tcap);
+  if (rc != kRcNotApplicable) {
+    release();
+    return rc;
   }
   const int64_t nsets = C / 2;
   hipGraph_t graph = nullptr;

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "qrows.h"
 
 namespace svm355 {
 namespace {
@@ -381,6 +382,295 @@ struct PersistShared {
   double gv[2], ga[2];          // global winners of the current epoch
   uint32_t gi[2];
   int timeout;
+  int64_t rslot[2];             // cached row source: slots of rows (i_high, i_low) ...
+  int32_t rmiss[2];             // ... and whether this epoch fills them
+};
+
+// ---- Row sources of the persistent solver.  choose() runs on one lane of every workgroup once the
+// pair is known (before the barrier that publishes it); fetch() then gives every thread the rows'
+// values for its elements plus K11 / K22 / K12, issuing all loads in one memory round trip.
+struct ResidentRows {  // the resident n x n Gram
+  const double* __restrict__ K;
+  int64_t ldk;
+  __device__ __forceinline__ void choose(PersistShared&, uint32_t, uint32_t) const {}
+  template <int NT, int E>
+  __device__ __forceinline__ void fetch(const PersistShared&, int64_t ih, int64_t il, int64_t lo, int t,
+                                        int64_t hi_end, double (&kh)[E], double (&kl)[E], double& K11,
+                                        double& K22, double& K12) const {
+    K11 = K[ih * ldk + ih];
+    K22 = K[il * ldk + il];
+    K12 = K[ih * ldk + il];
+    const double* Kh = K + ih * ldk;
+    const double* Kl = K + il * ldk;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = lo + t + NT * e;
+      const bool ok = i < hi_end;
+      kh[e] = ok ? Kh[i] : 0.0;
+      kl[e] = ok ? Kl[i] : 0.0;
+    }
+  }
+};
+
+// Kernel rows held in an HBM row cache of nslots x ldc doubles, computed from the rows themselves
+// on a miss (qrows.h).  The 2-way set-associative directory (int32 tags + MRU way per set) lives
+// in LDS and is REPLICATED in every workgroup: all workgroups see the same pair sequence and run the
+// same deterministic lookups, so they agree on every slot and miss without exchanging anything.  On
+// a miss each workgroup computes its own slice of the row (kval2: both rows of the pair in one pass
+// over each element's quantised row) and writes it into the slot; hits read the slot, exactly like
+// the resident Gram.  Values are bit-identical to the exact-integer Gram, hence the trajectory.
+template <bool INT>
+struct CachedRows {
+  QRows q;
+  double* __restrict__ cache;
+  int64_t ldc;
+  int32_t* tags;    // LDS, nslots entries (-1 = empty)
+  uint8_t* mru;     // LDS, nslots / 2 entries
+  int64_t nsets;
+  double neg_gamma;
+
+  __device__ __forceinline__ int64_t lookup(int64_t row, int64_t keep, int32_t* miss) const {
+    const int64_t set = row % nsets, s0 = 2 * set;
+    if (tags[s0] == int32_t(row)) {
+      mru[set] = 0;
+      *miss = 0;
+      return s0;
+    }
+    if (tags[s0 + 1] == int32_t(row)) {
+      mru[set] = 1;
+      *miss = 0;
+      return s0 + 1;
+    }
+    int way = 1 - int(mru[set]);
+    if (s0 + way == keep) way = 1 - way;
+    tags[s0 + way] = int32_t(row);
+    mru[set] = uint8_t(way);
+    *miss = 1;
+    return s0 + way;
+  }
+  __device__ __forceinline__ void choose(PersistShared& sh, uint32_t ih, uint32_t il) const {
+    int32_t mh = 0, ml = 0;
+    const int64_t sh_ = lookup(ih, -1, &mh);
+    const int64_t sl_ = lookup(il, sh_, &ml);
+    sh.rslot[0] = sh_;
+    sh.rslot[1] = sl_;
+    sh.rmiss[0] = mh;
+    sh.rmiss[1] = ml;
+  }
+  // K(ih, il) of the exact-integer path, computed redundantly by every wave: lane s takes k-step s
+  // (and s + 64), then the steps are combined in order with the igram group flushes -> kval bits.
+  __device__ __forceinline__ double k12(int64_t ih, int64_t il) const {
+    if constexpr (INT) {
+      const int lane = threadIdx.x & 63, nsteps = q.kq / 32;
+      int32_t d[2] = {0, 0};
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int s = lane + 64 * r;
+        if (s < nsteps) {
+          const int4* pa = reinterpret_cast<const int4*>(q.Q + ih * int64_t(q.kq)) + 2 * s;
+          const int4* pb = reinterpret_cast<const int4*>(q.Q + il * int64_t(q.kq)) + 2 * s;
+          const int4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+          int32_t acc = 0;
+          acc = __builtin_amdgcn_sdot4(a0.x, b0.x, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.y, b0.y, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.z, b0.z, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.w, b0.w, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.x, b1.x, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.y, b1.y, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.z, b1.z, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.w, b1.w, acc, false);
+          d[r] = acc;
+        }
+      }
+      int32_t acc = 0;
+      double x = 0.0;
+      for (int s = 0; s < nsteps; ++s) {
+        acc += __builtin_amdgcn_readlane(d[s >> 6], s & 63);
+        if (s < q.main_step0) {
+          const double wg = q.step_w[s];
+          if (wg != 0.0) {
+            x += wg * double(acc);
+            acc = 0;
+          }
+        }
+      }
+      const int32_t D0 = q.N0[ih] + q.N0[il] - 2 * acc;
+      double dist = q.w0 * double(D0);
+      if (q.main_step0 > 0) dist += (q.WN[ih] + q.WN[il]) - 2.0 * x;
+      dist = dist > 0.0 ? dist : 0.0;
+      return exp(neg_gamma * dist);
+    } else {
+      return kval<false>(q, ih, il, neg_gamma);
+    }
+  }
+  template <int NT, int E>
+  __device__ __forceinline__ void fetch(const PersistShared& sh, int64_t ih, int64_t il, int64_t lo, int t,
+                                        int64_t hi_end, double (&kh)[E], double (&kl)[E], double& K11,
+                                        double& K22, double& K12) const {
+    const int32_t mh = sh.rmiss[0], ml = sh.rmiss[1];
+    double* Ch = cache + sh.rslot[0] * ldc;
+    double* Cl = cache + sh.rslot[1] * ldc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = lo + t + NT * e;
+      const bool ok = i < hi_end;
+      kh[e] = (ok && !mh) ? Ch[i] : 0.0;
+      kl[e] = (ok && !ml) ? Cl[i] : 0.0;
+    }
+    K11 = 1.0;  // kval(a, a): the Gram's diagonal is exactly 1
+    K22 = 1.0;
+    K12 = k12(ih, il);
+    if constexpr (INT) {
+      // elements in groups per pass (bounded register footprint next to the E-element state)
+      constexpr int EG = E < 4 ? E : (E == 8 ? 2 : 4);
+#pragma unroll
+      for (int e0 = 0; e0 < E; e0 += EG) {
+        if (mh && ml)
+          fill<NT, E, EG, true, true>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
+        else if (mh)
+          fill<NT, E, EG, true, false>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
+        else if (ml)
+          fill<NT, E, EG, false, true>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
+      }
+    } else if (mh | ml) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t i = lo + t + NT * e;
+        if (i < hi_end) {
+          double a, b;
+          kval2<INT>(q, ih, il, i, neg_gamma, &a, &b);
+          if (mh) {
+            kh[e] = a;
+            Ch[i] = a;
+          }
+          if (ml) {
+            kl[e] = b;
+            Cl[i] = b;
+          }
+        }
+      }
+    }
+  }
+  // Miss fill of the exact-integer rows for this thread's E elements: the k-step loop is outermost,
+  // so every step issues the loads of all E elements' chunks at once (E-fold memory parallelism
+  // against the one-element-at-a-time walk of kval2) -- per element the arithmetic and its order
+  // are kval's, so the values are bit-identical.  DA / DB: rows ih / il missed.
+  template <int NT, int E, int EG, bool DA, bool DB>
+  __device__ __forceinline__ void fill(int e0, int64_t ih, int64_t il, int64_t lo, int t, int64_t hi_end,
+                                       double (&khf)[E], double (&klf)[E], double* Ch, double* Cl) const {
+    double* kh = khf + e0;  // this pass: elements e0 .. e0 + EG - 1
+    double* kl = klf + e0;
+    lo += int64_t(NT) * e0;
+    const int4* pa = reinterpret_cast<const int4*>(q.Q + ih * int64_t(q.kq));
+    const int4* pb = reinterpret_cast<const int4*>(q.Q + il * int64_t(q.kq));
+    const int4* pq = q.Qt ? reinterpret_cast<const int4*>(q.Qt) : nullptr;
+    const int64_t cs = q.Qt ? q.n_rows : 1;  // chunk stride (interleaved) or 1 (row-major rows)
+    int32_t acca[EG], accb[EG];
+    double xa[EG], xb[EG];
+    const int4* pi[EG];
+#pragma unroll
+    for (int e = 0; e < EG; ++e) {
+      const int64_t i = lo + t + NT * e;
+      const int64_t ic = i < hi_end ? i : lo;  // clamped (valid) row for the tail's dummy loads
+      pi[e] = pq ? pq + ic : reinterpret_cast<const int4*>(q.Q + ic * int64_t(q.kq));
+      acca[e] = accb[e] = 0;
+      xa[e] = xb[e] = 0.0;
+    }
+    const int nsteps = q.kq / 32;
+    // double-buffered: step s + 1's chunks are in flight while step s is reduced
+    int4 c0[EG], c1[EG], n0[EG], n1[EG];
+#pragma unroll
+    for (int e = 0; e < EG; ++e) {
+      c0[e] = pi[e][0];
+      c1[e] = pi[e][cs];
+    }
+#pragma unroll 2
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) {
+#pragma unroll
+        for (int e = 0; e < EG; ++e) {
+          n0[e] = pi[e][(2 * s + 2) * cs];
+          n1[e] = pi[e][(2 * s + 3) * cs];
+        }
+      }
+      int4 a0, a1, b0, b1;
+      if (DA) {
+        a0 = pa[2 * s];
+        a1 = pa[2 * s + 1];
+      }
+      if (DB) {
+        b0 = pb[2 * s];
+        b1 = pb[2 * s + 1];
+      }
+#pragma unroll
+      for (int e = 0; e < EG; ++e) {
+        if (DA) {
+          int32_t acc = acca[e];
+          acc = __builtin_amdgcn_sdot4(a0.x, c0[e].x, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.y, c0[e].y, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.z, c0[e].z, acc, false);
+          acc = __builtin_amdgcn_sdot4(a0.w, c0[e].w, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.x, c1[e].x, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.y, c1[e].y, acc, false);
+          acc = __builtin_amdgcn_sdot4(a1.z, c1[e].z, acc, false);
+          acca[e] = __builtin_amdgcn_sdot4(a1.w, c1[e].w, acc, false);
+        }
+        if (DB) {
+          int32_t acc = accb[e];
+          acc = __builtin_amdgcn_sdot4(b0.x, c0[e].x, acc, false);
+          acc = __builtin_amdgcn_sdot4(b0.y, c0[e].y, acc, false);
+          acc = __builtin_amdgcn_sdot4(b0.z, c0[e].z, acc, false);
+          acc = __builtin_amdgcn_sdot4(b0.w, c0[e].w, acc, false);
+          acc = __builtin_amdgcn_sdot4(b1.x, c1[e].x, acc, false);
+          acc = __builtin_amdgcn_sdot4(b1.y, c1[e].y, acc, false);
+          acc = __builtin_amdgcn_sdot4(b1.z, c1[e].z, acc, false);
+          accb[e] = __builtin_amdgcn_sdot4(b1.w, c1[e].w, acc, false);
+        }
+      }
+      if (s < q.main_step0) {
+        const double wg = q.step_w[s];
+        if (wg != 0.0) {  // igram_tri_kernel's group flush, same order and expression
+#pragma unroll
+          for (int e = 0; e < EG; ++e) {
+            if (DA) {
+              xa[e] += wg * double(acca[e]);
+              acca[e] = 0;
+            }
+            if (DB) {
+              xb[e] += wg * double(accb[e]);
+              accb[e] = 0;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EG; ++e) {
+        c0[e] = n0[e];
+        c1[e] = n1[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EG; ++e) {
+      const int64_t i = lo + t + NT * e;
+      if (i >= hi_end) continue;
+      if (DA) {
+        double dist = q.w0 * double(q.N0[ih] + q.N0[i] - 2 * acca[e]);
+        if (q.main_step0 > 0) dist += (q.WN[ih] + q.WN[i]) - 2.0 * xa[e];
+        dist = dist > 0.0 ? dist : 0.0;
+        const double v = ih == i ? 1.0 : exp(neg_gamma * dist);
+        kh[e] = v;
+        Ch[i] = v;
+      }
+      if (DB) {
+        double dist = q.w0 * double(q.N0[il] + q.N0[i] - 2 * accb[e]);
+        if (q.main_step0 > 0) dist += (q.WN[il] + q.WN[i]) - 2.0 * xb[e];
+        dist = dist > 0.0 ? dist : 0.0;
+        const double v = il == i ? 1.0 : exp(neg_gamma * dist);
+        kl[e] = v;
+        Cl[i] = v;
+      }
+    }
+  }
 };
 
 // Diagnostic build (STAMP = true, SVM355_PSMO_STAMP=1): workgroup 0 / lane 0 accumulates
@@ -411,9 +701,9 @@ constexpr unsigned long long kRegisterTicks = 200000;
 // workgroup (NW = NT/64 waves), E register-resident elements per thread: element e of thread t is
 // training point lo + t + NT*e of the workgroup's slice.  Epochs continue from epoch0 (record tags
 // must never repeat on a slot array); returns the last epoch used.
-template <int NT, int E, bool STAMP, bool XLOCAL>
+template <int NT, int E, bool STAMP, bool XLOCAL, class Rows>
 __device__ __forceinline__ uint32_t persist_solve(
-    PersistShared& sh, int G, int g, uint32_t epoch0, const double* __restrict__ K, int64_t ldk,
+    PersistShared& sh, int G, int g, uint32_t epoch0, const Rows& rows,
     const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice,
     unsigned long long* __restrict__ slots, SmoState* __restrict__ st, double C, double eps, double tau,
     int64_t max_iter, int64_t* __restrict__ trace, int64_t trace_cap, unsigned* __restrict__ err,
@@ -585,6 +875,9 @@ __device__ __forceinline__ uint32_t persist_solve(
         sh.gv[1] = wgx.v;
         sh.gi[1] = wgx.i;
         sh.ga[1] = awgx;
+        // a pair that will be updated: the row source prepares its rows (every workgroup alike)
+        if (!any_to && wgm.i != kSentinel && wgx.i != kSentinel && !(wgx.v <= wgm.v + 2.0 * tau))
+          rows.choose(sh, wgm.i, wgx.i);
         if (any_to) {
           sh.timeout = 1;
           __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -613,17 +906,9 @@ __device__ __forceinline__ uint32_t persist_solve(
     }
     // One memory round trip: scalars + this slice of rows i_high and i_low.
     const int32_t yh = y[ih], yl = y[il];
-    const double K11 = K[ih * ldk + ih], K22 = K[il * ldk + il], K12 = K[ih * ldk + il];
+    double K11, K22, K12;
     double kh[E], kl[E];
-    const double* Kh = K + ih * ldk;
-    const double* Kl = K + il * ldk;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int64_t i = lo + t + NT * e;
-      const bool ok = i < hi_end;
-      kh[e] = ok ? Kh[i] : 0.0;
-      kl[e] = ok ? Kl[i] : 0.0;
-    }
+    rows.template fetch<NT, E>(sh, ih, il, lo, t, hi_end, kh, kl, K11, K22, K12);
     PSTAMP(5);
     const double ah = sh.ga[0], al = sh.ga[1];
     const int s = yh * yl;
@@ -749,8 +1034,30 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
     G = glocal;
     g = s_rank;
   }
-  persist_solve<NT, E, STAMP, XLOCAL>(sh, G, g, 0, K, ldk, y, alpha, f, n, slice, slots, st, C, eps, tau, max_iter,
+  persist_solve<NT, E, STAMP, XLOCAL>(sh, G, g, 0, ResidentRows{K, ldk}, y, alpha, f, n, slice, slots, st, C, eps,
+                                      tau, max_iter,
                                       trace, trace_cap, err, spin_limit, stamps);
+}
+
+// Persistent SMO on the HBM row cache (n beyond the resident Gram; driven by rowcache.hip's
+// run_smo_rowcache): device-wide exchange over G co-resident workgroups, CachedRows as the row
+// source with its directory (nslots int32 tags + nslots / 2 MRU bytes) in dynamic LDS.
+template <int NT, int E, bool INT>
+__global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
+    QRows q, double* __restrict__ cache, int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* __restrict__ y,
+    double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
+    SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
+    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit) {
+  __shared__ PersistShared sh;
+  extern __shared__ __attribute__((aligned(16))) char rc_dir[];
+  int32_t* tags = reinterpret_cast<int32_t*>(rc_dir);
+  uint8_t* mru = reinterpret_cast<uint8_t*>(tags + nslots);
+  for (int64_t k = threadIdx.x; k < nslots; k += NT) tags[k] = -1;
+  for (int64_t k = threadIdx.x; k < nslots / 2; k += NT) mru[k] = 0;
+  __syncthreads();
+  const CachedRows<INT> rows{q, cache, ldc, tags, mru, nslots / 2, neg_gamma};
+  persist_solve<NT, E, false, false>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f, n, slice, slots, st, C,
+                                     eps, tau, max_iter, trace, trace_cap, err, spin_limit, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -811,7 +1118,8 @@ __global__ __launch_bounds__(NT) void smo_multi_kernel(
     __syncthreads();
     const int cls = s_cls;
     if (cls >= nclass) break;
-    epoch = persist_solve<NT, E, false, true>(sh, glocal, g, epoch, K, ldk, Y + int64_t(cls) * n, A + int64_t(cls) * n,
+    epoch = persist_solve<NT, E, false, true>(sh, glocal, g, epoch, ResidentRows{K, ldk}, Y + int64_t(cls) * n,
+                                              A + int64_t(cls) * n,
                                               F + int64_t(cls) * n, n, slice, tslots, st + cls, C, eps, tau, max_iter,
                                               nullptr, 0, err, spin_limit, nullptr);
     if (sh.timeout) break;
@@ -1146,6 +1454,81 @@ int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t
 }
 
 }  // namespace
+
+namespace {
+template <int E, bool INT>
+void launch_rc_e(hipStream_t s, int G, size_t lds, const QRows& q, double* cache, int64_t ldc, int64_t nslots,
+                 double neg_gamma, const int32_t* y, double* alpha, double* f, int64_t n, unsigned long long* slots,
+                 SmoState* st, const svm_params& p, int64_t* trace, int64_t tcap, unsigned* err) {
+  allow_lds(smo_rc_persistent_kernel<512, E, INT>, lds);
+  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT>), dim3(G), dim3(512), lds, s, q, cache, ldc, nslots,
+                     neg_gamma, y, alpha, f, n, int64_t(512) * E, slots, st, p.C, p.eps, p.tau, p.max_iter, trace, tcap,
+                     err, int64_t(1) << 24);
+}
+}  // namespace
+
+// Persistent row-cache solve (see smo_rc_persistent_kernel).  f / alpha hold the initial state (cold
+// or warm, set up by the caller); cache: nslots x ldc doubles.  Returns kRcNotApplicable when no
+// persistent shape covers n (the caller then replays its select/step graph).
+int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double* cache, int64_t ldc, int64_t nslots,
+                          const int32_t* y, double* alpha, double* f, int64_t n, const svm_params& p, svm_result* r,
+                          int64_t* trace, int64_t trace_cap) {
+  if (const char* m = getenv("SVM355_RC_SMO"); m && !strcmp(m, "graph")) return kRcNotApplicable;
+  if (n <= 0 || n >= int64_t(kSentinel)) return kRcNotApplicable;
+  // Up to 8 register-resident points per thread (n <= 64 x 512 x 8 = 262,144): the E = 16 shape
+  // needs more than 256 VGPRs and spills, so larger n keep the replayed select / step graph.
+  int E = 0;
+  for (int e = 1; e <= 8 && !E; e *= 2)
+    if ((n + 512 * e - 1) / (512 * e) <= kMaxG) E = e;
+  if (!E) return kRcNotApplicable;
+  const int G = int((n + 512 * E - 1) / (512 * E));
+  // Directory in LDS: up to 16384 slots (64 KB of tags + 8 KB of MRU bits) next to PersistShared.
+  const int64_t nd = std::min<int64_t>(nslots, 16384) / 2 * 2;
+  if (nd < 4) return kRcNotApplicable;
+  const size_t lds = (size_t(nd) * 4 + size_t(nd) / 2 + 15) / 16 * 16;
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t s = ctx->stream;
+  const int64_t tcap = trace ? std::max<int64_t>(trace_cap, 0) : 0;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t off_slots = 0, slot_bytes = size_t(2) * kMaxG * kRecStride * 8 + 256;
+  const size_t off_st = off_slots + al(slot_bytes);
+  const size_t off_trace = off_st + al(sizeof(SmoState));
+  int rc = ctx->ensure_ws(off_trace + al(size_t(tcap) * 16));
+  if (rc) return rc;
+  rc = ctx->ensure_pinned(sizeof(SmoState) * 3);
+  if (rc) return rc;
+  char* ws = static_cast<char*>(ctx->ws);
+  auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
+  auto* err = reinterpret_cast<unsigned*>(ws + off_slots + size_t(2) * kMaxG * kRecStride * 8);
+  auto* st = reinterpret_cast<SmoState*>(ws + off_st);
+  int64_t* dtrace = tcap ? reinterpret_cast<int64_t*>(ws + off_trace) : nullptr;
+  SmoState* hst = static_cast<SmoState*>(ctx->pinned);
+  hst[0] = SmoState{0, 0, 0.0, 0.0, 0.0, 0.0, 1, 0, SVM_STOP_RUNNING};
+  SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));
+  SVMD_CHECK(hipMemcpyAsync(st, &hst[0], sizeof(SmoState), hipMemcpyHostToDevice, s));
+  const double ng = -p.gamma;
+#define SVM_RC_CASE(e)                                                                                              \
+  case e:                                                                                                           \
+    if (int_rows)                                                                                                   \
+      launch_rc_e<e, true>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err);     \
+    else                                                                                                            \
+      launch_rc_e<e, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err);    \
+    break;
+  switch (E) {
+    SVM_RC_CASE(1) SVM_RC_CASE(2) SVM_RC_CASE(4) SVM_RC_CASE(8)
+  }
+#undef SVM_RC_CASE
+  SVMD_LAUNCH_CHECK();
+  unsigned herr = 0;
+  SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipMemcpyAsync(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  if (herr) {
+    set_error("row-cache SMO: persistent solver timed out waiting for a workgroup record (G=%d)", G);
+    return SVM_ERR_DEVICE;
+  }
+  return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
+}
 
 int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
             int32_t warm, const svm_params& p, svm_result* r, int64_t* trace, int64_t trace_cap) {

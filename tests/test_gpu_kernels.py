@@ -446,6 +446,29 @@ def test_row_cache_smo_bit_identical_to_full_gram(dev, D, cache_rows):
     np.testing.assert_array_equal(a_rows.cpu().numpy(), a_full.cpu().numpy())
 
 
+@pytest.mark.parametrize("n,cache_rows", [(2500, 64), (40000, 512)])
+def test_persistent_row_cache_equals_graph_row_cache(dev, D, monkeypatch, n, cache_rows):
+    """The persistent row-cache solver (replicated LDS directory, slices filled on a miss) against
+    the replayed select / step graph: the same trace, alphas and b; at n = 40k the device-wide team
+    has 40 workgroups and a 512-row cache that evicts."""
+    tr = synthetic_mnist(n, seed=23)
+    Xd = D.upload_rows(tr.compact().X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    yd = torch.from_numpy(tr.y).to(dev)
+    ldc = (n + 1) // 2 * 2
+    out = {}
+    for mode in ("persistent", "graph"):
+        monkeypatch.setenv("SVM355_RC_SMO", mode)
+        a = torch.zeros(n, dtype=torch.float64, device=dev)
+        r, info = D.train(Xd, sqn, yd, a, SVMParams(), mn=mn, mx=mx, kcache="rows", cache_bytes=cache_rows * ldc * 8,
+                          trace_cap=200000)
+        out[mode] = (r, info["trace"], a.cpu().numpy())
+    (r1, t1, a1), (r2, t2, a2) = out["persistent"], out["graph"]
+    assert r1.stop_reason == "converged" and r1.iterations == r2.iterations and r1.b == r2.b
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(a1, a2)
+
+
 def test_row_cache_warm_start_bit_identical(dev, D):
     n = 1800
     tr = synthetic_mnist(n, seed=22)
