@@ -354,6 +354,23 @@ __device__ __forceinline__ double read_lane64(double x, int src) {
   return mk64(uint32_t(__builtin_amdgcn_readlane(int(lo32(x)), src)),
               uint32_t(__builtin_amdgcn_readlane(int(hi32(x)), src)));
 }
+// Inclusive prefix sum over the 64 lanes (lane L gets x[0] + ... + x[L]); full wave.  DPP only:
+// Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8; lanes shifted in from outside the row
+// read 0), then row_bcast:15 adds row 0's total to row 1 and row 2's to row 3, and row_bcast:31
+// adds lane 31's (rows 0-1 total) to rows 2 and 3.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int32_t dpp_add_src(int32_t x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
+  x += dpp_add_src<0x111>(x);  // row_shr:1
+  x += dpp_add_src<0x112>(x);  // row_shr:2
+  x += dpp_add_src<0x114>(x);  // row_shr:4
+  x += dpp_add_src<0x118>(x);  // row_shr:8
+  x += dpp_add_src<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_add_src<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
 // Requires a full wave (EXEC = all 64 lanes).  L = number of leading lanes that may hold candidates;
 // lanes >= L must hold "no candidate" sentinels (value +inf for MIN / -inf for MAX, index
 // kSentinel), which never beat a real candidate.
@@ -430,13 +447,14 @@ struct CachedRows {
   double neg_gamma;
 
   __device__ __forceinline__ int64_t lookup(int64_t row, int64_t keep, int32_t* miss) const {
-    const int64_t set = row % nsets, s0 = 2 * set;
-    if (tags[s0] == int32_t(row)) {
+    const int64_t set = uint32_t(row) % uint32_t(nsets), s0 = 2 * set;  // row < 2^31, nsets <= 8192
+    const int2 tw = reinterpret_cast<const int2*>(tags)[set];           // both ways in one LDS read
+    if (tw.x == int32_t(row)) {
       mru[set] = 0;
       *miss = 0;
       return s0;
     }
-    if (tags[s0 + 1] == int32_t(row)) {
+    if (tw.y == int32_t(row)) {
       mru[set] = 1;
       *miss = 0;
       return s0 + 1;
@@ -459,47 +477,78 @@ struct CachedRows {
   }
   // K(ih, il) of the exact-integer path, computed redundantly by every wave: lane s takes k-step s
   // (and s + 64), then the steps are combined in order with the igram group flushes -> kval bits.
-  __device__ __forceinline__ double k12(int64_t ih, int64_t il) const {
+  // mid() runs after K12's own loads are issued and before their data is used: loads it issues
+  // (the hit path's row reads) stay in flight through K12's arithmetic, since the in-order vmcnt
+  // wait for K12's operands does not cover loads issued after them.
+  template <class Mid>
+  __device__ __forceinline__ double k12(int64_t ih, int64_t il, Mid mid) const {
     if constexpr (INT) {
       const int lane = threadIdx.x & 63, nsteps = q.kq / 32;
       int32_t d[2] = {0, 0};
+      double wl[2] = {0.0, 0.0};  // step s's flush weight in lane s & 63 (no loads in the serial loop)
+      int4 a0[2], a1[2], b0[2], b1[2];
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         const int s = lane + 64 * r;
+        if (s < q.main_step0) wl[r] = q.step_w[s];
+        a0[r] = a1[r] = b0[r] = b1[r] = int4{0, 0, 0, 0};
         if (s < nsteps) {
           const int4* pa = reinterpret_cast<const int4*>(q.Q + ih * int64_t(q.kq)) + 2 * s;
           const int4* pb = reinterpret_cast<const int4*>(q.Q + il * int64_t(q.kq)) + 2 * s;
-          const int4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-          int32_t acc = 0;
-          acc = __builtin_amdgcn_sdot4(a0.x, b0.x, acc, false);
-          acc = __builtin_amdgcn_sdot4(a0.y, b0.y, acc, false);
-          acc = __builtin_amdgcn_sdot4(a0.z, b0.z, acc, false);
-          acc = __builtin_amdgcn_sdot4(a0.w, b0.w, acc, false);
-          acc = __builtin_amdgcn_sdot4(a1.x, b1.x, acc, false);
-          acc = __builtin_amdgcn_sdot4(a1.y, b1.y, acc, false);
-          acc = __builtin_amdgcn_sdot4(a1.z, b1.z, acc, false);
-          acc = __builtin_amdgcn_sdot4(a1.w, b1.w, acc, false);
-          d[r] = acc;
+          a0[r] = pa[0];
+          a1[r] = pa[1];
+          b0[r] = pb[0];
+          b1[r] = pb[1];
         }
       }
-      int32_t acc = 0;
+      const int32_t n0h = q.N0[ih], n0l = q.N0[il];
+      const double wnh = q.main_step0 > 0 ? q.WN[ih] : 0.0, wnl = q.main_step0 > 0 ? q.WN[il] : 0.0;
+      mid();
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {  // zero operands past nsteps give d = 0
+        int32_t acc = 0;
+        acc = __builtin_amdgcn_sdot4(a0[r].x, b0[r].x, acc, false);
+        acc = __builtin_amdgcn_sdot4(a0[r].y, b0[r].y, acc, false);
+        acc = __builtin_amdgcn_sdot4(a0[r].z, b0[r].z, acc, false);
+        acc = __builtin_amdgcn_sdot4(a0[r].w, b0[r].w, acc, false);
+        acc = __builtin_amdgcn_sdot4(a1[r].x, b1[r].x, acc, false);
+        acc = __builtin_amdgcn_sdot4(a1[r].y, b1[r].y, acc, false);
+        acc = __builtin_amdgcn_sdot4(a1[r].z, b1[r].z, acc, false);
+        acc = __builtin_amdgcn_sdot4(a1[r].w, b1[r].w, acc, false);
+        d[r] = acc;
+      }
+      // kval's serial walk is "acc += d[s]; at a flush step: x += w * acc, acc = 0".  The integer
+      // group sums are exact, so they come from an inclusive prefix scan over the steps (group sum
+      // = P[flush] - P[previous flush]); only the FP64 accumulation stays serial, over the flush
+      // steps alone and in step order -- the same operands in the same order as kval.
+      const int32_t P0 = wave_incl_scan(d[0]);
+      const int32_t P1 = nsteps > 64 ? wave_incl_scan(d[1]) + __builtin_amdgcn_readlane(P0, 63) : 0;
+      uint64_t m0 = __ballot(lane < q.main_step0 && wl[0] != 0.0);
+      uint64_t m1 = __ballot(lane + 64 < q.main_step0 && wl[1] != 0.0);
+      int32_t prev = 0;
       double x = 0.0;
-      for (int s = 0; s < nsteps; ++s) {
-        acc += __builtin_amdgcn_readlane(d[s >> 6], s & 63);
-        if (s < q.main_step0) {
-          const double wg = q.step_w[s];
-          if (wg != 0.0) {
-            x += wg * double(acc);
-            acc = 0;
-          }
-        }
+      while (m0) {
+        const int s = __builtin_ctzll(m0);
+        m0 &= m0 - 1;
+        const int32_t ps = __builtin_amdgcn_readlane(P0, s);
+        x += read_lane64(wl[0], s) * double(ps - prev);
+        prev = ps;
       }
-      const int32_t D0 = q.N0[ih] + q.N0[il] - 2 * acc;
+      while (m1) {
+        const int s = __builtin_ctzll(m1);
+        m1 &= m1 - 1;
+        const int32_t ps = __builtin_amdgcn_readlane(P1, s);
+        x += read_lane64(wl[1], s) * double(ps - prev);
+        prev = ps;
+      }
+      const int32_t acc = __builtin_amdgcn_readlane(nsteps > 64 ? P1 : P0, 63) - prev;
+      const int32_t D0 = n0h + n0l - 2 * acc;
       double dist = q.w0 * double(D0);
-      if (q.main_step0 > 0) dist += (q.WN[ih] + q.WN[il]) - 2.0 * x;
+      if (q.main_step0 > 0) dist += (wnh + wnl) - 2.0 * x;
       dist = dist > 0.0 ? dist : 0.0;
       return exp(neg_gamma * dist);
     } else {
+      mid();
       return kval<false>(q, ih, il, neg_gamma);
     }
   }
@@ -510,6 +559,46 @@ struct CachedRows {
     const int32_t mh = sh.rmiss[0], ml = sh.rmiss[1];
     double* Ch = cache + sh.rslot[0] * ldc;
     double* Cl = cache + sh.rslot[1] * ldc;
+    K11 = 1.0;  // kval(a, a): the Gram's diagonal is exactly 1
+    K22 = 1.0;
+    if constexpr (INT) {
+      if (!(mh | ml)) {  // hit: the row reads overlap K12's arithmetic
+        K12 = k12(ih, il, [&] {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int64_t i = lo + t + NT * e;
+            const bool ok = i < hi_end;
+            kh[e] = ok ? Ch[i] : 0.0;
+            kl[e] = ok ? Cl[i] : 0.0;
+          }
+        });
+        return;
+      }
+      K12 = k12(ih, il, [] {});
+      // A miss first writes this thread's elements of the missed row(s) into the slot, in groups of
+      // EG elements with the group loop kept rolled, so the fill's registers do not stack on the
+      // E-element solver state; then every element is read back from the slot like a hit (a
+      // thread reading its own stores).
+      constexpr int EG = E < 4 ? E : 4;
+#pragma unroll 1
+      for (int e0 = 0; e0 < E; e0 += EG) {
+        if (mh && ml)
+          fill<NT, EG, true, true>(lo + int64_t(NT) * e0, ih, il, t, hi_end, Ch, Cl);
+        else if (mh)
+          fill<NT, EG, true, false>(lo + int64_t(NT) * e0, ih, il, t, hi_end, Ch, Cl);
+        else
+          fill<NT, EG, false, true>(lo + int64_t(NT) * e0, ih, il, t, hi_end, Ch, Cl);
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t i = lo + t + NT * e;
+        const bool ok = i < hi_end;
+        kh[e] = ok ? Ch[i] : 0.0;
+        kl[e] = ok ? Cl[i] : 0.0;
+      }
+      return;
+    }
+    K12 = k12(ih, il, [] {});
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int64_t i = lo + t + NT * e;
@@ -517,22 +606,7 @@ struct CachedRows {
       kh[e] = (ok && !mh) ? Ch[i] : 0.0;
       kl[e] = (ok && !ml) ? Cl[i] : 0.0;
     }
-    K11 = 1.0;  // kval(a, a): the Gram's diagonal is exactly 1
-    K22 = 1.0;
-    K12 = k12(ih, il);
-    if constexpr (INT) {
-      // elements in groups per pass (bounded register footprint next to the E-element state)
-      constexpr int EG = E < 4 ? E : (E == 8 ? 2 : 4);
-#pragma unroll
-      for (int e0 = 0; e0 < E; e0 += EG) {
-        if (mh && ml)
-          fill<NT, E, EG, true, true>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
-        else if (mh)
-          fill<NT, E, EG, true, false>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
-        else if (ml)
-          fill<NT, E, EG, false, true>(e0, ih, il, lo, t, hi_end, kh, kl, Ch, Cl);
-      }
-    } else if (mh | ml) {
+    if (mh | ml) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int64_t i = lo + t + NT * e;
@@ -554,13 +628,11 @@ struct CachedRows {
   // Miss fill of the exact-integer rows for this thread's E elements: the k-step loop is outermost,
   // so every step issues the loads of all E elements' chunks at once (E-fold memory parallelism
   // against the one-element-at-a-time walk of kval2) -- per element the arithmetic and its order
-  // are kval's, so the values are bit-identical.  DA / DB: rows ih / il missed.
-  template <int NT, int E, int EG, bool DA, bool DB>
-  __device__ __forceinline__ void fill(int e0, int64_t ih, int64_t il, int64_t lo, int t, int64_t hi_end,
-                                       double (&khf)[E], double (&klf)[E], double* Ch, double* Cl) const {
-    double* kh = khf + e0;  // this pass: elements e0 .. e0 + EG - 1
-    double* kl = klf + e0;
-    lo += int64_t(NT) * e0;
+  // are kval's, so the values are bit-identical.  DA / DB: rows ih / il missed.  Elements
+  // lo + t + NT * e, e < EG.
+  template <int NT, int EG, bool DA, bool DB>
+  __device__ __forceinline__ void fill(int64_t lo, int64_t ih, int64_t il, int t, int64_t hi_end, double* Ch,
+                                       double* Cl) const {
     const int4* pa = reinterpret_cast<const int4*>(q.Q + ih * int64_t(q.kq));
     const int4* pb = reinterpret_cast<const int4*>(q.Q + il * int64_t(q.kq));
     const int4* pq = q.Qt ? reinterpret_cast<const int4*>(q.Qt) : nullptr;
@@ -577,21 +649,12 @@ struct CachedRows {
       xa[e] = xb[e] = 0.0;
     }
     const int nsteps = q.kq / 32;
-    // double-buffered: step s + 1's chunks are in flight while step s is reduced
-    int4 c0[EG], c1[EG], n0[EG], n1[EG];
-#pragma unroll
-    for (int e = 0; e < EG; ++e) {
-      c0[e] = pi[e][0];
-      c1[e] = pi[e][cs];
-    }
-#pragma unroll 2
+    int4 c0[EG], c1[EG];
     for (int s = 0; s < nsteps; ++s) {
-      if (s + 1 < nsteps) {
 #pragma unroll
-        for (int e = 0; e < EG; ++e) {
-          n0[e] = pi[e][(2 * s + 2) * cs];
-          n1[e] = pi[e][(2 * s + 3) * cs];
-        }
+      for (int e = 0; e < EG; ++e) {
+        c0[e] = pi[e][(2 * s) * cs];
+        c1[e] = pi[e][(2 * s + 1) * cs];
       }
       int4 a0, a1, b0, b1;
       if (DA) {
@@ -643,11 +706,6 @@ struct CachedRows {
           }
         }
       }
-#pragma unroll
-      for (int e = 0; e < EG; ++e) {
-        c0[e] = n0[e];
-        c1[e] = n1[e];
-      }
     }
 #pragma unroll
     for (int e = 0; e < EG; ++e) {
@@ -657,17 +715,13 @@ struct CachedRows {
         double dist = q.w0 * double(q.N0[ih] + q.N0[i] - 2 * acca[e]);
         if (q.main_step0 > 0) dist += (q.WN[ih] + q.WN[i]) - 2.0 * xa[e];
         dist = dist > 0.0 ? dist : 0.0;
-        const double v = ih == i ? 1.0 : exp(neg_gamma * dist);
-        kh[e] = v;
-        Ch[i] = v;
+        Ch[i] = ih == i ? 1.0 : exp(neg_gamma * dist);
       }
       if (DB) {
         double dist = q.w0 * double(q.N0[il] + q.N0[i] - 2 * accb[e]);
         if (q.main_step0 > 0) dist += (q.WN[il] + q.WN[i]) - 2.0 * xb[e];
         dist = dist > 0.0 ? dist : 0.0;
-        const double v = il == i ? 1.0 : exp(neg_gamma * dist);
-        kl[e] = v;
-        Cl[i] = v;
+        Cl[i] = il == i ? 1.0 : exp(neg_gamma * dist);
       }
     }
   }
@@ -734,7 +788,9 @@ __device__ __forceinline__ uint32_t persist_solve(
   uint32_t epoch = epoch0 + 1;
   for (;; ++epoch) {
     if (STAMP) {
-      const bool on = g == 0 && threadIdx.x == 0 && epoch >= kStampFrom && epoch < kStampFrom + kStampCount;
+      // window start: stamps[8] when the host set it (SVM355_PSMO_STAMP_FROM), else kStampFrom
+      const uint32_t from = stamps[8] ? uint32_t(stamps[8]) : kStampFrom;
+      const bool on = g == 0 && threadIdx.x == 0 && epoch >= from && epoch < from + kStampCount;
       if (on && !stamping) rt0 = __builtin_amdgcn_s_memrealtime();
       if (!on && stamping) sacc[7] = __builtin_amdgcn_s_memrealtime() - rt0;
       stamping = on;
@@ -1042,12 +1098,12 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
 // Persistent SMO on the HBM row cache (n beyond the resident Gram; driven by rowcache.hip's
 // run_smo_rowcache): device-wide exchange over G co-resident workgroups, CachedRows as the row
 // source with its directory (nslots int32 tags + nslots / 2 MRU bytes) in dynamic LDS.
-template <int NT, int E, bool INT>
+template <int NT, int E, bool INT, bool STAMP>
 __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
     QRows q, double* __restrict__ cache, int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* __restrict__ y,
     double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
     SmoState* __restrict__ st, double C, double eps, double tau, int64_t max_iter, int64_t* __restrict__ trace,
-    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit) {
+    int64_t trace_cap, unsigned* __restrict__ err, int64_t spin_limit, unsigned long long* __restrict__ stamps) {
   __shared__ PersistShared sh;
   extern __shared__ __attribute__((aligned(16))) char rc_dir[];
   int32_t* tags = reinterpret_cast<int32_t*>(rc_dir);
@@ -1056,8 +1112,8 @@ __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
   for (int64_t k = threadIdx.x; k < nslots / 2; k += NT) mru[k] = 0;
   __syncthreads();
   const CachedRows<INT> rows{q, cache, ldc, tags, mru, nslots / 2, neg_gamma};
-  persist_solve<NT, E, false, false>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f, n, slice, slots, st, C,
-                                     eps, tau, max_iter, trace, trace_cap, err, spin_limit, nullptr);
+  persist_solve<NT, E, STAMP, false>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f, n, slice, slots, st,
+                                     C, eps, tau, max_iter, trace, trace_cap, err, spin_limit, stamps);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1456,14 +1512,14 @@ int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t
 }  // namespace
 
 namespace {
-template <int E, bool INT>
+template <int E, bool INT, bool STAMP>
 void launch_rc_e(hipStream_t s, int G, size_t lds, const QRows& q, double* cache, int64_t ldc, int64_t nslots,
                  double neg_gamma, const int32_t* y, double* alpha, double* f, int64_t n, unsigned long long* slots,
                  SmoState* st, const svm_params& p, int64_t* trace, int64_t tcap, unsigned* err) {
-  allow_lds(smo_rc_persistent_kernel<512, E, INT>, lds);
-  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT>), dim3(G), dim3(512), lds, s, q, cache, ldc, nslots,
+  allow_lds(smo_rc_persistent_kernel<512, E, INT, STAMP>, lds);
+  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT, STAMP>), dim3(G), dim3(512), lds, s, q, cache, ldc, nslots,
                      neg_gamma, y, alpha, f, n, int64_t(512) * E, slots, st, p.C, p.eps, p.tau, p.max_iter, trace, tcap,
-                     err, int64_t(1) << 24);
+                     err, int64_t(1) << 24, reinterpret_cast<unsigned long long*>(err) + 8);
 }
 }  // namespace
 
@@ -1475,6 +1531,7 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
                           int64_t* trace, int64_t trace_cap) {
   if (const char* m = getenv("SVM355_RC_SMO"); m && !strcmp(m, "graph")) return kRcNotApplicable;
   if (n <= 0 || n >= int64_t(kSentinel)) return kRcNotApplicable;
+  if (int_rows && q.kq > 32 * 128) return kRcNotApplicable;  // CachedRows::k12: two k-steps per lane
   // Up to 8 register-resident points per thread (n <= 64 x 512 x 8 = 262,144): the E = 16 shape
   // needs more than 256 VGPRs and spills, so larger n keep the replayed select / step graph.
   int E = 0;
@@ -1507,12 +1564,24 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));
   SVMD_CHECK(hipMemcpyAsync(st, &hst[0], sizeof(SmoState), hipMemcpyHostToDevice, s));
   const double ng = -p.gamma;
-#define SVM_RC_CASE(e)                                                                                              \
+  const char* stv = getenv("SVM355_PSMO_STAMP");
+  const bool stamp = stv && atoi(stv);
+  if (stamp) {
+    const char* fv = getenv("SVM355_PSMO_STAMP_FROM");
+    const unsigned long long from = fv ? std::max(1ll, atoll(fv)) : 0ull;
+    SVMD_CHECK(hipMemcpyAsync(reinterpret_cast<unsigned long long*>(err) + 16, &from, 8, hipMemcpyHostToDevice, s));
+    SVMD_CHECK(hipStreamSynchronize(s));
+  }
+#define SVM_RC_CASE(e)                                                                                             \
   case e:                                                                                                           \
-    if (int_rows)                                                                                                   \
-      launch_rc_e<e, true>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err);     \
+    if (int_rows && stamp)                                                                                          \
+      launch_rc_e<e, true, true>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err); \
+    else if (int_rows)                                                                                              \
+      launch_rc_e<e, true, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap,    \
+                                  err);                                                                             \
     else                                                                                                            \
-      launch_rc_e<e, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err);    \
+      launch_rc_e<e, false, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap,   \
+                                   err);                                                                            \
     break;
   switch (E) {
     SVM_RC_CASE(1) SVM_RC_CASE(2) SVM_RC_CASE(4) SVM_RC_CASE(8)
@@ -1526,6 +1595,15 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   if (herr) {
     set_error("row-cache SMO: persistent solver timed out waiting for a workgroup record (G=%d)", G);
     return SVM_ERR_DEVICE;
+  }
+  if (stamp && int_rows) {
+    unsigned long long hs[8];
+    SVMD_CHECK(hipMemcpy(hs, reinterpret_cast<unsigned long long*>(err) + 8, sizeof(hs), hipMemcpyDeviceToHost));
+    const double cnt = double(kStampCount);
+    fprintf(stderr, "[rc stamps G=%d E=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
+            "globalred+choose+barrier2 %.0f | rows (hit read / miss fill) %.0f | update %.0f | us/iter %.3f\n", G, E,
+            hs[0] / cnt, hs[1] / cnt, hs[2] / cnt, hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, hs[6] / cnt,
+            double(hs[7]) / 100.0 / cnt);
   }
   return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
 }
