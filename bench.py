@@ -46,7 +46,10 @@ METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV pa
 
 def critical_path(solves, topology):
     """Per round: the slowest rank's local solve (tree: slowest rank of every layer) + rank 0's merge.
+    Solve times are the solo device times when the run measured them (SVM355_CASCADE_SERIAL_SOLVES=1:
+    ranks sharing one GPU take turns, so each solve is timed as on a GPU of its own), else wall times.
     Returns ([[round, local_max_ms, merge_ms, local_max_iterations, merge_iterations]], total ms)."""
+    solves = [dict(s, ms=s["solo_ms"]) if s.get("solo_ms", -1.0) >= 0 else s for s in solves]
     rounds = sorted({s["round"] for s in solves})
     out, tot = [], 0.0
     for r in rounds:
@@ -213,6 +216,9 @@ def main(argv=None):
                  "round_ms": [round(x, 3) for x in r.round_ms], "transport": r.transport,
                  "driver_train_ms": round(r.train_ms, 3), "rank0_phase_ms": r.phase_ms,
                  "per_round_critical_path": crit, "critical_path_solve_ms": crit_ms,
+                 "critical_path_basis": "solo device time per solve (serial-solve rehearsal)"
+                 if any(s.get("solo_ms", -1.0) >= 0 for s in solves) else "wall time per solve",
+                 "row_cache_solves": int(sum(s.get("row_cache", False) for s in solves)),
                  "rank0_smo_iterations": int(sum(s["iterations"] for s in r0)),
                  "skipped_solves": int(sum(s["skipped"] for s in solves)),
                  "max_rank_smo_iterations": max(sum(s["iterations"] for s in solves if s["rank"] == q)

@@ -116,7 +116,7 @@ class SvmCascadeOut(ctypes.Structure):
     ]
 
 
-SOLVE_COLS = 10  # svm355.h SVM_CASCADE_SOLVE_COLS
+SOLVE_COLS = 12  # svm355.h SVM_CASCADE_SOLVE_COLS
 CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
                   "final", "setup")
 

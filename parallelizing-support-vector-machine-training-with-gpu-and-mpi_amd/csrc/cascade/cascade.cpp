@@ -311,7 +311,7 @@ class Rank {
     DSet out = assemble({Segment{&S, nullptr, 0, nullptr, &keep, false}});
     log.push_back(
         SolveLog{t_.rank(), rnd, layer, S.k, st.iterations, ms_between(t0, Clock::now()), st.b, st.stop, st.gram_ms,
-                              skipped_now});
+                              skipped_now, st.row_cache, B_.take_solo_ms()});
     return {std::move(out), st.b};
   }
 

@@ -130,6 +130,7 @@ struct SolveStats {
   double b = 0.0;
   int32_t stop = 0;
   double gram_ms = 0.0;
+  bool row_cache = false;  // solved on the HBM row cache (the k x k Gram did not fit)
 };
 
 class Backend {
@@ -162,6 +163,10 @@ class Backend {
   // an update -- checked from a cross-kernel K(S, S[0:nz]) only, before any Gram work.  The margin
   // covers the check's own rounding, so a true answer never changes a result.  Default: never.
   virtual bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) { return false; }
+  // Device time of the solve work since the last call, measured with the device to this rank alone
+  // (HIP backend with SVM355_CASCADE_SERIAL_SOLVES=1: a one-GPU rehearsal of P ranks runs their
+  // solves one at a time, so each is timed as it would run on its own GPU); < 0 when not measured.
+  virtual double take_solo_ms() { return -1.0; }
   virtual void trace_push(const char*) {}  // roctx ranges (HIP backend)
   virtual void trace_pop() {}
 };
@@ -280,6 +285,8 @@ struct SolveLog {
   int32_t stop = 0;
   double gram_ms = 0.0;  // of ms: the kernel matrix (device backend)
   bool skipped = false;  // warm start already met the stop test (Backend::warm_start_converged)
+  bool row_cache = false;  // SolveStats::row_cache
+  double solo_ms = -1.0;   // Backend::take_solo_ms (skip check + solve), < 0 = not measured
 };
 
 // Wall time of this rank per driver phase (host clock; with SVM355_CASCADE_PROFILE=1 every phase

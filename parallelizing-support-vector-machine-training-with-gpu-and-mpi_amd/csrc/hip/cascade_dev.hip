@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <utility>
 
 #include "cascade.h"
 #include "cascade_capi.h"
@@ -260,6 +261,42 @@ class HipBackend final : public Backend {
     d2h(ids, ids_d_, k * 8);
   }
   SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
+    return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
+  }
+  bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) override {
+    return solo([&] { return kkt_check(S, nz, d, p); });
+  }
+  double take_solo_ms() override {
+    if (!solo_any_) return -1.0;
+    const double v = solo_acc_;
+    solo_acc_ = 0.0;
+    solo_any_ = false;
+    return v;
+  }
+  void trace_push(const char* name) override { svmd_trace_push(name); }
+  void trace_pop() override { svmd_trace_pop(); }
+
+ private:
+  // SVM355_CASCADE_SERIAL_SOLVES=1: solves (and skip checks) of all ranks of this process take one
+  // lock, and each is timed from an idle stream to its completion -- the device time the solve
+  // would take on a GPU of its own (one-GPU rehearsals of P ranks; bench.py's critical path).
+  static std::mutex& solo_mutex() {
+    static std::mutex m;
+    return m;
+  }
+  template <class F>
+  decltype(std::declval<F&>()()) solo(F&& f) {
+    if (!serial_) return f();
+    std::lock_guard<std::mutex> lk(solo_mutex());
+    sync();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto r = f();
+    sync();
+    solo_acc_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    solo_any_ = true;
+    return r;
+  }
+  SolveStats solve_impl(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
     const int64_t ldd = ld(d);
     grow(&sqn_, &sqn_cap_, size_t(S.k) * 8);
     auto* sqn = static_cast<double*>(sqn_);
@@ -267,15 +304,29 @@ class HipBackend final : public Backend {
     svm_result r{};
     svmd_timing tm{};
     int32_t used = 0;
-    check(svmd_train_q(ctx_, S.X.as<double>(), sqn, S.k, ldd, ldd, S.y.as<int32_t>(), S.a.as<double>(), 1, &p, &r,
-                       nullptr, 0, &tm, mn_h, mx_h, d, 0, &used),
-          "svmd_train_q");
-    return SolveStats{r.iterations, r.b, r.stop_reason, tm.gram_ms};
+    // A partition whose k x k Gram does not fit (large-n cascades; ranks sharing one GPU in a
+    // loopback rehearsal) is solved on the HBM row cache instead: the same exact-integer kernel
+    // values, computed on demand (rowcache.hip / smo.hip's persistent row-cache solver).
+    // SVM355_CASCADE_GRAM=rows forces that path (tests).
+    const char* gm = getenv("SVM355_CASCADE_GRAM");
+    int rc = SVM_ERR_OOM;
+    if (!(gm && !strcmp(gm, "rows")))
+      rc = svmd_train_q(ctx_, S.X.as<double>(), sqn, S.k, ldd, ldd, S.y.as<int32_t>(), S.a.as<double>(), 1, &p, &r,
+                        nullptr, 0, &tm, mn_h, mx_h, d, 0, &used);
+    const bool on_rows = rc == SVM_ERR_OOM;
+    if (on_rows) {
+      release_cache();  // unused blocks of this backend's set allocator, then the context's Gram
+      check(svmd_release_cache(ctx_), "svmd_release_cache");
+      rc = svmd_train_rows(ctx_, S.X.as<double>(), sqn, S.k, ldd, d, S.y.as<int32_t>(), S.a.as<double>(), 1, &p, &r,
+                           mn_h, mx_h, 0, 0, &used, nullptr, 0);
+    }
+    check(rc, "svmd_train");
+    return SolveStats{r.iterations, r.b, r.stop_reason, tm.gram_ms, on_rows};
   }
   // f from the cross-kernel K(S, S[0:nz]) (MFMA f64 decision path) instead of the int8-exact Gram
   // the solve would build: the two kernel values agree to a few ulps, so f agrees to ~1e-9 here
   // (nz <= a few thousand, alpha <= C); a 1e-7 margin on the stop test covers it.
-  bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) override {
+  bool kkt_check(DSet& S, int64_t nz, int64_t d, const svm_params& p) {
     const char* e = getenv("SVM355_CASCADE_SKIP");  // =0 disables the check (A/B runs, tests)
     if ((e && atoi(e) == 0) || nz <= 0 || nz > S.k) return false;
     const int64_t ldd = ld(d), k = S.k;
@@ -301,10 +352,6 @@ class HipBackend final : public Backend {
     constexpr double kMargin = 1e-7;
     return h[1] <= h[0] + 2.0 * p.tau - kMargin;
   }
-  void trace_push(const char* name) override { svmd_trace_push(name); }
-  void trace_pop() override { svmd_trace_pop(); }
-
- private:
   static void check(int rc, const char* what) {
     if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
   }
@@ -342,6 +389,12 @@ class HipBackend final : public Backend {
   std::map<void*, size_t> live_;
   void *idx_ = nullptr, *ids_d_ = nullptr, *sqn_ = nullptr, *kkt_ = nullptr;
   size_t idx_cap_ = 0, ids_cap_ = 0, sqn_cap_ = 0, kkt_cap_ = 0;
+  const bool serial_ = [] {
+    const char* v = getenv("SVM355_CASCADE_SERIAL_SOLVES");
+    return v && atoi(v) != 0;
+  }();
+  double solo_acc_ = 0.0;
+  bool solo_any_ = false;
 };
 
 // ------------------------------------------------------------------------------ RcclTransport

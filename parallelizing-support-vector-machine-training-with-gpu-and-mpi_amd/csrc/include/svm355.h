@@ -133,7 +133,7 @@ typedef struct svm_cascade_cfg {
   double fail_stall_s;     //   (the others then hit comm_timeout_s)
 } svm_cascade_cfg;
 
-#define SVM_CASCADE_SOLVE_COLS 10
+#define SVM_CASCADE_SOLVE_COLS 12
 // Result of a cascade fit (allocated by the library, release with svm_cascade_free).
 typedef struct svm_cascade_out {
   int32_t world, rank, rounds, converged;
@@ -154,7 +154,9 @@ typedef struct svm_cascade_out {
   int64_t n_solves;
   double* solves;          // n_solves x SVM_CASCADE_SOLVE_COLS: rank, round, layer (star 0 local /
                            //   -1 merge, tree step), rows, SMO iterations, ms, b, stop reason, of ms
-                           //   the kernel matrix, skipped (warm start already optimal)
+                           //   the kernel matrix, skipped (warm start already optimal), row cache
+                           //   (solved on kernel rows computed on demand: the Gram did not fit),
+                           //   solo ms (device time alone, serial-solve rehearsals; < 0 otherwise)
   int64_t n_ranks;
   double* rank_train_ms;   // train_ms of each rank this call drove
   char transport[16];

@@ -57,7 +57,8 @@ class CascadeResult:
             solves = [{"rank": int(s[0]), "round": int(s[1]),
                        "layer": LAYER_NAMES.get(int(s[2]), f"layer{int(s[2])}"), "n": int(s[3]),
                        "iterations": int(s[4]), "ms": float(s[5]), "b": float(s[6]),
-                       "stop": N.STOP_NAMES.get(int(s[7]), str(int(s[7]))), "gram_ms": float(s[8]), "skipped": bool(s[9])} for s in sol]
+                       "stop": N.STOP_NAMES.get(int(s[7]), str(int(s[7]))), "gram_ms": float(s[8]), "skipped": bool(s[9]),
+                       "row_cache": bool(s[10]), "solo_ms": float(s[11])} for s in sol]
             phases = dict(zip(N.CASCADE_PHASES, [round(float(v), 3) for v in o.phase_ms]))
             return cls(arr(o.ids, o.n_sv, np.int64), arr(o.y, o.n_sv, np.int32), arr(o.alpha, o.n_sv, np.float64),
                        arr(o.sv_rows, o.n_sv * o.d, np.float64).reshape(o.n_sv, o.d), arr(o.mn, o.d, np.float64),

@@ -77,6 +77,25 @@ def test_optimal_warm_start_skip_changes_nothing(data, monkeypatch, topology, wo
     assert all(ref[(s["rank"], s["round"], s["layer"])] == 1 for s in skipped)
 
 
+@pytest.mark.parametrize("topology,world", [("star", 2), ("tree", 2)])
+def test_row_cache_solves_equal_gram_solves(data, monkeypatch, topology, world):
+    """A partition whose Gram does not fit is solved on the HBM row cache (cascade_dev.hip
+    HipBackend::solve); SVM355_CASCADE_GRAM=rows forces that path.  The row-cache solver follows
+    the resident-Gram trajectory bit for bit (warm starts included), so the cascade is unchanged."""
+    tr, _ = data
+    X = tr.compact().X
+    fit = lambda: CascadeSVM(SVMParams(), topology=topology).fit(X, tr.y, world=world, device="cuda",
+                                                                 transport="loopback").result
+    a = fit()
+    monkeypatch.setenv("SVM355_CASCADE_GRAM", "rows")
+    b = fit()
+    assert not any(s["row_cache"] for s in a.solves)
+    assert all(s["row_cache"] for s in b.solves if not s["skipped"])
+    assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
+    np.testing.assert_array_equal(a.alpha, b.alpha)
+    assert [s["iterations"] for s in a.solves] == [s["iterations"] for s in b.solves]
+
+
 @pytest.mark.parametrize("topology", ["star", "tree"])
 def test_rccl_group_equals_loopback(data, topology):
     tr, _ = data
