@@ -36,6 +36,10 @@ import time
 
 import numpy as np
 
+# RCCL between processes (torchrun ranks) needs dmabuf IPC; the legacy IPC mode fails with
+# "hipIpcGetMemHandle: invalid argument" on these hosts.  Must be set before the HSA runtime starts.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 REF_GPU_S = 58.570  # GPU SMO training time, 60k
 REF_SERIAL_S = 3285.662  # serial SMO training time, 60k
 REF_GPU_PRED_S = 38.297  # GPU prediction time, 60k train / 10k test

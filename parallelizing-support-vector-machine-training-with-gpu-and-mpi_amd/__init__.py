@@ -6,13 +6,21 @@ re-designed for gfx950:
 
 * ``svm355.models.SVC``              RBF SVM, first-order SMO (reference semantics), CPU oracle or GPU
 * ``svm355.models.OneVsRestSVC``     all digits one-vs-rest over ONE resident Gram (10 SMO solves)
-* ``svm355.parallel.CascadeSVM``     classical tree and modified two-layer star Cascade SVM over
-                                     ``torch.distributed`` (RCCL on GPUs, gloo on CPUs) or threads
+* ``svm355.parallel.CascadeSVM``     classical tree and modified two-layer star Cascade SVM: one native
+                                     driver over RCCL (a thread per GPU, or one rank per process under
+                                     torchrun) or the loopback transport (CPU oracle / one-GPU rehearsal)
 * ``svm355.utils.data``              CSV I/O, one-vs-rest labels, min-max scaling, synthetic MNIST
-* ``svm355.ops``                     device kernels (MFMA f64 RBF Gram, fused WSS, SMO step, predict)
+* ``svm355.ops``                     device kernels (exact-integer int8-MFMA and f64-MFMA RBF Grams,
+                                     persistent SMO solvers, HBM row cache, predict)
 * CLIs: ``python -m svm355 {serial,gpu,sweep,cascade}`` and native ``bin/svm_serial``, ``bin/svm_gpu``
 """
-from .utils.config import SVMParams
+import os as _os
+
+# RCCL between processes needs dmabuf IPC (the legacy mode fails on these hosts); effective only if
+# set before the first HIP call of the process.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+from .utils.config import SVMParams  # noqa: E402
 from .utils.data import Dataset, MinMaxScaler, load_csv, one_vs_rest, synthetic_mnist, write_csv
 from .models.multiclass import OneVsRestSVC
 from .models.svc import SVC
