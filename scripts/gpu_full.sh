@@ -1,15 +1,18 @@
 #!/bin/bash
-# Round validation on one MI355X: GPU tests, smoke, 1-GPU bench, RCCL cascade path on one rank,
-# 2-rank gloo rehearsal of the multi-GPU bench, CLI sweep.  Every GPU step has its own time limit
-# and the script stops at the first failure.
+# Full GPU check of the tree: every GPU test, smoke(), bench N=1, and a rocprofv3 kernel-stats profile
+# of bench (steps 2, warmup 1).  Outputs under gpurun_out/full_*.
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-run() { local name=$1 lim=$2; shift 2; echo "=== $name"; timeout -k 10 $lim "$@" > gpurun_out/$name.txt 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.txt | tail -${TAILN:-6}; echo "=== $name rc=$rc"; return $rc; }
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q || exit 1
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
-run bench1 600 python bench.py --steps 5 --warmup 1 || exit 1
-run bench_nccl1_cascade 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 1 --steps 2 --warmup 1 --cascade || exit 1
-run bench_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29522 bench.py --gpus 2 --steps 2 --warmup 1 --backend gloo || exit 1
-run sweep 600 python -m svm355 sweep --synthetic 60000,10000 --warmup 1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  > gpurun_out/full_pytest_gpu.txt 2>&1; rc=$?
+tail -3 gpurun_out/full_pytest_gpu.txt
+[ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" gpurun_out/full_pytest_gpu.txt | head -80; exit $rc; }
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/full_smoke.txt 2>&1 || { tail -20 gpurun_out/full_smoke.txt; exit 1; }
+tail -1 gpurun_out/full_smoke.txt
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --out gpurun_out/full_bench.json > gpurun_out/full_bench.log 2>&1 || { tail -20 gpurun_out/full_bench.log; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/full_bench.json')); print('bench', d['value'], d['ms_per_step'], d['iterations'], d['b'], d['n_sv'], d['step_upload_alloc_gram_smo_fit_ms'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/full_prof -o run -- python3 bench.py --steps 2 --warmup 1 \
+  > gpurun_out/full_prof.log 2>&1 || { tail -20 gpurun_out/full_prof.log; exit 1; }
+f=$(find gpurun_out/full_prof -name "*kernel_stats.csv" | head -1); echo "stats: $f"; head -12 "$f" | cut -c1-200
