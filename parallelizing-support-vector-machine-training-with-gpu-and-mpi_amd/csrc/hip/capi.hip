@@ -122,6 +122,7 @@ SVM_API void svmd_destroy(void* h) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->gram) (void)hipFree(ctx->gram);
+  if (ctx->rc_cache) (void)hipFree(ctx->rc_cache);
   if (ctx->count_d) (void)hipFree(ctx->count_d);
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
   if (ctx->ev_out) (void)hipEventDestroy(ctx->ev_out);
@@ -138,14 +139,27 @@ SVM_API int svmd_selftest_exp(void* h, const double* x_d, int64_t n, double* lib
   return ctx->end();
 }
 
-SVM_API int svmd_release_cache(void* h) {
-  SVMD_CTX(h);
+static int release_gram(DeviceCtx* ctx) {
   if (ctx->gram) {
     SVMD_CHECK(hipSetDevice(ctx->device));
     SVMD_CHECK(hipStreamSynchronize(ctx->stream));
     SVMD_CHECK(hipFree(ctx->gram));
     ctx->gram = nullptr;
     ctx->gram_bytes = 0;
+  }
+  return SVM_OK;
+}
+
+SVM_API int svmd_release_cache(void* h) {  // the library-owned Gram and the row-cache slab
+  SVMD_CTX(h);
+  int rc = release_gram(ctx);
+  if (rc) return rc;
+  if (ctx->rc_cache) {
+    SVMD_CHECK(hipSetDevice(ctx->device));
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+    SVMD_CHECK(hipFree(ctx->rc_cache));
+    ctx->rc_cache = nullptr;
+    ctx->rc_cache_bytes = 0;
   }
   return SVM_OK;
 }
@@ -357,7 +371,14 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
         ctx->gram = nullptr;
         ctx->gram_bytes = 0;
       }
-      const hipError_t e = hipMalloc(&ctx->gram, bytes);
+      hipError_t e = hipMalloc(&ctx->gram, bytes);
+      if (e != hipSuccess && ctx->rc_cache) {  // give back an idle row-cache slab and retry
+        (void)hipGetLastError();
+        SVMD_CHECK(hipFree(ctx->rc_cache));
+        ctx->rc_cache = nullptr;
+        ctx->rc_cache_bytes = 0;
+        e = hipMalloc(&ctx->gram, bytes);
+      }
       if (e != hipSuccess) {
         set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s", double(bytes) * 1e-9,
                   hipGetErrorString(e));
@@ -423,11 +444,14 @@ SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int
   if (gram_mode != 1 && mn_h && mx_h) plan_quant(mn_h, mx_h, d, &P);
   if (cache_bytes <= 0) {
     // Default: room for 16384 rows (an SMO touches a few thousand distinct rows at MNIST scale),
-    // capped at 60% of the free HBM (after releasing a cached library-owned Gram).
-    svmd_release_cache(ctx);
+    // capped at 60% of the HBM that is free or already this context's slab (after releasing a
+    // cached library-owned Gram).
+    rc = release_gram(ctx);
+    if (rc) return rc;
     size_t fr = 0, tot = 0;
     SVMD_CHECK(hipMemGetInfo(&fr, &tot));
-    cache_bytes = std::min<int64_t>(int64_t(double(fr) * 0.6), int64_t(16384) * ((n + 1) / 2 * 2) * 8);
+    cache_bytes = std::min<int64_t>(int64_t(double(fr + ctx->rc_cache_bytes) * 0.6),
+                                    int64_t(16384) * ((n + 1) / 2 * 2) * 8);
   }
   int32_t used = 0;
   TraceRange tr("svm355:smo:rowcache");

@@ -21,6 +21,10 @@ struct DeviceCtx {
   // svmd_release_cache / svmd_destroy or when a larger one is needed.
   double* gram = nullptr;
   size_t gram_bytes = 0;
+  // Row-cache slab (rowcache.hip), kept like the Gram: a large-n fit does not map and unmap tens of
+  // GB per call, and the default cache size does not depend on what the last free left unmapped.
+  double* rc_cache = nullptr;
+  size_t rc_cache_bytes = 0;
   unsigned long long* count_d = nullptr;  // device counter for count_sv
   // Cached SMO iteration graph (smo.hip) and the argument key it was captured for.
   hipGraphExec_t smo_exec = nullptr;
@@ -64,6 +68,21 @@ struct DeviceCtx {
     SVMD_CHECK(hipMalloc(&ws, sz));
     ws_bytes = sz;
     return SVM_OK;
+  }
+  double* ensure_rc_cache(size_t bytes) {  // nullptr when the allocation fails
+    if (bytes <= rc_cache_bytes) return rc_cache;
+    if (rc_cache) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+      (void)hipFree(rc_cache);
+      rc_cache = nullptr;
+      rc_cache_bytes = 0;
+    }
+    if (hipMalloc(&rc_cache, bytes) != hipSuccess) {
+      rc_cache = nullptr;
+      return nullptr;
+    }
+    rc_cache_bytes = bytes;
+    return rc_cache;
   }
   int ensure_pinned(size_t bytes) {
     if (bytes <= pinned_bytes) return SVM_OK;

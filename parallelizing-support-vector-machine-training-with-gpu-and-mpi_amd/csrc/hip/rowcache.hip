@@ -422,7 +422,7 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
   auto* stamp = static_cast<int64_t*>(dalloc(size_t(C) * 8));
   auto* idx = static_cast<int64_t*>(dalloc(size_t(n) * 8));
   auto* dtrace = tcap ? static_cast<int64_t*>(dalloc(size_t(tcap) * 16)) : nullptr;
-  auto* cache = static_cast<double*>(dalloc(size_t(C) * size_t(ldc) * 8));
+  double* cache = ctx->ensure_rc_cache(size_t(C) * size_t(ldc) * 8);  // context-held slab
   if (!f || !part || !st || !tags || !stamp || !idx || !cache || (tcap && !dtrace)) {
     release();
     set_error("row cache: out of device memory (cache of %lld rows x %lld)", (long long)C, (long long)n);
@@ -475,8 +475,20 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
       }
     }
   }
+  const char* vb = getenv("SVM355_RC_VERBOSE");
+  const bool verbose = vb && atoi(vb);
+  auto ms_since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
+  if (verbose) (void)hipStreamSynchronize(s);
+  const double t_prep = ms_since(t0);
   rc = run_smo_rc_persistent(ctx, q, int_ok, cache, ldc, C, y, alpha, f, n, p, r, trace, tcap);
   if (rc != kRcNotApplicable) {
+    if (verbose)
+      fprintf(stderr, "[rowcache n=%lld] cache %lld slots (%.1f GB, slab %.1f GB) | prep (alloc, quantise, interleave) "
+              "%.1f ms | persistent solve %.1f ms, %lld iterations\n", (long long)n, (long long)C,
+              double(C) * double(ldc) * 8e-9, double(ctx->rc_cache_bytes) * 1e-9, t_prep, ms_since(t0) - t_prep,
+              (long long)(r ? r->iterations : -1));
     release();
     return rc;
   }

@@ -371,6 +371,14 @@ __device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
   x += dpp_add_src<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
   return x;
 }
+// a strictly before b in wave_arg's order: the value key (smallest for MIN, largest for MAX), then
+// the lowest index.  A lane merging several candidates with it holds the one wave_arg would pick.
+template <bool MIN>
+__device__ __forceinline__ bool beats(VI a, VI b) {
+  const uint64_t ka = order_key(a.v), kb = order_key(b.v);
+  if (ka != kb) return MIN ? ka < kb : ka > kb;
+  return a.i < b.i;
+}
 // Requires a full wave (EXEC = all 64 lanes).  L = number of leading lanes that may hold candidates;
 // lanes >= L must hold "no candidate" sentinels (value +inf for MIN / -inf for MAX, index
 // kSentinel), which never beat a real candidate.
@@ -754,8 +762,10 @@ constexpr unsigned long long kRegisterTicks = 200000;
 // One solve of the persistent SMO by G co-resident workgroups (this one is g), NT threads per
 // workgroup (NW = NT/64 waves), E register-resident elements per thread: element e of thread t is
 // training point lo + t + NT*e of the workgroup's slice.  Epochs continue from epoch0 (record tags
-// must never repeat on a slot array); returns the last epoch used.
-template <int NT, int E, bool STAMP, bool XLOCAL, class Rows>
+// must never repeat on a slot array); returns the last epoch used.  RPL = records per sweep lane:
+// G <= 64 * RPL workgroups (lane L of wave 0 polls records L, L + 64, ...; slot arrays of 64 * RPL
+// records per epoch parity).  The exchange-skew stamps exist for RPL = 1 only.
+template <int NT, int E, bool STAMP, bool XLOCAL, class Rows, int RPL = 1>
 __device__ __forceinline__ uint32_t persist_solve(
     PersistShared& sh, int G, int g, uint32_t epoch0, const Rows& rows,
     const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice,
@@ -830,7 +840,7 @@ __device__ __forceinline__ uint32_t persist_solve(
     }
     __syncthreads();
     PSTAMP(1);
-    unsigned long long* rec = slots + (size_t(epoch & 1) * kMaxG) * kRecStride;
+    unsigned long long* rec = slots + (size_t(epoch & 1) * (64 * RPL)) * kRecStride;
     if (w == 0) {
       // ---- 2. merge the NW waves and publish this workgroup's record (lanes 0..9, one granule each)
       VI a{inf, kSentinel}, b{-inf, kSentinel};
@@ -887,22 +897,29 @@ __device__ __forceinline__ uint32_t persist_solve(
                              __HIP_MEMORY_SCOPE_AGENT);
       }
       PSTAMP(2);
-      if (STAMP && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
+      if (STAMP && RPL == 1 && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
         stamps[kSkewBase + g * kSkewEpochs + (epoch - kStampFrom)] = __builtin_amdgcn_s_memrealtime();
-      // ---- 3. lane L polls workgroup L's record until its ten tags equal the epoch
+      // ---- 3. lane L polls the records of workgroups L, L + 64, ... until their ten tags equal the
+      // epoch (every spin round re-reads all of them: one round trip, not one per record), then
+      // keeps the best of them under wave_arg's order (value key, then the lowest index)
       VI gm{inf, kSentinel}, gx{-inf, kSentinel};
       double agm = 0.0, agx = 0.0;
       bool timed_out = false;
       if (lane < G) {
-        const unsigned long long* r = rec + size_t(lane) * kRecStride;
-        uint32_t v[kGranules];
+        uint32_t v[RPL][kGranules];
         for (int64_t spins = 0;; ++spins) {
           bool ok = true;
 #pragma unroll
-          for (int k = 0; k < kGranules; ++k) {
-            const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[k] = uint32_t(x);
-            ok &= uint32_t(x >> 32) == epoch;
+          for (int rr = 0; rr < RPL; ++rr) {
+            if (RPL == 1 || lane + 64 * rr < G) {
+              const unsigned long long* r = rec + size_t(lane + 64 * rr) * kRecStride;
+#pragma unroll
+              for (int k = 0; k < kGranules; ++k) {
+                const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[rr][k] = uint32_t(x);
+                ok &= uint32_t(x >> 32) == epoch;
+              }
+            }
           }
           if (ok) break;
           if (spins > spin_limit) {
@@ -912,14 +929,24 @@ __device__ __forceinline__ uint32_t persist_solve(
           __builtin_amdgcn_s_sleep(1);
         }
         if (!timed_out) {
-          gm = VI{mk64(v[0], v[1]), v[2]};
-          agm = mk64(v[3], v[4]);
-          gx = VI{mk64(v[5], v[6]), v[7]};
-          agx = mk64(v[8], v[9]);
+#pragma unroll
+          for (int rr = 0; rr < RPL; ++rr) {
+            if (RPL == 1 || lane + 64 * rr < G) {
+              const VI cm{mk64(v[rr][0], v[rr][1]), v[rr][2]}, cx{mk64(v[rr][5], v[rr][6]), v[rr][7]};
+              if (rr == 0 || beats<true>(cm, gm)) {
+                gm = cm;
+                agm = mk64(v[rr][3], v[rr][4]);
+              }
+              if (rr == 0 || beats<false>(cx, gx)) {
+                gx = cx;
+                agx = mk64(v[rr][8], v[rr][9]);
+              }
+            }
+          }
         }
       }
       const bool any_to = __any(timed_out);
-      if (STAMP && g == 0 && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
+      if (STAMP && RPL == 1 && g == 0 && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
         stamps[kSkewBase + kMaxG * kSkewEpochs + (epoch - kStampFrom)] = __builtin_amdgcn_s_memrealtime();
       PSTAMP(3);
       const VIL wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
@@ -1098,7 +1125,7 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
 // Persistent SMO on the HBM row cache (n beyond the resident Gram; driven by rowcache.hip's
 // run_smo_rowcache): device-wide exchange over G co-resident workgroups, CachedRows as the row
 // source with its directory (nslots int32 tags + nslots / 2 MRU bytes) in dynamic LDS.
-template <int NT, int E, bool INT, bool STAMP>
+template <int NT, int E, bool INT, bool STAMP, int RPL>
 __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
     QRows q, double* __restrict__ cache, int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* __restrict__ y,
     double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
@@ -1112,8 +1139,9 @@ __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
   for (int64_t k = threadIdx.x; k < nslots / 2; k += NT) mru[k] = 0;
   __syncthreads();
   const CachedRows<INT> rows{q, cache, ldc, tags, mru, nslots / 2, neg_gamma};
-  persist_solve<NT, E, STAMP, false>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f, n, slice, slots, st,
-                                     C, eps, tau, max_iter, trace, trace_cap, err, spin_limit, stamps);
+  persist_solve<NT, E, STAMP, false, CachedRows<INT>, RPL>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f,
+                                                          n, slice, slots, st, C, eps, tau, max_iter, trace, trace_cap,
+                                                          err, spin_limit, stamps);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1512,15 +1540,31 @@ int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t
 }  // namespace
 
 namespace {
-template <int E, bool INT, bool STAMP>
+template <int E, bool INT, bool STAMP, int RPL>
 void launch_rc_e(hipStream_t s, int G, size_t lds, const QRows& q, double* cache, int64_t ldc, int64_t nslots,
                  double neg_gamma, const int32_t* y, double* alpha, double* f, int64_t n, unsigned long long* slots,
                  SmoState* st, const svm_params& p, int64_t* trace, int64_t tcap, unsigned* err) {
-  allow_lds(smo_rc_persistent_kernel<512, E, INT, STAMP>, lds);
-  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT, STAMP>), dim3(G), dim3(512), lds, s, q, cache, ldc, nslots,
-                     neg_gamma, y, alpha, f, n, int64_t(512) * E, slots, st, p.C, p.eps, p.tau, p.max_iter, trace, tcap,
-                     err, int64_t(1) << 24, reinterpret_cast<unsigned long long*>(err) + 8);
+  allow_lds(smo_rc_persistent_kernel<512, E, INT, STAMP, RPL>, lds);
+  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT, STAMP, RPL>), dim3(G), dim3(512), lds, s, q, cache, ldc,
+                     nslots, neg_gamma, y, alpha, f, n, int64_t(512) * E, slots, st, p.C, p.eps, p.tau, p.max_iter,
+                     trace, tcap, err, int64_t(1) << 24, reinterpret_cast<unsigned long long*>(err) + 8);
 }
+template <int E, int RPL>
+void launch_rc_variant(bool int_rows, bool stamp, hipStream_t s, int G, size_t lds, const QRows& q, double* cache,
+                       int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* y, double* alpha, double* f,
+                       int64_t n, unsigned long long* slots, SmoState* st, const svm_params& p, int64_t* trace,
+                       int64_t tcap, unsigned* err) {
+  if (int_rows && stamp)
+    launch_rc_e<E, true, true, RPL>(s, G, lds, q, cache, ldc, nslots, neg_gamma, y, alpha, f, n, slots, st, p, trace,
+                                    tcap, err);
+  else if (int_rows)
+    launch_rc_e<E, true, false, RPL>(s, G, lds, q, cache, ldc, nslots, neg_gamma, y, alpha, f, n, slots, st, p, trace,
+                                     tcap, err);
+  else
+    launch_rc_e<E, false, false, RPL>(s, G, lds, q, cache, ldc, nslots, neg_gamma, y, alpha, f, n, slots, st, p, trace,
+                                      tcap, err);
+}
+constexpr int kRcMaxG = 256;  // records per epoch parity of the row-cache solver's slot array
 }  // namespace
 
 // Persistent row-cache solve (see smo_rc_persistent_kernel).  f / alpha hold the initial state (cold
@@ -1532,13 +1576,27 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   if (const char* m = getenv("SVM355_RC_SMO"); m && !strcmp(m, "graph")) return kRcNotApplicable;
   if (n <= 0 || n >= int64_t(kSentinel)) return kRcNotApplicable;
   if (int_rows && q.kq > 32 * 128) return kRcNotApplicable;  // CachedRows::k12: two k-steps per lane
-  // Up to 8 register-resident points per thread (n <= 64 x 512 x 8 = 262,144): the E = 16 shape
-  // needs more than 256 VGPRs and spills, so larger n keep the replayed select / step graph.
-  int E = 0;
-  for (int e = 1; e <= 8 && !E; e *= 2)
-    if ((n + 512 * e - 1) / (512 * e) <= kMaxG) E = e;
+  // Shape: up to 8 register-resident points per thread (E = 16 needs more than 256 VGPRs and
+  // spills) and one 512-thread workgroup per CU, all co-resident.  Teams of up to 64 workgroups
+  // (one record per sweep lane) with E <= 4, then 128 and 256 (two / four records per lane, capped
+  // by the CU count) with E <= 8: n <= 256 x 512 x 8 = 1,048,576.  Measured (profiles/
+  // r2_rowcache_persistent.txt): at 60k 59 x E=2 beats 118 x E=1 (98 vs 104 ms); at 250k 123 x E=4
+  // beats 62 x E=8 (465 vs 572 ms: half the miss fill per workgroup); 256-wide teams lose to 128
+  // wherever both fit.  SVM355_RC_MAXG=128|256 starts at a wider team.  Larger n keep the replayed
+  // select / step graph.
+  int ncu = 0;
+  SVMD_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  int cap0 = 64;
+  if (const char* v = getenv("SVM355_RC_MAXG")) cap0 = std::max(64, std::min(kRcMaxG, atoi(v)));
+  int E = 0, G = 0;
+  for (int cap = cap0; cap <= kRcMaxG && !E; cap *= 2) {
+    const int maxg = std::min(cap, ncu);
+    for (int e = 1; e <= (cap == 64 ? 4 : 8) && !E; e *= 2)
+      if ((n + 512 * e - 1) / (512 * e) <= maxg) E = e;
+  }
   if (!E) return kRcNotApplicable;
-  const int G = int((n + 512 * E - 1) / (512 * E));
+  G = int((n + 512 * E - 1) / (512 * E));
+  const int rpl = G <= 64 ? 1 : G <= 128 ? 2 : 4;
   // Directory in LDS: up to 16384 slots (64 KB of tags + 8 KB of MRU bits) next to PersistShared.
   const int64_t nd = std::min<int64_t>(nslots, 16384) / 2 * 2;
   if (nd < 4) return kRcNotApplicable;
@@ -1547,7 +1605,9 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   hipStream_t s = ctx->stream;
   const int64_t tcap = trace ? std::max<int64_t>(trace_cap, 0) : 0;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  const size_t off_slots = 0, slot_bytes = size_t(2) * kMaxG * kRecStride * 8 + 256;
+  // records (both epoch parities), error word + phase stamps, exchange-skew stamps (RPL = 1)
+  const size_t rec_bytes = size_t(2) * kRcMaxG * kRecStride * 8;
+  const size_t off_slots = 0, slot_bytes = rec_bytes + 256 + (size_t(kMaxG) + 1) * kSkewEpochs * 8;
   const size_t off_st = off_slots + al(slot_bytes);
   const size_t off_trace = off_st + al(sizeof(SmoState));
   int rc = ctx->ensure_ws(off_trace + al(size_t(tcap) * 16));
@@ -1556,7 +1616,7 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   if (rc) return rc;
   char* ws = static_cast<char*>(ctx->ws);
   auto* slots = reinterpret_cast<unsigned long long*>(ws + off_slots);
-  auto* err = reinterpret_cast<unsigned*>(ws + off_slots + size_t(2) * kMaxG * kRecStride * 8);
+  auto* err = reinterpret_cast<unsigned*>(ws + off_slots + rec_bytes);
   auto* st = reinterpret_cast<SmoState*>(ws + off_st);
   int64_t* dtrace = tcap ? reinterpret_cast<int64_t*>(ws + off_trace) : nullptr;
   SmoState* hst = static_cast<SmoState*>(ctx->pinned);
@@ -1572,19 +1632,17 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
     SVMD_CHECK(hipMemcpyAsync(reinterpret_cast<unsigned long long*>(err) + 16, &from, 8, hipMemcpyHostToDevice, s));
     SVMD_CHECK(hipStreamSynchronize(s));
   }
-#define SVM_RC_CASE(e)                                                                                             \
-  case e:                                                                                                           \
-    if (int_rows && stamp)                                                                                          \
-      launch_rc_e<e, true, true>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap, err); \
-    else if (int_rows)                                                                                              \
-      launch_rc_e<e, true, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap,    \
-                                  err);                                                                             \
-    else                                                                                                            \
-      launch_rc_e<e, false, false>(s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, n, slots, st, p, dtrace, tcap,   \
-                                   err);                                                                            \
-    break;
-  switch (E) {
-    SVM_RC_CASE(1) SVM_RC_CASE(2) SVM_RC_CASE(4) SVM_RC_CASE(8)
+#define SVM_RC_CASE(e, r)                                                                                           \
+  else if (E == e && rpl == r) launch_rc_variant<e, r>(int_rows, stamp, s, G, lds, q, cache, ldc, nd, ng, y, alpha, f, \
+                                                       n, slots, st, p, dtrace, tcap, err);
+  if (false) {
+  }
+  SVM_RC_CASE(1, 1) SVM_RC_CASE(2, 1) SVM_RC_CASE(4, 1) SVM_RC_CASE(8, 1)
+  SVM_RC_CASE(1, 2) SVM_RC_CASE(2, 2) SVM_RC_CASE(4, 2) SVM_RC_CASE(8, 2)
+  SVM_RC_CASE(1, 4) SVM_RC_CASE(2, 4) SVM_RC_CASE(4, 4) SVM_RC_CASE(8, 4)
+  else {
+    set_error("row-cache SMO: no kernel for E=%d, %d records per lane", E, rpl);
+    return SVM_ERR_INTERNAL;
   }
 #undef SVM_RC_CASE
   SVMD_LAUNCH_CHECK();
@@ -1600,8 +1658,8 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
     unsigned long long hs[8];
     SVMD_CHECK(hipMemcpy(hs, reinterpret_cast<unsigned long long*>(err) + 8, sizeof(hs), hipMemcpyDeviceToHost));
     const double cnt = double(kStampCount);
-    fprintf(stderr, "[rc stamps G=%d E=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
-            "globalred+choose+barrier2 %.0f | rows (hit read / miss fill) %.0f | update %.0f | us/iter %.3f\n", G, E,
+    fprintf(stderr, "[rc stamps G=%d E=%d RPL=%d] cycles/iter: scan+wavered %.0f | barrier1 %.0f | publish %.0f | sweep %.0f | "
+            "globalred+choose+barrier2 %.0f | rows (hit read / miss fill) %.0f | update %.0f | us/iter %.3f\n", G, E, rpl,
             hs[0] / cnt, hs[1] / cnt, hs[2] / cnt, hs[3] / cnt, hs[4] / cnt, hs[5] / cnt, hs[6] / cnt,
             double(hs[7]) / 100.0 / cnt);
   }

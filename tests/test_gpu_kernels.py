@@ -469,6 +469,30 @@ def test_persistent_row_cache_equals_graph_row_cache(dev, D, monkeypatch, n, cac
     np.testing.assert_array_equal(a1, a2)
 
 
+def test_row_cache_wide_teams_follow_the_same_trajectory(dev, D, monkeypatch):
+    """Teams of more than 64 workgroups (each sweep lane merges two or four records under wave_arg's
+    order, smo.hip persist_solve<..., RPL>): n = 70k as 35 x E=4 (one record per lane), 69 x E=2
+    (SVM355_RC_MAXG=128: two) and 137 x E=1 (=256: four) -- the same trace, alphas and b."""
+    n = 70000
+    tr = synthetic_mnist(n, seed=24)
+    Xd = D.upload_rows(tr.compact().X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    yd = torch.from_numpy(tr.y).to(dev)
+    out = {}
+    for maxg in ("64", "128", "256"):
+        monkeypatch.setenv("SVM355_RC_MAXG", maxg)
+        a = torch.zeros(n, dtype=torch.float64, device=dev)
+        r, info = D.train(Xd, sqn, yd, a, SVMParams(), mn=mn, mx=mx, kcache="rows", trace_cap=200000)
+        out[maxg] = (r, info["trace"], a.cpu().numpy())
+    r0, t0, a0 = out["64"]
+    assert r0.stop_reason == "converged"
+    for maxg in ("128", "256"):
+        r, t, a = out[maxg]
+        assert r.iterations == r0.iterations and r.b == r0.b, maxg
+        np.testing.assert_array_equal(t, t0)
+        np.testing.assert_array_equal(a, a0)
+
+
 def test_row_cache_warm_start_bit_identical(dev, D):
     n = 1800
     tr = synthetic_mnist(n, seed=22)
