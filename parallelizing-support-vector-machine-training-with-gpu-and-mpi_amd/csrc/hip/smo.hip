@@ -212,9 +212,12 @@ __global__ void smo_init_cold_kernel(const int32_t* __restrict__ y, double* __re
   if (i == 0) *st = SmoState{0, 0, 0.0, 0.0, 0.0, 0.0, 1, 0, SVM_STOP_RUNNING};
 }
 
-// Warm start, step 1: ascending list of j with alpha_j != 0 (single workgroup, ballot compaction).
-__global__ __launch_bounds__(1024) void nonzero_compact_kernel(const double* __restrict__ alpha, int64_t n,
-                                                               int64_t* __restrict__ idx,
+// Warm start, step 1: ascending list of j with alpha_j != 0 (single workgroup, ballot compaction),
+// with coef_k = alpha_j * y_j next to it -- the first product of the reference's
+// alpha_j * y_j * K(j, i), so step 2 computes the same bits.
+__global__ __launch_bounds__(1024) void nonzero_compact_kernel(const double* __restrict__ alpha,
+                                                               const int32_t* __restrict__ y, int64_t n,
+                                                               int64_t* __restrict__ idx, double* __restrict__ coef,
                                                                int64_t* __restrict__ count, SmoState* st) {
   __shared__ int64_t wave_cnt[16];
   __shared__ int64_t base;
@@ -229,7 +232,11 @@ __global__ __launch_bounds__(1024) void nonzero_compact_kernel(const double* __r
     __syncthreads();
     int64_t off = base;
     for (int k = 0; k < w; ++k) off += wave_cnt[k];
-    if (nz) idx[off + __popcll(m & ((1ull << lane) - 1ull))] = i;
+    if (nz) {
+      const int64_t k = off + __popcll(m & ((1ull << lane) - 1ull));
+      idx[k] = i;
+      coef[k] = alpha[i] * double(y[i]);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       int64_t tot = 0;
@@ -245,22 +252,35 @@ __global__ __launch_bounds__(1024) void nonzero_compact_kernel(const double* __r
 }
 
 // Warm start, step 2: f_i = sum_{j in nz, ascending} alpha_j y_j K[j][i] - y_i
-// (mpi_svm_main3.cpp:169-186; column access K[j][i] is coalesced across i).
-__global__ __launch_bounds__(256) void warm_f_kernel(const double* __restrict__ K, int64_t ldk,
-                                                     const int32_t* __restrict__ y,
-                                                     const double* __restrict__ alpha,
-                                                     const int64_t* __restrict__ idx,
-                                                     const int64_t* __restrict__ count,
-                                                     double* __restrict__ f, int64_t n) {
+// (mpi_svm_main3.cpp:169-186; column access K[j][i] is coalesced across i).  The sum stays serial in
+// ascending j per point (the reference's order); the wave-uniform idx / coef loads are read kWarmU
+// at a time and the kWarmU column loads issued before the adds consume them, so each group costs
+// one memory round trip instead of a dependent chain per term.  64-thread blocks spread a
+// cascade-sized n over many CUs.
+constexpr int kWarmU = 8;
+__global__ __launch_bounds__(64) void warm_f_kernel(const double* __restrict__ K, int64_t ldk,
+                                                    const int32_t* __restrict__ y,
+                                                    const int64_t* __restrict__ idx,
+                                                    const double* __restrict__ coef,
+                                                    const int64_t* __restrict__ count,
+                                                    double* __restrict__ f, int64_t n) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
   const int64_t cnt = *count;
+  const int64_t ic = i < n ? i : n - 1;  // tail lanes read a valid column, store nothing
   double sum = 0.0;
-  for (int64_t k = 0; k < cnt; ++k) {
-    const int64_t j = idx[k];
-    sum += alpha[j] * double(y[j]) * K[j * ldk + i];
+  int64_t k = 0;
+  for (; k + kWarmU <= cnt; k += kWarmU) {
+    double kv[kWarmU], c[kWarmU];
+#pragma unroll
+    for (int u = 0; u < kWarmU; ++u) {
+      c[u] = coef[k + u];
+      kv[u] = K[idx[k + u] * ldk + ic];
+    }
+#pragma unroll
+    for (int u = 0; u < kWarmU; ++u) sum += c[u] * kv[u];
   }
-  f[i] = sum - static_cast<double>(y[i]);
+  for (; k < cnt; ++k) sum += coef[k] * K[idx[k] * ldk + ic];
+  if (i < n) f[i] = sum - static_cast<double>(y[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1683,7 +1703,8 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   const size_t off_part = off_f + al(size_t(n) * 8);
   const size_t off_state = off_part + al(size_t(nblk) * sizeof(Partial));
   const size_t off_idx = off_state + al(sizeof(SmoState));
-  const size_t off_cnt = off_idx + al(size_t(n) * 8);
+  const size_t off_coef = off_idx + al(size_t(n) * 8);
+  const size_t off_cnt = off_coef + al(size_t(n) * 8);
   const size_t off_trace = off_cnt + al(8);
   const size_t off_slots = off_trace + al(size_t(tcap) * 16);
   // records + error word + phase stamps + exchange-skew stamps
@@ -1698,6 +1719,7 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   Partial* part = reinterpret_cast<Partial*>(ws + off_part);
   SmoState* st = reinterpret_cast<SmoState*>(ws + off_state);
   int64_t* idx = reinterpret_cast<int64_t*>(ws + off_idx);
+  double* coef = reinterpret_cast<double*>(ws + off_coef);
   int64_t* cnt = reinterpret_cast<int64_t*>(ws + off_cnt);
   int64_t* dtrace = tcap ? reinterpret_cast<int64_t*>(ws + off_trace) : nullptr;
 
@@ -1706,10 +1728,10 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
                        n, st);
     SVMD_LAUNCH_CHECK();
   } else {
-    hipLaunchKernelGGL(nonzero_compact_kernel, dim3(1), dim3(1024), 0, s, alpha, n, idx, cnt, st);
+    hipLaunchKernelGGL(nonzero_compact_kernel, dim3(1), dim3(1024), 0, s, alpha, y, n, idx, coef, cnt, st);
     SVMD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(warm_f_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, K, ldk, y, alpha,
-                       idx, cnt, f, n);
+    hipLaunchKernelGGL(warm_f_kernel, dim3(unsigned((n + 63) / 64)), dim3(64), 0, s, K, ldk, y, idx, coef, cnt, f,
+                       n);
     SVMD_LAUNCH_CHECK();
   }
 
