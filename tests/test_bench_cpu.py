@@ -1,0 +1,63 @@
+"""bench.py's host-side logic on the CPU: the cascade critical path (the per-round slowest local
+solve plus rank 0's merge; the solo device times of a serial-solve rehearsal when present), the
+launch checks of ``--gpus N``, and the solve-log fields the critical path reads from the native
+driver."""
+import sys
+from pathlib import Path
+
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+from svm355 import SVMParams  # noqa: E402
+from svm355.parallel.cascade import CascadeSVM  # noqa: E402
+from svm355.utils.data import synthetic_mnist  # noqa: E402
+
+
+def _s(rank, rnd, layer, ms, it, solo=-1.0):
+    return {"rank": rank, "round": rnd, "layer": layer, "ms": ms, "iterations": it, "solo_ms": solo}
+
+
+def test_star_critical_path_takes_slowest_local_plus_merge():
+    solves = [_s(0, 1, "local", 5.0, 100), _s(1, 1, "local", 7.0, 90), _s(0, 1, "merge", 3.0, 40),
+              _s(0, 2, "local", 1.0, 10), _s(1, 2, "local", 2.0, 20), _s(0, 2, "merge", 0.5, 5)]
+    rows, tot = bench.critical_path(solves, "star")
+    assert rows == [[1, 7.0, 3.0, 100, 40], [2, 2.0, 0.5, 20, 5]]
+    assert tot == pytest.approx(12.5)
+
+
+def test_tree_critical_path_takes_slowest_rank_of_every_layer():
+    solves = [_s(0, 1, "layer1", 4.0, 50), _s(1, 1, "layer1", 6.0, 70), _s(2, 1, "layer1", 5.0, 60),
+              _s(3, 1, "layer1", 1.0, 10), _s(0, 1, "layer2", 2.0, 30), _s(2, 1, "layer2", 3.0, 35),
+              _s(0, 1, "layer4", 1.5, 20)]
+    rows, tot = bench.critical_path(solves, "tree")
+    assert rows == [[1, 6.0, 4.5, 70, 55]]
+    assert tot == pytest.approx(10.5)
+
+
+def test_critical_path_prefers_solo_device_times():
+    """A serial-solve rehearsal (SVM355_CASCADE_SERIAL_SOLVES=1) logs each solve's time alone on the
+    device; the wall time of ranks sharing one GPU would overstate the P-GPU critical path."""
+    solves = [_s(0, 1, "local", 50.0, 100, solo=5.0), _s(1, 1, "local", 70.0, 90, solo=7.5),
+              _s(0, 1, "merge", 30.0, 40, solo=3.0)]
+    rows, tot = bench.critical_path(solves, "star")
+    assert rows == [[1, 7.5, 3.0, 100, 40]]
+    assert tot == pytest.approx(10.5)
+
+
+def test_more_gpus_than_visible_is_refused(capsys):
+    """Launched directly on a host without N GPUs, bench exits non-zero with a message (unless a
+    loopback rehearsal is asked for) instead of hanging or silently running fewer ranks."""
+    assert bench.main(["--gpus", "2", "--steps", "1", "--warmup", "0"]) == 2
+    assert "visible GPUs" in capsys.readouterr().err
+
+
+def test_cpu_solve_log_has_the_fields_the_critical_path_reads():
+    tr = synthetic_mnist(600, seed=5)
+    r = CascadeSVM(SVMParams(n_threads=2)).fit(tr.X, tr.y, world=2).result
+    assert r.solves
+    for s in r.solves:
+        assert {"rank", "round", "layer", "ms", "iterations", "skipped", "row_cache", "solo_ms"} <= set(s)
+        assert s["row_cache"] is False and s["solo_ms"] < 0  # CPU backend: no row cache, no solo timing
+    rows, tot = bench.critical_path(r.solves, "star")
+    assert len(rows) == r.rounds and tot > 0
