@@ -4,8 +4,12 @@
 // Reference: the reference never stores the Gram; it keeps the last i_high / i_low rows and
 // recomputes a row (calc_kernel_matrix, gpu_svm_main3.cu:137-147, :394-411) whenever the pair
 // changes.  Here rows live in a 2-way set-associative LRU cache of C slots (C x n doubles, sized
-// from the free HBM), and the host is never involved per iteration.  One SMO iteration = two
-// kernels of a replayed hipGraph:
+// from the free HBM, held by the device context), and the host is never involved per iteration.
+//
+// Default solver: smo.hip's persistent row-cache kernel (run_smo_rc_persistent: one launch, the
+// directory replicated in every workgroup's LDS, misses filled per workgroup slice from the
+// chunk-interleaved quantised rows built here), for n <= 1,048,576.  Beyond its shapes (or with
+// SVM355_RC_SMO=graph) one SMO iteration = two kernels of a replayed hipGraph:
 //
 //   kc_select  f += ch*row(ih) + cl*row(il) for the previous pair — each row read from its cache
 //              slot or, on a miss, computed here for every column and stored into the slot (the

@@ -8,8 +8,11 @@ over the SVs (main3.cpp:391-402; the serial/GPU programs map 0 to -1, the cascad
 
 Backends
   device="cpu"   native C++ oracle (bit-exact reference arithmetic), ``n_threads`` workers
-  device="cuda"  gfx950 kernels: H2D, fused min/max + scale + row norms, MFMA f64 RBF Gram kept
-                 resident in HBM, graph-replayed device SMO, MFMA decision function
+  device="cuda"  gfx950 kernels: H2D, fused min/max + scale + row norms, the exact-integer int8-MFMA
+                 RBF Gram (f64-MFMA for real-valued data) kept resident in HBM, the persistent
+                 device SMO (one launch, register-resident slices), MFMA decision function over the
+                 SVs; ``kcache="rows"`` (automatic when the Gram does not fit) solves on the HBM row
+                 cache instead
 """
 from __future__ import annotations
 
