@@ -44,6 +44,8 @@ class SvmParams(ctypes.Structure):
         ("max_iter", c_int64),
         ("n_threads", c_int32),
         ("verbose", c_int32),
+        ("wss", c_int32),
+        ("reserved", c_int32),
     ]
 
 
@@ -267,6 +269,6 @@ def ptr(a) -> int:
 
 
 def params_struct(C=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, sv_tol=1e-8, max_iter=100000,
-                  n_threads=1, verbose=0) -> SvmParams:
+                  n_threads=1, verbose=0, wss=1) -> SvmParams:
     return SvmParams(float(C), float(gamma), float(tau), float(eps), float(sv_tol), int(max_iter),
-                     int(n_threads), int(verbose))
+                     int(n_threads), int(verbose), int(wss), 0)

@@ -7,6 +7,12 @@
 //   stop when b_low <= b_high + 2*tau, no candidate, infeasible [U,V], eta <= eps, or iterations
 //   exceed max_iter; b = (b_high + b_low)/2.
 // Kernel rows of i_high / i_low are recomputed only when the index changes (main3.cpp:216-232).
+//
+// Opt-in (svm_params.wss = 2, not the reference): second-order selection of the second index
+// (Fan, Chen & Lin 2005, WSS 2).  i_high and the stop test stay first-order; then
+//   j = argmin over t in I_low with f_t > f_{i_high} of  -(f_t - f_{i_high})^2 / a_t,
+//   a_t = K(i,i) + K(t,t) - 2 K(i,t)  (K(t,t) = 1 for the RBF kernel; a_t <= 0 -> eps),
+// lowest index on ties, and the pair (i_high, j) gets the same two-variable update.
 // With n_threads > 1 the O(n) loops are split into static chunks; each element is computed by the
 // same expression, and the argmin/argmax merge keeps the serial lowest-index rule, so the result is
 // bit-identical to the serial run.
@@ -144,17 +150,49 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
       i_high_prev = i_high;
       rows.fill(i_high, Kh.data(), n, team);
     }
-    if (i_low != i_low_prev) {
-      i_low_prev = i_low;
-      rows.fill(i_low, Kl.data(), n, team);
+    int64_t i_low_upd = i_low;  // the second index of the update
+    double f_low = b_low;
+    if (p.wss == 2) {  // second-order choice of the second index (needs row i_high)
+      const double K11 = Kh[size_t(i_high)];
+      auto scan2 = [&](int64_t c) {
+        const int64_t lo = c * chunk, hi = std::min(n, lo + chunk);
+        Pick g{std::numeric_limits<double>::infinity(), n};
+        for (int64_t t = lo; t < hi; ++t) {
+          const double a = alpha[t], ft = f[size_t(t)];
+          const bool in_low = (y[t] == 1 && a > 0.0 + eps) || (y[t] == -1 && a < C - eps);
+          if (!in_low || !(ft > b_high)) continue;
+          const double bb = ft - b_high;
+          double at = K11 + 1.0 - 2.0 * Kh[size_t(t)];
+          if (at <= 0.0) at = eps;
+          const double gain = -(bb * bb) / at;
+          if (gain < g.v) g = {gain, t};
+        }
+        pl[size_t(c)] = g;
+      };
+      if (nchunks == 1) {
+        scan2(0);
+      } else {
+        team.parallel_for(nchunks, [&](int64_t lo, int64_t hi) {
+          for (int64_t c = lo; c < hi; ++c) scan2(c);
+        });
+      }
+      Pick g = pl[0];
+      for (int64_t c = 1; c < nchunks; ++c)
+        if (pl[size_t(c)].v < g.v) g = pl[size_t(c)];
+      i_low_upd = g.i;  // exists: the first-order i_low has f > b_high + 2 tau
+      f_low = f[size_t(i_low_upd)];
+    }
+    if (i_low_upd != i_low_prev) {
+      i_low_prev = i_low_upd;
+      rows.fill(i_low_upd, Kl.data(), n, team);
     }
     // --- two-variable update (main3.cpp:235-266)
-    const int s = y[i_high] * y[i_low];
+    const int s = y[i_high] * y[i_low_upd];
     const double K11 = Kh[size_t(i_high)];
-    const double K22 = Kl[size_t(i_low)];
-    const double K12 = Kh[size_t(i_low)];
+    const double K22 = Kl[size_t(i_low_upd)];
+    const double K12 = Kh[size_t(i_low_upd)];
     const double eta = K11 + K22 - 2.0 * K12;
-    const double ah = alpha[i_high], al = alpha[i_low];
+    const double ah = alpha[i_high], al = alpha[i_low_upd];
     double U, V;
     if (s == -1) {
       U = std::max(0.0, al - ah);
@@ -171,21 +209,21 @@ int smo_solve(const Rows& rows, const int32_t* y, int64_t n, double* alpha, int3
       stop = SVM_STOP_NONPOS_ETA;
       break;
     }
-    double al_new = al + y[i_low] * (b_high - b_low) / eta;
+    double al_new = al + y[i_low_upd] * (b_high - f_low) / eta;
     if (al_new > V) al_new = V;
     if (al_new < U) al_new = U;
     const double ah_new = ah + s * (al - al_new);
     // --- f update (main3.cpp:268-275): f_i += (dh*y_h)*Kh_i + (dl*y_l)*Kl_i
     const double dh = ah_new - ah, dl = al_new - al;
-    const int32_t yh = y[i_high], yl = y[i_low];
+    const int32_t yh = y[i_high], yl = y[i_low_upd];
     team.parallel_for(n, [&](int64_t lo, int64_t hi) {
       for (int64_t i = lo; i < hi; ++i) f[size_t(i)] += dh * yh * Kh[size_t(i)] + dl * yl * Kl[size_t(i)];
     });
     alpha[i_high] = ah_new;
-    alpha[i_low] = al_new;
+    alpha[i_low_upd] = al_new;
     if (trace && n_trace < trace_cap) {
       trace[2 * n_trace] = i_high;
-      trace[2 * n_trace + 1] = i_low;
+      trace[2 * n_trace + 1] = i_low_upd;
       ++n_trace;
     }
     ++num_iter;

@@ -50,6 +50,8 @@ typedef struct svm_params {
   int64_t max_iter;  // default 100000 (num_iter starts at 1)
   int32_t n_threads; // CPU worker threads (1 = the serial reference baseline)
   int32_t verbose;
+  int32_t wss;       // working-set selection: 0 / 1 = first order (reference), 2 = second-order j
+  int32_t reserved;
 } svm_params;
 
 typedef struct svm_result {

@@ -40,10 +40,13 @@ class SVMParams:
     sv_tol: float = 1e-8
     max_iter: int = 100000
     n_threads: int = 1
+    # working-set selection: 1 = first order (the reference, Keerthi et al.), 2 = second-order choice
+    # of the second index (Fan, Chen & Lin 2005; opt-in, not the reference's trajectory)
+    wss: int = 1
 
     def to_struct(self, verbose: int = 0):
         return params_struct(self.C, self.gamma, self.tau, self.eps, self.sv_tol, self.max_iter,
-                             self.n_threads, verbose)
+                             self.n_threads, verbose, self.wss)
 
     def replace(self, **kw) -> "SVMParams":
         return dataclasses.replace(self, **kw)

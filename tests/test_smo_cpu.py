@@ -13,8 +13,10 @@ from svm355.ops import cpu as C
 from svm355.utils.data import MinMaxScaler
 
 
-def py_reference_smo(X, y, C_=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, max_iter=100000, alpha=None):
-    """Line-by-line transcription of SMO_train (main3.cpp:162-294), warm start if alpha given."""
+def py_reference_smo(X, y, C_=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, max_iter=100000, alpha=None, wss=1):
+    """Line-by-line transcription of SMO_train (main3.cpp:162-294), warm start if alpha given.
+    wss=2: the second index is chosen by second-order gain (Fan, Chen & Lin 2005, WSS 2) among
+    I_low points with f above b_high; i_high, the stop test and b stay first-order."""
     n, d = X.shape
 
     def kern(a, b):
@@ -62,6 +64,22 @@ def py_reference_smo(X, y, C_=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, max_iter
         if ih != ihp:
             ihp = ih
             Kh = [kern(X[ih], X[j]) for j in range(n)]
+        if wss == 2:
+            jbest, gbest = n, math.inf
+            for t in range(n):
+                in_l = (y[t] == 1 and alpha[t] > 0.0 + eps) or (y[t] == -1 and alpha[t] < C_ - eps)
+                if not in_l or not f[t] > bh:
+                    continue
+                bb = f[t] - bh
+                at = Kh[ih] + 1.0 - 2.0 * Kh[t]  # K(t, t) = 1 for the RBF kernel
+                if at <= 0.0:
+                    at = eps
+                g = -(bb * bb) / at
+                if g < gbest:
+                    gbest, jbest = g, t
+            il, bl_upd = jbest, f[jbest]
+        else:
+            bl_upd = bl
         if il != ilp:
             ilp = il
             Kl = [kern(X[il], X[j]) for j in range(n)]
@@ -78,7 +96,7 @@ def py_reference_smo(X, y, C_=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, max_iter
         if eta <= eps:
             reason = "nonpositive_eta"
             break
-        aln = al + y[il] * (bh - bl) / eta
+        aln = al + y[il] * (bh - bl_upd) / eta
         aln = min(aln, V)
         aln = max(aln, U)
         ahn = ah + s * (al - aln)
@@ -110,6 +128,37 @@ def test_oracle_bit_identical_to_python_transcription(seed):
     assert res.stop_reason == reason
     np.testing.assert_array_equal(a, a_ref)
     assert res.b == b_ref
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_wss2_oracle_bit_identical_to_python_transcription(seed):
+    X, y = _toy(seed=seed)
+    p = SVMParams(gamma=0.5, wss=2)
+    a, res, _ = C.smo_train(X, y, p)
+    a_ref, it_ref, b_ref, reason = py_reference_smo(X, y.tolist(), gamma=0.5, wss=2)
+    assert res.iterations == it_ref
+    assert res.stop_reason == reason
+    np.testing.assert_array_equal(a, a_ref)
+    assert res.b == b_ref
+
+
+def test_wss2_reaches_the_first_order_optimum_in_fewer_iterations(small_mnist):
+    """Second-order selection changes the path, not the problem: same SVs (within 2), b within the
+    stopping tolerance, fewer iterations, same result with any thread count."""
+    tr, _ = small_mnist
+    X = MinMaxScaler().fit_transform(tr.X[:600])
+    y = tr.y[:600]
+    a1, r1, _ = C.smo_train(X, y, SVMParams(n_threads=2))
+    a2, r2, t2 = C.smo_train(X, y, SVMParams(n_threads=2, wss=2), trace_cap=100000)
+    a2s, r2s, t2s = C.smo_train(X, y, SVMParams(n_threads=1, wss=2), trace_cap=100000)
+    assert r1.stop_reason == r2.stop_reason == "converged"
+    assert r2.iterations < r1.iterations
+    sv1, sv2 = set(np.flatnonzero(a1 > 1e-8).tolist()), set(np.flatnonzero(a2 > 1e-8).tolist())
+    assert len(sv1 ^ sv2) <= 2
+    assert abs(r1.b - r2.b) < 1e-4 * max(1.0, abs(r1.b))
+    assert r2.iterations == r2s.iterations and r2.b == r2s.b
+    np.testing.assert_array_equal(a2, a2s)
+    np.testing.assert_array_equal(t2, t2s)
 
 
 def test_warm_start_bit_identical_to_python_transcription():
