@@ -429,6 +429,7 @@ struct PersistShared {
   int timeout;
   int64_t rslot[2];             // cached row source: slots of rows (i_high, i_low) ...
   int32_t rmiss[2];             // ... and whether this epoch fills them
+  double k12;                   // second-order selection: K(i_high, j) from the winner's record
 };
 
 // ---- Row sources of the persistent solver.  choose() runs on one lane of every workgroup once the
@@ -785,7 +786,12 @@ constexpr unsigned long long kRegisterTicks = 200000;
 // must never repeat on a slot array); returns the last epoch used.  RPL = records per sweep lane:
 // G <= 64 * RPL workgroups (lane L of wave 0 polls records L, L + 64, ...; slot arrays of 64 * RPL
 // records per epoch parity).  The exchange-skew stamps exist for RPL = 1 only.
-template <int NT, int E, bool STAMP, bool XLOCAL, class Rows, int RPL = 1>
+// WSS2 (opt-in, resident Gram, RPL = 1): second-order choice of the second index (smo_cpu.cpp):
+// after the first exchange names i_high (and the first-order maximum for the stop test), every
+// workgroup reads its slice of row i_high, computes -(f_t - f_ih)^2 / a_t over its I_low points
+// above f_ih, and a second exchange (the next epoch) picks the minimum; its record carries the
+// gain, j, alpha_j, f_j and K(i_high, j) (from the owner's row slice).
+template <int NT, int E, bool STAMP, bool XLOCAL, class Rows, int RPL = 1, bool WSS2 = false>
 __device__ __forceinline__ uint32_t persist_solve(
     PersistShared& sh, int G, int g, uint32_t epoch0, const Rows& rows,
     const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice,
@@ -999,7 +1005,8 @@ __device__ __forceinline__ uint32_t persist_solve(
       stop = SVM_STOP_NO_CANDIDATE;
       break;
     }
-    const int64_t ih = uih, il = uil;
+    const int64_t ih = uih;
+    int64_t il = uil;
     const double bh = sh.gv[0], bl = sh.gv[1];
     b_high = bh;
     b_low = bl;
@@ -1007,13 +1014,157 @@ __device__ __forceinline__ uint32_t persist_solve(
       stop = SVM_STOP_CONVERGED;
       break;
     }
-    // One memory round trip: scalars + this slice of rows i_high and i_low.
-    const int32_t yh = y[ih], yl = y[il];
     double K11, K22, K12;
     double kh[E], kl[E];
-    rows.template fetch<NT, E>(sh, ih, il, lo, t, hi_end, kh, kl, K11, K22, K12);
+    int32_t yh, yl;
+    double bl_upd = bl, al = sh.ga[1];  // the second index's f and alpha in the update
+    if constexpr (WSS2) {
+      static_assert(RPL == 1, "second-order selection: one record per sweep lane");
+      // ---- 4b. row i_high, the local second-order candidate, a second exchange for j
+      const double* Kh = rows.K + ih * rows.ldk;
+      K11 = Kh[ih];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t i = lo + t + NT * e;
+        kh[e] = i < hi_end ? Kh[i] : 0.0;
+      }
+      VI cm{inf, kSentinel};
+      double ca = 0.0, cf = 0.0, ck = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double a = ar[e], ft = fr[e];
+        const int32_t yt = yr[e];
+        const bool in_low = (yt == 1 && a > c_lo) || (yt == -1 && a < c_hi);
+        if (!in_low || !(ft > bh)) continue;
+        const double bb = ft - bh;
+        double at = K11 + 1.0 - 2.0 * kh[e];  // K(t, t) = 1 for the RBF kernel
+        if (at <= 0.0) at = eps;
+        const double gain = -(bb * bb) / at;
+        if (gain < cm.v) {  // ascending index within a thread: strict compare keeps the lowest
+          cm = VI{gain, uint32_t(lo + t + NT * e)};
+          ca = a;
+          cf = ft;
+          ck = kh[e];
+        }
+      }
+      {
+        const VIL wc = wave_arg<true>(cm);
+        const double wa = read_lane64(ca, wc.lane), wf = read_lane64(cf, wc.lane), wk = read_lane64(ck, wc.lane);
+        if (lane == 0) {
+          sh.wv[0][w] = wc.v;
+          sh.wi[0][w] = wc.i;
+          sh.wa[0][w] = wa;
+          sh.wv[1][w] = wf;
+          sh.wa[1][w] = wk;
+        }
+      }
+      __syncthreads();
+      ++epoch;  // the second exchange's tags (records alternate parity buffers per exchange)
+      unsigned long long* rec2 = slots + (size_t(epoch & 1) * (64 * RPL)) * kRecStride;
+      if (w == 0) {
+        VI a{inf, kSentinel};
+        double aa = 0.0, af = 0.0, ak = 0.0;
+        {
+          VI c{inf, kSentinel};
+          double c_a = 0.0, c_f = 0.0, c_k = 0.0;
+          if (lane < NW) {
+            c = VI{sh.wv[0][lane], sh.wi[0][lane]};
+            c_a = sh.wa[0][lane];
+            c_f = sh.wv[1][lane];
+            c_k = sh.wa[1][lane];
+          }
+          const VIL r = wave_arg<true, NW>(c);
+          a = VI{r.v, r.i};
+          aa = read_lane64(c_a, r.lane);
+          af = read_lane64(c_f, r.lane);
+          ak = read_lane64(c_k, r.lane);
+        }
+        if (lane < kGranules) {
+          uint32_t pay = lo32(a.v);
+          pay = lane == 1 ? hi32(a.v) : pay;
+          pay = lane == 2 ? a.i : pay;
+          pay = lane == 3 ? lo32(aa) : pay;
+          pay = lane == 4 ? hi32(aa) : pay;
+          pay = lane == 5 ? lo32(af) : pay;
+          pay = lane == 6 ? hi32(af) : pay;
+          pay = lane == 7 ? a.i : pay;
+          pay = lane == 8 ? lo32(ak) : pay;
+          pay = lane == 9 ? hi32(ak) : pay;
+          if constexpr (XLOCAL)  // same scope rule as the first exchange (memory-model note above)
+            __hip_atomic_store(rec2 + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            __hip_atomic_store(rec2 + size_t(g) * kRecStride + lane, (uint64_t(epoch) << 32) | pay, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        VI gm{inf, kSentinel};
+        double ga = 0.0, gf = 0.0, gk = 0.0;
+        bool timed_out = false;
+        if (lane < G) {
+          const unsigned long long* r = rec2 + size_t(lane) * kRecStride;
+          uint32_t v[kGranules];
+          for (int64_t spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < kGranules; ++k) {
+              const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              v[k] = uint32_t(x);
+              ok &= uint32_t(x >> 32) == epoch;
+            }
+            if (ok) break;
+            if (spins > spin_limit) {
+              timed_out = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!timed_out) {
+            gm = VI{mk64(v[0], v[1]), v[2]};
+            ga = mk64(v[3], v[4]);
+            gf = mk64(v[5], v[6]);
+            gk = mk64(v[8], v[9]);
+          }
+        }
+        const bool any_to2 = __any(timed_out);
+        const VIL wgm = wave_arg<true>(gm);
+        const double wga = read_lane64(ga, wgm.lane), wgf = read_lane64(gf, wgm.lane), wgk = read_lane64(gk, wgm.lane);
+        if (lane == 0) {
+          sh.gi[1] = wgm.i;
+          sh.ga[1] = wga;
+          sh.gv[1] = wgf;
+          sh.k12 = wgk;
+          if (any_to2) {
+            sh.timeout = 1;
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      __syncthreads();
+      if (sh.timeout) {
+        stop = -1;
+        break;
+      }
+      il = sh.gi[1];  // exists: the first-order i_low lies above f_ih + 2 tau
+      bl_upd = sh.gv[1];
+      al = sh.ga[1];
+      K12 = sh.k12;
+      const double* Kl = rows.K + il * rows.ldk;
+      K22 = Kl[il];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t i = lo + t + NT * e;
+        kl[e] = i < hi_end ? Kl[i] : 0.0;
+      }
+      yh = y[ih];
+      yl = y[il];
+    } else {
+      // One memory round trip: scalars + this slice of rows i_high and i_low.
+      yh = y[ih];
+      yl = y[il];
+      rows.template fetch<NT, E>(sh, ih, il, lo, t, hi_end, kh, kl, K11, K22, K12);
+    }
     PSTAMP(5);
-    const double ah = sh.ga[0], al = sh.ga[1];
+    const double ah = sh.ga[0];
     const int s = yh * yl;
     const double eta = K11 + K22 - 2.0 * K12;
     double U, V;
@@ -1032,7 +1183,7 @@ __device__ __forceinline__ uint32_t persist_solve(
       stop = SVM_STOP_NONPOS_ETA;
       break;
     }
-    double al_new = al + double(yl) * (bh - bl) / eta;
+    double al_new = al + double(yl) * (bh - bl_upd) / eta;
     if (al_new > V) al_new = V;
     if (al_new < U) al_new = U;
     const double ah_new = ah + double(s) * (al - al_new);
@@ -1120,7 +1271,7 @@ __device__ __forceinline__ unsigned xcc_id() {
 // stores, L1-bypassing sc1 loads) instead of the device-wide fabric.  If XCD 0 receives fewer than
 // glocal workgroups the registration is abandoned before any state is touched (err = 2) and the
 // host falls back to the device-wide kernel.
-template <int NT, int E, bool STAMP, bool XLOCAL = false>
+template <int NT, int E, bool STAMP, bool XLOCAL = false, bool WSS2 = false>
 __global__ __launch_bounds__(NT) void smo_persistent_kernel(
     const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ y, double* __restrict__ alpha,
     double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
@@ -1137,7 +1288,8 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
     G = glocal;
     g = s_rank;
   }
-  persist_solve<NT, E, STAMP, XLOCAL>(sh, G, g, 0, ResidentRows{K, ldk}, y, alpha, f, n, slice, slots, st, C, eps,
+  persist_solve<NT, E, STAMP, XLOCAL, ResidentRows, 1, WSS2>(sh, G, g, 0, ResidentRows{K, ldk}, y, alpha, f, n, slice,
+                                                             slots, st, C, eps,
                                       tau, max_iter,
                                       trace, trace_cap, err, spin_limit, stamps);
 }
@@ -1453,9 +1605,24 @@ void allow_lds(Kern k, size_t bytes) {
 template <int NT, int E>
 int launch_persistent_e(hipStream_t s, int G, const double* K, int64_t ldk, const int32_t* y, double* alpha,
                         double* f, int64_t n, unsigned long long* slots, SmoState* st, double C, double eps,
-                        double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err, bool xlocal) {
+                        double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err, bool xlocal,
+                        bool wss2) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(err) + 8;
   const int64_t slice = int64_t(NT) * E;
+  if (wss2) {  // opt-in second-order selection (no stamp variant)
+    if (xlocal) {
+      const size_t lds = xcd_lds_pad(NT);
+      allow_lds(smo_persistent_kernel<NT, E, false, true, true>, lds);
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, true, true>), dim3(16 * G), dim3(NT), lds, s, K, ldk, y,
+                         alpha, f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 22,
+                         stamps, G, register_ticks());
+    } else {
+      hipLaunchKernelGGL((smo_persistent_kernel<NT, E, false, false, true>), dim3(G), dim3(NT), 0, s, K, ldk, y, alpha,
+                         f, n, slice, slots, st, C, eps, tau, max_iter, trace, tcap, err, int64_t(1) << 24, stamps);
+    }
+    SVMD_LAUNCH_CHECK();
+    return SVM_OK;
+  }
   const char* sv = getenv("SVM355_PSMO_STAMP");
   if (xlocal) {
     // Over-provisioned grid: ~2*G workgroups per XCD under round-robin dispatch; G of XCD 0's join.
@@ -1521,11 +1688,11 @@ int persistent_grid(int64_t n, int* G_out, int* E_out, int* NT_out, int gcap) {
 int launch_persistent(hipStream_t s, int NT, int E, int G, const double* K, int64_t ldk, const int32_t* y,
                       double* alpha, double* f, int64_t n, unsigned long long* slots, SmoState* st, double C,
                       double eps, double tau, int64_t max_iter, int64_t* trace, int64_t tcap, unsigned* err,
-                      bool xlocal) {
+                      bool xlocal, bool wss2) {
 #define SVM_PSMO_CASE(nt, e)                                                                                 \
   if (NT == nt && E == e)                                                                                    \
     return launch_persistent_e<nt, e>(s, G, K, ldk, y, alpha, f, n, slots, st, C, eps, tau, max_iter, trace, \
-                                      tcap, err, xlocal);
+                                      tcap, err, xlocal, wss2);
   SVM_PSMO_CASE(256, 1) SVM_PSMO_CASE(256, 2) SVM_PSMO_CASE(256, 4) SVM_PSMO_CASE(256, 8) SVM_PSMO_CASE(256, 16)
   SVM_PSMO_CASE(512, 1) SVM_PSMO_CASE(512, 2) SVM_PSMO_CASE(512, 4) SVM_PSMO_CASE(512, 8)
   SVM_PSMO_CASE(1024, 1) SVM_PSMO_CASE(1024, 2) SVM_PSMO_CASE(1024, 4)
@@ -1742,7 +1909,10 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   const bool force_single = mode && strcmp(mode, "single") == 0;
   int64_t single_max = kSingleDefaultMax;
   if (const char* v = getenv("SVM355_SMO_SINGLE_MAX")) single_max = atoll(v);
-  if ((force_single || !mode || strcmp(mode, "auto") == 0) && (force_single || n <= single_max) && n <= 8192) {
+  // Second-order selection (p.wss == 2, opt-in) exists in the persistent solver only.
+  const bool wss2 = p.wss == 2;
+  if (!wss2 && (force_single || !mode || strcmp(mode, "auto") == 0) && (force_single || n <= single_max) &&
+      n <= 8192) {
     int snt = kSingleDefaultNT;
     if (const char* v = getenv("SVM355_SMO_SINGLE_NT")) snt = atoi(v);
     if (snt != 256 && snt != 512 && snt != 1024) snt = kSingleDefaultNT;
@@ -1785,7 +1955,7 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
     }
     return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
   }
-  const bool want_persistent = !(mode && strcmp(mode, "graph") == 0);
+  const bool want_persistent = wss2 || !(mode && strcmp(mode, "graph") == 0);
   // XCD-local exchange (all workgroups on one XCD, records through its L2): SVM355_PSMO_XCD=1/0
   // forces it on/off; the default enables it up to kXcdDefaultMax points.
   bool xlocal = n <= kXcdDefaultMax;
@@ -1798,7 +1968,7 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
     for (int attempt = 0; attempt < 2; ++attempt) {
       SVMD_CHECK(hipMemsetAsync(slots, 0, slot_bytes, s));  // epochs restart at 1 every launch
       const int lrc = launch_persistent(s, NT, E, G, K, ldk, y, alpha, f, n, slots, st, p.C, p.eps, p.tau,
-                                        p.max_iter, dtrace, tcap, err, xlocal);
+                                        p.max_iter, dtrace, tcap, err, xlocal, wss2);
       if (lrc) return lrc;
       SVMD_CHECK(hipMemcpyAsync(&hst[2], st, sizeof(SmoState), hipMemcpyDeviceToHost, s));
       SVMD_CHECK(hipMemcpyAsync(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -1859,6 +2029,11 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
       }
     }
     return finish_smo(hst[2], r, trace, dtrace, tcap, t0);
+  }
+  if (wss2) {
+    set_error("svmd_smo: second-order selection (wss = 2) needs the persistent solver (n = %lld has no shape)",
+              (long long)n);
+    return SVM_ERR_ARG;
   }
 
   // Graph of kChunk iterations, cached per context for identical arguments.
@@ -1951,6 +2126,7 @@ int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y
   int G = 0, E = 0, NT = 0;
   bool ok = nclass < 1000 && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT, kXcdMaxG);
   ok = ok && ((NT == 256 && E <= 2) || (NT == 512 && E <= 4));
+  ok = ok && p.wss != 2;  // second-order selection: per-class persistent solves
   if (const char* v = getenv("SVM355_SMO_MULTI"); v && atoi(v) == 0) ok = false;
   if (batched) *batched = 0;
   if (ok) {

@@ -43,9 +43,13 @@ def _is_u8(X) -> bool:
 class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto"):
+                 scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto",
+                 wss: str = "first"):
+        if wss not in ("first", "second"):
+            raise ValueError("wss must be 'first' (the reference's selection) or 'second'")
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
-                                n_threads=n_threads if n_threads > 0 else default_threads())
+                                n_threads=n_threads if n_threads > 0 else default_threads(),
+                                wss=2 if wss == "second" else 1)
         self.device = device
         self.scale = scale
         self.zero_is_positive = zero_is_positive

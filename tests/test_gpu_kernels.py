@@ -132,6 +132,33 @@ def test_device_smo_bit_identical_to_oracle_on_same_gram(dev, D, mn_data, smo_mo
     assert r_gpu.b == r_cpu.b
 
 
+@pytest.mark.parametrize("n,xcd", [(900, "1"), (900, "0"), (9000, "1"), (20000, "1"), (20000, "0")],
+                         ids=["xcd-900", "device-900", "xcd-9k", "xcd-20k", "device-20k"])
+def test_device_wss2_bit_identical_to_oracle_on_same_gram(dev, D, monkeypatch, n, xcd):
+    """Opt-in second-order selection (svm_params.wss = 2): the persistent solver's second exchange
+    picks the same j as the CPU oracle on the same (device-built) Gram -- identical (i, j) traces,
+    alphas and b -- in fewer iterations than first order."""
+    monkeypatch.setenv("SVM355_PSMO_XCD", xcd)
+    tr = synthetic_mnist(n, seed=31)
+    Xd = D.upload_rows(tr.compact().X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    Kd, _ = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    K = Kd[:, :n].contiguous().cpu().numpy()
+    yd = torch.from_numpy(tr.y).to(dev)
+    p2 = SVMParams(n_threads=8, wss=2)
+    a_cpu, r_cpu, t_cpu = C.smo_train_gram(K, tr.y, p2, trace_cap=200000)
+    ad = torch.zeros(n, dtype=torch.float64, device=dev)
+    r_gpu, t_gpu = D.smo(Kd, yd, ad, p2, n=n, trace_cap=200000)
+    assert r_gpu.stop_reason == r_cpu.stop_reason == "converged"
+    assert r_gpu.iterations == r_cpu.iterations
+    np.testing.assert_array_equal(t_gpu, t_cpu)
+    np.testing.assert_array_equal(ad.cpu().numpy(), a_cpu)
+    assert r_gpu.b == r_cpu.b
+    a1 = torch.zeros(n, dtype=torch.float64, device=dev)
+    r1, _ = D.smo(Kd, yd, a1, SVMParams(), n=n)
+    assert r_gpu.iterations < r1.iterations
+
+
 def test_persistent_vs_graph_many_workgroups(dev, D, monkeypatch):
     """Many workgroups (G = 40 at n = 20000): both device paths bit-identical."""
     tr = synthetic_mnist(20000, seed=9)
