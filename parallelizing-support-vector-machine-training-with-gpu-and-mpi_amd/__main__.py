@@ -86,6 +86,8 @@ def _cascade(argv) -> int:
     ap.add_argument("--gamma", type=float, default=0.00125)
     ap.add_argument("--tau", type=float, default=1e-5)
     ap.add_argument("--max-rounds", type=int, default=50)
+    ap.add_argument("--wss", choices=["first", "second"], default="first",
+                    help="working-set selection: first order (the reference) or the opt-in second-order choice")
     ap.add_argument("--cpu", action="store_true", help="CPU thread-ranks on the native oracle instead of GPUs")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU; thread-ranks of this process)")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
@@ -102,7 +104,8 @@ def _cascade(argv) -> int:
     if a.native:
         args = ["--topology", a.topology, "--gpus", str(max(1, a.gpus)), "--transport", a.transport,
                 "--max-rounds", str(a.max_rounds), "--C", str(a.C), "--gamma", str(a.gamma), "--tau", str(a.tau),
-                "--positive-label", str(a.positive_label), "--seed", str(a.seed), "--comm-timeout", str(a.comm_timeout)]
+                "--positive-label", str(a.positive_label), "--seed", str(a.seed), "--comm-timeout", str(a.comm_timeout),
+                "--wss", a.wss]
         if a.synthetic:
             args += ["--synthetic", a.synthetic]
         else:
@@ -130,7 +133,8 @@ def _cascade(argv) -> int:
     if tr.n == 0:
         print("Error: No data read from file.", file=sys.stderr)
         return 1
-    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // max(1, a.gpus)))
+    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // max(1, a.gpus)),
+                       wss=2 if a.wss == "second" else 1)
     model = CascadeSVM(params, topology=a.topology, max_rounds=a.max_rounds, verbose=a.verbose,
                        checkpoint_dir=a.checkpoint_dir, resume=a.resume, comm_timeout_s=a.comm_timeout)
     device = "cpu" if a.cpu else "cuda"

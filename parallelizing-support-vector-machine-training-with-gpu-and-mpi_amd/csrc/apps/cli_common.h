@@ -11,6 +11,8 @@
 //   --json F         machine-readable summary
 //   --gram auto|fp64|int  (svm_gpu) RBF Gram path: exact-integer int8 MFMA for pixel data, or FP64 MFMA
 //   --warmup W       (svm_gpu) untimed training runs first (steady-state timings)
+//   --wss first|second  working-set selection: first order (the reference, default) or the opt-in
+//                    second-order choice of the second index (Fan, Chen & Lin 2005)
 #pragma once
 #include <chrono>
 #include <cstdio>
@@ -42,7 +44,7 @@ inline void usage(const char* prog) {
           "usage: %s [--dataset P | --train F --test F | --synthetic N[,M] [--seed S]] [--n-limit N]\n"
           "          [--C 10] [--gamma 0.00125] [--tau 1e-5] [--eps 1e-12] [--sv-tol 1e-8]\n"
           "          [--max-iter 100000] [--positive-label 1] [--threads T] [--model-dir D] [--json F]\n"
-          "          [--gram auto|fp64|int] [--warmup W]\n",
+          "          [--gram auto|fp64|int] [--warmup W] [--wss first|second]\n",
           prog);
 }
 
@@ -84,6 +86,13 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
     else if (a == "--gram") {
       const std::string g = next("--gram");
       o.gram_mode = g == "fp64" ? 1 : g == "int" ? 2 : 0;
+    } else if (a == "--wss") {
+      const std::string w = next("--wss");
+      if (w != "first" && w != "second") {
+        fprintf(stderr, "--wss must be first or second\n");
+        return false;
+      }
+      o.p.wss = w == "second" ? 2 : 1;
     }
     else if (a == "-h" || a == "--help") {
       usage(argv[0]);

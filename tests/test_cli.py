@@ -35,6 +35,19 @@ def test_cli_serial_reference_lines(tmp_path):
         assert (tmp_path / "m" / f).exists()
 
 
+def test_cli_serial_second_order_selection(tmp_path):
+    """--wss second: the opt-in second-order selection reaches the same model in fewer iterations."""
+    runs = {}
+    for wss in ("first", "second"):
+        js = tmp_path / f"{wss}.json"
+        _run(["serial", "--synthetic", "600,200", "--wss", wss, "--json", str(js)], tmp_path)
+        runs[wss] = json.loads(js.read_text())
+    f, s = runs["first"], runs["second"]
+    assert s["stop_reason"] == f["stop_reason"] == "converged"
+    assert s["iterations"] < f["iterations"]
+    assert s["n_sv"] == f["n_sv"] and s["accuracy"] == f["accuracy"]
+
+
 @pytest.mark.parametrize("topology", ["star", "tree"])
 def test_cli_cascade_single_rank_cpu(tmp_path, topology):
     js = tmp_path / "c.json"
