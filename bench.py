@@ -94,6 +94,8 @@ def main(argv=None):
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
     ap.add_argument("--baseline-1gpu", type=int, default=3,
                     help="N > 1: single-GPU fits timed after the cascade for speedup_vs_1gpu (0 = skip)")
+    ap.add_argument("--wss", choices=["first", "second"], default="first",
+                    help="working-set selection: first order (the reference; the headline) or the opt-in second-order")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
 
@@ -129,7 +131,7 @@ def main(argv=None):
 
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))  # bootstrap store + timing max
 
-    params = SVMParams()
+    params = SVMParams(wss=2 if a.wss == "second" else 1)
     te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
     if multiproc:
         lo, hi = partition_bounds(a.n, world_env, rank)
@@ -164,7 +166,7 @@ def main(argv=None):
     def step():
         nonlocal model
         if not use_cascade:
-            model = SVC(device=str(dev)).fit(tr.X, tr.y)
+            model = SVC(device=str(dev), wss=a.wss).fit(tr.X, tr.y)
         elif multiproc:
             model = CascadeSVM(params, topology=a.topology).fit_rank(crank, tr.X, tr.y, np.arange(lo, hi), a.n)
         else:
@@ -251,12 +253,12 @@ def main(argv=None):
             if rank == 0:
                 full = tr if not multiproc else synthetic_mnist(a.n, seed=a.seed)
                 full = full.compact() if a.input == "u8" else full
-                SVC(device=str(dev)).fit(full.X, full.y)  # warm
+                SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)  # warm
                 ts = []
                 for _ in range(a.baseline_1gpu):
                     torch.cuda.synchronize(dev)
                     tb = time.perf_counter()
-                    SVC(device=str(dev)).fit(full.X, full.y)
+                    SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
                     torch.cuda.synchronize(dev)
                     ts.append(time.perf_counter() - tb)
                 one = float(np.median(ts))
@@ -279,7 +281,7 @@ def main(argv=None):
             "dtype": "fp64",
             "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
             "config": {
-                "model": "RBF SVM, first-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
+                "model": f"RBF SVM, {a.wss}-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,
                 "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{a.gpus}",
