@@ -438,10 +438,6 @@ SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int
                             int32_t* gram_used, int64_t* trace_host, int64_t trace_cap) {
   SVMD_CTX(h);
   const svm_params q = resolve(p);
-  if (q.wss == 2) {
-    set_error("svmd_train_rows: second-order selection (wss = 2) is implemented for the resident Gram only");
-    return SVM_ERR_ARG;
-  }
   int rc = ctx->begin();
   if (rc) return rc;
   QuantPlan P;

@@ -487,6 +487,12 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
   if (verbose) (void)hipStreamSynchronize(s);
   const double t_prep = ms_since(t0);
   rc = run_smo_rc_persistent(ctx, q, int_ok, cache, ldc, C, y, alpha, f, n, p, r, trace, tcap);
+  if (rc == kRcNotApplicable && p.wss == 2) {
+    release();
+    set_error("row cache: second-order selection (wss = 2) needs the persistent row-cache solver (exact-integer "
+              "rows, n <= 1,048,576)");
+    return SVM_ERR_ARG;
+  }
   if (rc != kRcNotApplicable) {
     if (verbose)
       fprintf(stderr, "[rowcache n=%lld] cache %lld slots (%.1f GB, slab %.1f GB) | prep (alloc, quantise, interleave) "

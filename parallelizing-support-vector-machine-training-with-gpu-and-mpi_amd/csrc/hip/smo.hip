@@ -435,10 +435,25 @@ struct PersistShared {
 // ---- Row sources of the persistent solver.  choose() runs on one lane of every workgroup once the
 // pair is known (before the barrier that publishes it); fetch() then gives every thread the rows'
 // values for its elements plus K11 / K22 / K12, issuing all loads in one memory round trip.
+// Second-order selection reads the pair's rows one at a time (row i_high before the second exchange,
+// row j after it): choose_one() (lane 0 of wave 0, `keep` = a slot that must survive) and fetch_one()
+// (every thread: its elements of the row, and K(row, row)).
 struct ResidentRows {  // the resident n x n Gram
   const double* __restrict__ K;
   int64_t ldk;
   __device__ __forceinline__ void choose(PersistShared&, uint32_t, uint32_t) const {}
+  __device__ __forceinline__ void choose_one(PersistShared&, int, uint32_t, int64_t) const {}
+  template <int NT, int E>
+  __device__ __forceinline__ void fetch_one(const PersistShared&, int, int64_t row, int64_t lo, int t,
+                                            int64_t hi_end, double (&k)[E], double& diag) const {
+    const double* R = K + row * ldk;
+    diag = R[row];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = lo + t + NT * e;
+      k[e] = i < hi_end ? R[i] : 0.0;
+    }
+  }
   template <int NT, int E>
   __device__ __forceinline__ void fetch(const PersistShared&, int64_t ih, int64_t il, int64_t lo, int t,
                                         int64_t hi_end, double (&kh)[E], double (&kl)[E], double& K11,
@@ -494,6 +509,35 @@ struct CachedRows {
     mru[set] = uint8_t(way);
     *miss = 1;
     return s0 + way;
+  }
+  __device__ __forceinline__ void choose_one(PersistShared& sh, int which, uint32_t row, int64_t keep) const {
+    int32_t m = 0;
+    sh.rslot[which] = lookup(row, keep, &m);
+    sh.rmiss[which] = m;
+  }
+  template <int NT, int E>
+  __device__ __forceinline__ void fetch_one(const PersistShared& sh, int which, int64_t row, int64_t lo, int t,
+                                            int64_t hi_end, double (&k)[E], double& diag) const {
+    diag = 1.0;  // kval(a, a)
+    double* Cr = cache + sh.rslot[which] * ldc;
+    if (sh.rmiss[which]) {
+      if constexpr (INT) {
+        constexpr int EG = E < 4 ? E : 4;
+#pragma unroll 1
+        for (int e0 = 0; e0 < E; e0 += EG) fill<NT, EG, true, false>(lo + int64_t(NT) * e0, row, row, t, hi_end, Cr, Cr);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int64_t i = lo + t + NT * e;
+          if (i < hi_end) Cr[i] = kval<false>(q, row, i, neg_gamma);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {  // this thread's own stores, or a filled slot from an earlier epoch
+      const int64_t i = lo + t + NT * e;
+      k[e] = i < hi_end ? Cr[i] : 0.0;
+    }
   }
   __device__ __forceinline__ void choose(PersistShared& sh, uint32_t ih, uint32_t il) const {
     int32_t mh = 0, ml = 0;
@@ -984,9 +1028,14 @@ __device__ __forceinline__ uint32_t persist_solve(
         sh.gv[1] = wgx.v;
         sh.gi[1] = wgx.i;
         sh.ga[1] = awgx;
-        // a pair that will be updated: the row source prepares its rows (every workgroup alike)
-        if (!any_to && wgm.i != kSentinel && wgx.i != kSentinel && !(wgx.v <= wgm.v + 2.0 * tau))
-          rows.choose(sh, wgm.i, wgx.i);
+        // a pair that will be updated: the row source prepares its rows (every workgroup alike;
+        // second-order selection: row i_high now, the second row after the second exchange)
+        if (!any_to && wgm.i != kSentinel && wgx.i != kSentinel && !(wgx.v <= wgm.v + 2.0 * tau)) {
+          if constexpr (WSS2)
+            rows.choose_one(sh, 0, wgm.i, -1);
+          else
+            rows.choose(sh, wgm.i, wgx.i);
+        }
         if (any_to) {
           sh.timeout = 1;
           __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1019,15 +1068,8 @@ __device__ __forceinline__ uint32_t persist_solve(
     int32_t yh, yl;
     double bl_upd = bl, al = sh.ga[1];  // the second index's f and alpha in the update
     if constexpr (WSS2) {
-      static_assert(RPL == 1, "second-order selection: one record per sweep lane");
       // ---- 4b. row i_high, the local second-order candidate, a second exchange for j
-      const double* Kh = rows.K + ih * rows.ldk;
-      K11 = Kh[ih];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int64_t i = lo + t + NT * e;
-        kh[e] = i < hi_end ? Kh[i] : 0.0;
-      }
+      rows.template fetch_one<NT, E>(sh, 0, ih, lo, t, hi_end, kh, K11);
       VI cm{inf, kSentinel};
       double ca = 0.0, cf = 0.0, ck = 0.0;
 #pragma unroll
@@ -1100,16 +1142,21 @@ __device__ __forceinline__ uint32_t persist_solve(
         VI gm{inf, kSentinel};
         double ga = 0.0, gf = 0.0, gk = 0.0;
         bool timed_out = false;
-        if (lane < G) {
-          const unsigned long long* r = rec2 + size_t(lane) * kRecStride;
-          uint32_t v[kGranules];
+        if (lane < G) {  // lane L: records L, L + 64, ... (as in the first exchange)
+          uint32_t v[RPL][kGranules];
           for (int64_t spins = 0;; ++spins) {
             bool ok = true;
 #pragma unroll
-            for (int k = 0; k < kGranules; ++k) {
-              const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              v[k] = uint32_t(x);
-              ok &= uint32_t(x >> 32) == epoch;
+            for (int rr = 0; rr < RPL; ++rr) {
+              if (RPL == 1 || lane + 64 * rr < G) {
+                const unsigned long long* r = rec2 + size_t(lane + 64 * rr) * kRecStride;
+#pragma unroll
+                for (int k = 0; k < kGranules; ++k) {
+                  const unsigned long long x = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  v[rr][k] = uint32_t(x);
+                  ok &= uint32_t(x >> 32) == epoch;
+                }
+              }
             }
             if (ok) break;
             if (spins > spin_limit) {
@@ -1119,10 +1166,18 @@ __device__ __forceinline__ uint32_t persist_solve(
             __builtin_amdgcn_s_sleep(1);
           }
           if (!timed_out) {
-            gm = VI{mk64(v[0], v[1]), v[2]};
-            ga = mk64(v[3], v[4]);
-            gf = mk64(v[5], v[6]);
-            gk = mk64(v[8], v[9]);
+#pragma unroll
+            for (int rr = 0; rr < RPL; ++rr) {
+              if (RPL == 1 || lane + 64 * rr < G) {
+                const VI c{mk64(v[rr][0], v[rr][1]), v[rr][2]};
+                if (rr == 0 || beats<true>(c, gm)) {
+                  gm = c;
+                  ga = mk64(v[rr][3], v[rr][4]);
+                  gf = mk64(v[rr][5], v[rr][6]);
+                  gk = mk64(v[rr][8], v[rr][9]);
+                }
+              }
+            }
           }
         }
         const bool any_to2 = __any(timed_out);
@@ -1133,6 +1188,7 @@ __device__ __forceinline__ uint32_t persist_solve(
           sh.ga[1] = wga;
           sh.gv[1] = wgf;
           sh.k12 = wgk;
+          if (!any_to2 && wgm.i != kSentinel) rows.choose_one(sh, 1, wgm.i, sh.rslot[0]);  // keep row i_high
           if (any_to2) {
             sh.timeout = 1;
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1148,13 +1204,7 @@ __device__ __forceinline__ uint32_t persist_solve(
       bl_upd = sh.gv[1];
       al = sh.ga[1];
       K12 = sh.k12;
-      const double* Kl = rows.K + il * rows.ldk;
-      K22 = Kl[il];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int64_t i = lo + t + NT * e;
-        kl[e] = i < hi_end ? Kl[i] : 0.0;
-      }
+      rows.template fetch_one<NT, E>(sh, 1, il, lo, t, hi_end, kl, K22);
       yh = y[ih];
       yl = y[il];
     } else {
@@ -1297,7 +1347,7 @@ __global__ __launch_bounds__(NT) void smo_persistent_kernel(
 // Persistent SMO on the HBM row cache (n beyond the resident Gram; driven by rowcache.hip's
 // run_smo_rowcache): device-wide exchange over G co-resident workgroups, CachedRows as the row
 // source with its directory (nslots int32 tags + nslots / 2 MRU bytes) in dynamic LDS.
-template <int NT, int E, bool INT, bool STAMP, int RPL>
+template <int NT, int E, bool INT, bool STAMP, int RPL, bool WSS2 = false>
 __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
     QRows q, double* __restrict__ cache, int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* __restrict__ y,
     double* __restrict__ alpha, double* __restrict__ f, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
@@ -1311,7 +1361,7 @@ __global__ __launch_bounds__(NT) void smo_rc_persistent_kernel(
   for (int64_t k = threadIdx.x; k < nslots / 2; k += NT) mru[k] = 0;
   __syncthreads();
   const CachedRows<INT> rows{q, cache, ldc, tags, mru, nslots / 2, neg_gamma};
-  persist_solve<NT, E, STAMP, false, CachedRows<INT>, RPL>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f,
+  persist_solve<NT, E, STAMP, false, CachedRows<INT>, RPL, WSS2>(sh, int(gridDim.x), int(blockIdx.x), 0, rows, y, alpha, f,
                                                           n, slice, slots, st, C, eps, tau, max_iter, trace, trace_cap,
                                                           err, spin_limit, stamps);
 }
@@ -1727,12 +1777,12 @@ int finish_smo(const SmoState& fin, svm_result* r, int64_t* trace, const int64_t
 }  // namespace
 
 namespace {
-template <int E, bool INT, bool STAMP, int RPL>
+template <int E, bool INT, bool STAMP, int RPL, bool WSS2 = false>
 void launch_rc_e(hipStream_t s, int G, size_t lds, const QRows& q, double* cache, int64_t ldc, int64_t nslots,
                  double neg_gamma, const int32_t* y, double* alpha, double* f, int64_t n, unsigned long long* slots,
                  SmoState* st, const svm_params& p, int64_t* trace, int64_t tcap, unsigned* err) {
-  allow_lds(smo_rc_persistent_kernel<512, E, INT, STAMP, RPL>, lds);
-  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT, STAMP, RPL>), dim3(G), dim3(512), lds, s, q, cache, ldc,
+  allow_lds(smo_rc_persistent_kernel<512, E, INT, STAMP, RPL, WSS2>, lds);
+  hipLaunchKernelGGL((smo_rc_persistent_kernel<512, E, INT, STAMP, RPL, WSS2>), dim3(G), dim3(512), lds, s, q, cache, ldc,
                      nslots, neg_gamma, y, alpha, f, n, int64_t(512) * E, slots, st, p.C, p.eps, p.tau, p.max_iter,
                      trace, tcap, err, int64_t(1) << 24, reinterpret_cast<unsigned long long*>(err) + 8);
 }
@@ -1741,7 +1791,10 @@ void launch_rc_variant(bool int_rows, bool stamp, hipStream_t s, int G, size_t l
                        int64_t ldc, int64_t nslots, double neg_gamma, const int32_t* y, double* alpha, double* f,
                        int64_t n, unsigned long long* slots, SmoState* st, const svm_params& p, int64_t* trace,
                        int64_t tcap, unsigned* err) {
-  if (int_rows && stamp)
+  if (int_rows && p.wss == 2)  // opt-in second-order selection (exact-integer rows)
+    launch_rc_e<E, true, false, RPL, true>(s, G, lds, q, cache, ldc, nslots, neg_gamma, y, alpha, f, n, slots, st, p,
+                                           trace, tcap, err);
+  else if (int_rows && stamp)
     launch_rc_e<E, true, true, RPL>(s, G, lds, q, cache, ldc, nslots, neg_gamma, y, alpha, f, n, slots, st, p, trace,
                                     tcap, err);
   else if (int_rows)
@@ -1763,6 +1816,7 @@ int run_smo_rc_persistent(DeviceCtx* ctx, const QRows& q, bool int_rows, double*
   if (const char* m = getenv("SVM355_RC_SMO"); m && !strcmp(m, "graph")) return kRcNotApplicable;
   if (n <= 0 || n >= int64_t(kSentinel)) return kRcNotApplicable;
   if (int_rows && q.kq > 32 * 128) return kRcNotApplicable;  // CachedRows::k12: two k-steps per lane
+  if (p.wss == 2 && !int_rows) return kRcNotApplicable;       // second order: exact-integer rows only
   // Shape: up to 8 register-resident points per thread (E = 16 needs more than 256 VGPRs and
   // spills) and one 512-thread workgroup per CU, all co-resident.  Teams of up to 64 workgroups
   // (one record per sweep lane) with E <= 4, then 128 and 256 (two / four records per lane, capped

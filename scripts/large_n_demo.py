@@ -17,13 +17,15 @@ tr = synthetic_mnist(n, seed=2024)
 te = synthetic_mnist(10000, seed=2024, offset=n)
 print(f"data: {n} x 784 generated in {time.perf_counter() - t0:.1f} s; full Gram would need "
       f"{n * n * 8 / 1e9:.0f} GB, fits: {D.gram_fits(n, 'cuda:0')}", flush=True)
-for rep in range(2):
+Xu8 = tr.compact().X  # uint8 pixels, widened on the device
+wss_list = (sys.argv[2] if len(sys.argv) > 2 else "first").split(",")  # e.g. "first,second"
+for wss, rep in [(w, r) for w in wss_list for r in range(2)]:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    m = SVC(device="cuda:0").fit(tr.X, tr.y)
+    m = SVC(device="cuda:0", wss=wss).fit(Xu8, tr.y)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"fit {dt * 1e3:.1f} ms: kcache={m.timings_['kcache']} gram={m.timings_['gram_path']} "
+    print(f"[{wss}] fit {dt * 1e3:.1f} ms: kcache={m.timings_['kcache']} gram={m.timings_['gram_path']} "
           f"iterations={m.n_iter_} n_sv={len(m.support_)} b={m.b_:.12f} stop={m.stop_reason_} timings={m.timings_}",
           flush=True)
 print(f"test accuracy {m.score(te.X, te.y):.4f}", flush=True)

@@ -520,6 +520,40 @@ def test_row_cache_wide_teams_follow_the_same_trajectory(dev, D, monkeypatch):
         np.testing.assert_array_equal(a, a0)
 
 
+@pytest.mark.parametrize("n,cache_rows", [(2500, 6), (2500, 64), (40000, 512)])
+def test_row_cache_wss2_bit_identical_to_resident_gram(dev, D, n, cache_rows):
+    """Opt-in second-order selection on the persistent row-cache solver: row i_high is looked up before
+    the second exchange and row j after it, with i_high's slot kept (a 6-row cache evicts every
+    iteration) -- the same (i, j) trace, alphas and b as second order on the resident Gram."""
+    tr = synthetic_mnist(n, seed=25)
+    Xd = D.upload_rows(tr.compact().X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    yd = torch.from_numpy(tr.y).to(dev)
+    K, path = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    assert path == "int8-exact"
+    p2 = SVMParams(wss=2)
+    a_full = torch.zeros(n, dtype=torch.float64, device=dev)
+    r_full, t_full = D.smo(K, yd, a_full, p2, n=n, trace_cap=200000)
+    del K
+    ldc = (n + 1) // 2 * 2
+    a_rows = torch.zeros(n, dtype=torch.float64, device=dev)
+    r_rows, info = D.train(Xd, sqn, yd, a_rows, p2, mn=mn, mx=mx, kcache="rows", cache_bytes=cache_rows * ldc * 8,
+                           trace_cap=200000)
+    assert r_rows.stop_reason == r_full.stop_reason == "converged"
+    assert r_rows.iterations == r_full.iterations and r_rows.b == r_full.b
+    np.testing.assert_array_equal(info["trace"], t_full)
+    np.testing.assert_array_equal(a_rows.cpu().numpy(), a_full.cpu().numpy())
+
+
+def test_row_cache_wss2_needs_integer_rows(dev, D):
+    """Second order on real-valued rows (FP64 on-demand rows, graph-replayed solver) is refused loudly."""
+    rng = np.random.default_rng(6)
+    X = rng.normal(size=(300, 20))
+    y = np.where(X[:, 0] > 0, 1, -1).astype(np.int32)
+    with pytest.raises(Exception, match="second-order"):
+        SVC(device="cuda:0", kcache="rows", wss="second").fit(X, y)
+
+
 def test_row_cache_warm_start_bit_identical(dev, D):
     n = 1800
     tr = synthetic_mnist(n, seed=22)
