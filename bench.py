@@ -96,6 +96,9 @@ def main(argv=None):
                     help="N > 1: single-GPU fits timed after the cascade for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference; the headline) or the opt-in second-order")
+    ap.add_argument("--comm-timeout", type=float, default=120.0,
+                    help="N > 1: seconds any rank waits on an exchange before every rank aborts its communicator "
+                         "(a fit takes well under a second; a dead peer must not hang the run)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
 
@@ -147,11 +150,11 @@ def main(argv=None):
         if multiproc:
             from svm355.parallel.rccl import RcclRank
 
-            crank = RcclRank.from_torch_dist(dev_index)
+            crank = RcclRank.from_torch_dist(dev_index, a.comm_timeout)
         else:
             from svm355.parallel.rccl import DeviceGroup
 
-            group = DeviceGroup(a.gpus, a.transport)
+            group = DeviceGroup(a.gpus, a.transport, a.comm_timeout)
 
     def barrier_sync():
         torch.cuda.synchronize(dev)
@@ -168,9 +171,11 @@ def main(argv=None):
         if not use_cascade:
             model = SVC(device=str(dev), wss=a.wss).fit(tr.X, tr.y)
         elif multiproc:
-            model = CascadeSVM(params, topology=a.topology).fit_rank(crank, tr.X, tr.y, np.arange(lo, hi), a.n)
+            model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit_rank(
+                crank, tr.X, tr.y, np.arange(lo, hi), a.n)
         else:
-            model = CascadeSVM(params, topology=a.topology).fit(tr.X, tr.y, world=a.gpus, device="cuda", group=group)
+            model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit(
+                tr.X, tr.y, world=a.gpus, device="cuda", group=group)
 
     warm_ms = []
     for _ in range(a.warmup):
