@@ -48,35 +48,6 @@ REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
 METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
 
 
-def critical_path(solves, topology):
-    """Per round: the slowest rank's local solve (tree: slowest rank of every layer) + rank 0's merge.
-    Solve times are the solo device times when the run measured them (SVM355_CASCADE_SERIAL_SOLVES=1:
-    ranks sharing one GPU take turns, so each solve is timed as on a GPU of its own), else wall times.
-    Returns ([[round, local_max_ms, merge_ms, local_max_iterations, merge_iterations]], total ms)."""
-    solves = [dict(s, ms=s["solo_ms"]) if s.get("solo_ms", -1.0) >= 0 else s for s in solves]
-    rounds = sorted({s["round"] for s in solves})
-    out, tot = [], 0.0
-    for r in rounds:
-        rs = [s for s in solves if s["round"] == r]
-        if topology == "star":
-            loc = [s for s in rs if s["layer"] == "local"]
-            mer = [s for s in rs if s["layer"] == "merge"]
-            lm = max((s["ms"] for s in loc), default=0.0)
-            li = max((s["iterations"] for s in loc), default=0)
-            mm = sum(s["ms"] for s in mer)
-            mi = sum(s["iterations"] for s in mer)
-        else:
-            layers = sorted({s["layer"] for s in rs}, key=lambda x: int(x[5:]))
-            first = [s for s in rs if s["layer"] == layers[0]] if layers else []
-            lm = max((s["ms"] for s in first), default=0.0)
-            li = max((s["iterations"] for s in first), default=0)
-            mm = sum(max(s["ms"] for s in rs if s["layer"] == L) for L in layers[1:])
-            mi = sum(max(s["iterations"] for s in rs if s["layer"] == L) for L in layers[1:])
-        out.append([r, round(lm, 3), round(mm, 3), li, mi])
-        tot += lm + mm
-    return out, round(tot, 3)
-
-
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,7 +92,7 @@ def main(argv=None):
         return 2
 
     from svm355 import SVC, SVMParams
-    from svm355.parallel.cascade import CascadeSVM, partition_bounds
+    from svm355.parallel.cascade import CascadeSVM, critical_path, partition_bounds
     from svm355.utils.data import synthetic_mnist
 
     dev_index = local_rank if multiproc else 0

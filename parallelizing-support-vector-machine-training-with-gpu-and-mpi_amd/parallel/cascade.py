@@ -172,3 +172,34 @@ def partition_bounds(n_total: int, world: int, rank: int):
     chunk = (n_total + world - 1) // world
     lo = min(n_total, rank * chunk)
     return lo, min(n_total, lo + chunk)
+
+
+def critical_path(solves, topology: str):
+    """Per round: the slowest rank's local solve (tree: slowest rank of the first layer) + rank 0's
+    merge (tree: slowest rank of every later layer), i.e. the solve time of a run with one GPU per
+    rank, exchanges excluded.  Solve times are the solo device times when the run measured them
+    (SVM355_CASCADE_SERIAL_SOLVES=1: ranks sharing one GPU take turns, so each solve is timed as on a
+    GPU of its own), else wall times.  ``solves`` = ``CascadeResult.solves`` of every rank.
+    Returns ([[round, local_max_ms, merge_ms, local_max_iterations, merge_iterations]], total ms)."""
+    solves = [dict(s, ms=s["solo_ms"]) if s.get("solo_ms", -1.0) >= 0 else s for s in solves]
+    out, tot = [], 0.0
+    for r in sorted({s["round"] for s in solves}):
+        rs = [s for s in solves if s["round"] == r]
+        if topology == "star":
+            loc = [s for s in rs if s["layer"] == "local"]
+            mer = [s for s in rs if s["layer"] == "merge"]
+            lm = max((s["ms"] for s in loc), default=0.0)
+            li = max((s["iterations"] for s in loc), default=0)
+            mm = sum(s["ms"] for s in mer)
+            mi = sum(s["iterations"] for s in mer)
+        else:
+            layers = sorted({s["layer"] for s in rs}, key=lambda x: int(x[5:]))
+            first = [s for s in rs if s["layer"] == layers[0]] if layers else []
+            lm = max((s["ms"] for s in first), default=0.0)
+            li = max((s["iterations"] for s in first), default=0)
+            mm = sum(max(s["ms"] for s in rs if s["layer"] == L) for L in layers[1:])
+            mi = sum(max(s["iterations"] for s in rs if s["layer"] == L) for L in layers[1:])
+        out.append([r, round(lm, 3), round(mm, 3), li, mi])
+        tot += lm + mm
+    return out, round(tot, 3)
+

@@ -10,7 +10,7 @@ import pytest
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import bench  # noqa: E402
 from svm355 import SVMParams  # noqa: E402
-from svm355.parallel.cascade import CascadeSVM  # noqa: E402
+from svm355.parallel.cascade import CascadeSVM, critical_path  # noqa: E402
 from svm355.utils.data import synthetic_mnist  # noqa: E402
 
 
@@ -21,7 +21,7 @@ def _s(rank, rnd, layer, ms, it, solo=-1.0):
 def test_star_critical_path_takes_slowest_local_plus_merge():
     solves = [_s(0, 1, "local", 5.0, 100), _s(1, 1, "local", 7.0, 90), _s(0, 1, "merge", 3.0, 40),
               _s(0, 2, "local", 1.0, 10), _s(1, 2, "local", 2.0, 20), _s(0, 2, "merge", 0.5, 5)]
-    rows, tot = bench.critical_path(solves, "star")
+    rows, tot = critical_path(solves, "star")
     assert rows == [[1, 7.0, 3.0, 100, 40], [2, 2.0, 0.5, 20, 5]]
     assert tot == pytest.approx(12.5)
 
@@ -30,7 +30,7 @@ def test_tree_critical_path_takes_slowest_rank_of_every_layer():
     solves = [_s(0, 1, "layer1", 4.0, 50), _s(1, 1, "layer1", 6.0, 70), _s(2, 1, "layer1", 5.0, 60),
               _s(3, 1, "layer1", 1.0, 10), _s(0, 1, "layer2", 2.0, 30), _s(2, 1, "layer2", 3.0, 35),
               _s(0, 1, "layer4", 1.5, 20)]
-    rows, tot = bench.critical_path(solves, "tree")
+    rows, tot = critical_path(solves, "tree")
     assert rows == [[1, 6.0, 4.5, 70, 55]]
     assert tot == pytest.approx(10.5)
 
@@ -40,7 +40,7 @@ def test_critical_path_prefers_solo_device_times():
     device; the wall time of ranks sharing one GPU would overstate the P-GPU critical path."""
     solves = [_s(0, 1, "local", 50.0, 100, solo=5.0), _s(1, 1, "local", 70.0, 90, solo=7.5),
               _s(0, 1, "merge", 30.0, 40, solo=3.0)]
-    rows, tot = bench.critical_path(solves, "star")
+    rows, tot = critical_path(solves, "star")
     assert rows == [[1, 7.5, 3.0, 100, 40]]
     assert tot == pytest.approx(10.5)
 
@@ -59,5 +59,5 @@ def test_cpu_solve_log_has_the_fields_the_critical_path_reads():
     for s in r.solves:
         assert {"rank", "round", "layer", "ms", "iterations", "skipped", "row_cache", "solo_ms"} <= set(s)
         assert s["row_cache"] is False and s["solo_ms"] < 0  # CPU backend: no row cache, no solo timing
-    rows, tot = bench.critical_path(r.solves, "star")
+    rows, tot = critical_path(r.solves, "star")
     assert len(rows) == r.rounds and tot > 0

@@ -88,3 +88,21 @@ def test_cli_multiclass_two_ranks_gloo(tmp_path):
     assert "[rank 0] one-vs-rest over 10 classes on 2 rank(s)" in out
     s = json.loads(js.read_text())
     assert s["world"] == 2 and all(r == "converged" for r in s["stop_reasons"]) and s["accuracy"] > 0.8
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_cli_scale_sweeps_rank_counts(tmp_path, topology):
+    """scale = mpi_svm2.sh / mpi_svm3.sh over P: one row per rank count (the tree skips P = 3), the
+    single-device baseline, and the same converged model at every P (CPU thread-ranks)."""
+    js = tmp_path / "scale.json"
+    out = _run(["scale", "--cpu", "--synthetic", "500,200", "--ranks", "1,2,3,4", "--topology", topology,
+                "--repeats", "1", "--warmup", "0", "--json", str(js)], tmp_path)
+    s = json.loads(js.read_text())
+    assert s["device"] == "cpu" and s["single_n_sv"] > 0
+    rows = s["rows"]
+    assert [r["P"] for r in rows] == ([1, 2, 3, 4] if topology == "star" else [1, 2, 4])
+    for r in rows:
+        assert r["converged"] and r["rounds"] >= 1 and r["n_sv"] > 0
+        assert r["accuracy"] > 0.9
+        assert r["critical_path_solve_ms"] > 0 and r["efficiency_vs_single"] > 0
+    assert "efficiency" in out and "single CPU oracle" in out
