@@ -186,6 +186,8 @@ _HIP_SIGS = {
                                   c_int64, c_int32, POINTER(c_int32)]),
     "svmd_decision": (c_int32, [c_void_p, _P, _P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, c_int64,
                                 c_double, c_double, _P]),
+    "svmd_decision_int": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int64, c_double, _P,
+                                    POINTER(c_int32)]),
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
     "svmd_count_correct": (c_int32, [c_void_p, _P, _P, c_int64, c_int32, POINTER(c_int64)]),
     "svmd_cascade_group_create": (c_void_p, [c_int32, c_char_p, c_double]),

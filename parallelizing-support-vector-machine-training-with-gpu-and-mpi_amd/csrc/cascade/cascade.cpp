@@ -292,7 +292,8 @@ class Rank {
     bool skipped_now = false;
     {
       auto tm = timer(kPhSolve);
-      if (skippable && warm_rows > 0 && B_.warm_start_converged(S, warm_rows, d_, cfg_.params)) {
+      if (skippable && warm_rows > 0 &&
+          B_.warm_start_converged(S, warm_rows, d_, cfg_.params, mn_h.data(), mx_h.data())) {
         st.iterations = 1;  // what the solve reports when it stops at its first selection
         st.stop = SVM_STOP_CONVERGED;
         st.b = 0.0;         // not part of the model (skippable)

@@ -162,7 +162,10 @@ class Backend {
   // test b_low <= b_high + 2 tau already -- i.e. the solve would end at its first selection without
   // an update -- checked from a cross-kernel K(S, S[0:nz]) only, before any Gram work.  The margin
   // covers the check's own rounding, so a true answer never changes a result.  Default: never.
-  virtual bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) { return false; }
+  virtual bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h,
+                                    const double* mx_h) {
+    return false;
+  }
   // Device time of the solve work since the last call, measured with the device to this rank alone
   // (HIP backend with SVM355_CASCADE_SERIAL_SOLVES=1: a one-GPU rehearsal of P ranks runs their
   // solves one at a time, so each is timed as it would run on its own GPU); < 0 when not measured.

@@ -516,6 +516,34 @@ SVM_API int svmd_decision(void* h, const double* Xs_d, const double* ns_d, const
   return ctx->end();
 }
 
+SVM_API int svmd_decision_int(void* h, const double* X_d, int64_t k, int64_t ldx, int64_t d, const double* mn_h,
+                              const double* mx_h, const double* coef_d, int64_t nz, double gamma, double* out_d,
+                              int32_t* used) {
+  SVMD_CTX(h);
+  if (used) *used = 0;
+  if (k <= 0 || nz <= 0 || nz > k || !used) return SVM_OK;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P)) return SVM_OK;
+  int rc = ctx->begin();
+  if (rc) return rc;
+  TraceRange tr("svm355:decision_int");
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const int64_t ldk = (nz + 1) / 2 * 2;
+  const size_t block = al(size_t(k) * size_t(ldk) * 8);
+  rc = ctx->ensure_ws(block + igram_workspace(k, P));
+  if (rc) return rc;
+  double* Kb = static_cast<double*>(ctx->ws);
+  bool ok = false;
+  rc = run_igram_block(ctx->stream, X_d, k, ldx, nz, P, gamma, Kb, ldk, static_cast<char*>(ctx->ws) + block, &ok);
+  if (rc) return rc;
+  if (ok) {
+    rc = launch_gemv_rows(ctx->stream, Kb, ldk, k, nz, coef_d, 0.0, out_d);
+    if (rc) return rc;
+    *used = 1;
+  }
+  return ctx->end();
+}
+
 SVM_API int svmd_count_correct(void* h, const double* dec_d, const int32_t* y_d, int64_t m, int32_t zero_positive,
                                int64_t* correct) {
   SVMD_CTX(h);

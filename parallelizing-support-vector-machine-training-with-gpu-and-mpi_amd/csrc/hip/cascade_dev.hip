@@ -263,8 +263,9 @@ class HipBackend final : public Backend {
   SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
     return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
   }
-  bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p) override {
-    return solo([&] { return kkt_check(S, nz, d, p); });
+  bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h,
+                            const double* mx_h) override {
+    return solo([&] { return kkt_check(S, nz, d, p, mn_h, mx_h); });
   }
   double take_solo_ms() override {
     if (!solo_any_) return -1.0;
@@ -323,10 +324,11 @@ class HipBackend final : public Backend {
     check(rc, "svmd_train");
     return SolveStats{r.iterations, r.b, r.stop_reason, tm.gram_ms, on_rows};
   }
-  // f from the cross-kernel K(S, S[0:nz]) (MFMA f64 decision path) instead of the int8-exact Gram
-  // the solve would build: the two kernel values agree to a few ulps, so f agrees to ~1e-9 here
-  // (nz <= a few thousand, alpha <= C); a 1e-7 margin on the stop test covers it.
-  bool kkt_check(DSet& S, int64_t nz, int64_t d, const svm_params& p) {
+  // f from the cross-kernel K(S, S[0:nz]): the exact-integer block (int8 MFMA, the very values of
+  // the Gram the solve would build) for pixel data, else the MFMA f64 decision path, whose values
+  // agree with the Gram's to a few ulps, so f agrees to ~1e-9 here (nz <= a few thousand,
+  // alpha <= C); a 1e-7 margin on the stop test covers either.
+  bool kkt_check(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
     const char* e = getenv("SVM355_CASCADE_SKIP");  // =0 disables the check (A/B runs, tests)
     if ((e && atoi(e) == 0) || nz <= 0 || nz > S.k) return false;
     const int64_t ldd = ld(d), k = S.k;
@@ -340,9 +342,15 @@ class HipBackend final : public Backend {
     hipLaunchKernelGGL(coef_kernel, dim3(unsigned((nz + 255) / 256)), dim3(256), 0, stream_, S.a.as<double>(),
                        S.y.as<int32_t>(), nz, coef);
     hipcheck(hipGetLastError(), "coef kernel");
-    check(svmd_decision(ctx_, S.X.as<double>(), sqn, coef, nz, ldd, S.X.as<double>(), sqn, k, ldd, ldd, p.gamma, 0.0,
-                        sum),
-          "svmd_decision");
+    int32_t used_int = 0;
+    const char* ki = getenv("SVM355_CASCADE_SKIP_INT");  // =0: always the f64 cross-kernel (A/B)
+    if (!(ki && atoi(ki) == 0) && mn_h && mx_h)
+      check(svmd_decision_int(ctx_, S.X.as<double>(), k, ldd, d, mn_h, mx_h, coef, nz, p.gamma, sum, &used_int),
+            "svmd_decision_int");
+    if (!used_int)
+      check(svmd_decision(ctx_, S.X.as<double>(), sqn, coef, nz, ldd, S.X.as<double>(), sqn, k, ldd, ldd, p.gamma,
+                          0.0, sum),
+            "svmd_decision");
     hipLaunchKernelGGL(kkt_bounds_kernel, dim3(1), dim3(1024), 0, stream_, sum, S.y.as<int32_t>(), S.a.as<double>(), k,
                        p.C, p.eps, res);
     hipcheck(hipGetLastError(), "kkt kernel");

@@ -139,6 +139,8 @@ int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const Q
                   int32_t* N0, double* WN, bool* ok);
 int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const QuantPlan& P, double gamma, double* K,
               int64_t ldk, void* ws, bool* used);
+int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64_t ncols, const QuantPlan& P,
+                    double gamma, double* K, int64_t ldk, void* ws, bool* used);
 int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t d,
                      const QuantPlan& P, const int32_t* y, double* alpha, int32_t warm, const svm_params& p,
                      svm_result* r, size_t cache_bytes, int64_t* trace, int64_t trace_cap, int32_t* used_int);

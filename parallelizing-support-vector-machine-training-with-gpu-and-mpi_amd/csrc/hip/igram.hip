@@ -166,11 +166,14 @@ __global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict
 // off-diagonal tile also stored transposed.  kq = int8 columns (multiple of BK); columns
 // [0, main0) are the extra groups (main0 a multiple of 32), step_w[s] = weight of k-step s's group
 // if s is the LAST k-step of its group (flush), else 0.  BK = int8 columns per LDS stage.
-template <bool EXTRA, int BK>
+// RECT: the block K(rows [0, n), rows [0, ncols)) of the same quantised set instead of the
+// symmetric Gram (every 128 x 128 tile of the tiles x ctiles grid, no mirror), e.g. the kernel
+// values of a training set against its leading support vectors (the cascade's warm-start check).
+template <bool EXTRA, int BK, bool RECT = false>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
-    double* __restrict__ K, int64_t ldk, int64_t tiles) {
+    double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols) {
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
   constexpr int CPR = BK / 16;            // 16-byte chunks per staged row
@@ -186,10 +189,17 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   char* Bs = As + QBM * QLS;                         // 64 rows x QLS
   double* img = reinterpret_cast<double*>(smem + kTableBytes);  // epilogue: per-wave 32x33 images
 
-  const int64_t ntile = tiles * (tiles + 1) / 2;
+  const int64_t ctiles = RECT ? (ncols + QBM - 1) / QBM : tiles;
+  const int64_t ncol = RECT ? ncols : n;  // column bound
+  const int64_t ntile = RECT ? tiles * ctiles : tiles * (tiles + 1) / 2;
   const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
   int64_t tm, tn;
-  tri_tile(wg >> 1, tiles, tm, tn);
+  if (RECT) {
+    tm = (wg >> 1) / ctiles;
+    tn = (wg >> 1) - tm * ctiles;
+  } else {
+    tri_tile(wg >> 1, tiles, tm, tn);
+  }
   const int64_t bm = tm * QBM, bn = tn * QBM + (wg & 1) * QBN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -202,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     if (EXTRA) wn_r[t] = gi < n ? WN[gi] : 0.0;
   } else if (t < QBM + QBN) {
     const int64_t gj = bn + (t - QBM);
-    n0_c[t - QBM] = gj < n ? N0[gj] : 0;
-    if (EXTRA) wn_c[t - QBM] = gj < n ? WN[gj] : 0.0;
+    n0_c[t - QBM] = gj < ncol ? N0[gj] : 0;
+    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[gj] : 0.0;
   }
 
   // Staging per BK-column stage: thread t copies 16-byte chunk t % CPR of rows t / CPR + RPP * p.
@@ -284,10 +294,10 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   // ---- epilogue in the 32x32 accumulator layout: col = lane & 31,
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
   double* im = img + w * (32 * 33);
-  const bool mirror = tm != tn;
+  const bool mirror = !RECT && tm != tn;
   // Interior tiles (the vast majority) skip the per-element bounds tests; store addresses are a
   // per-lane base plus a wave-uniform (scalar) row offset.
-  const bool interior = bm + QBM <= n && bn + QBM <= n;
+  const bool interior = bm + QBM <= n && bn + QBM <= ncol;
   const int64_t row0 = bm + w * 32 + 4 * h;  // this lane's row for r = 0
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj) {
@@ -317,7 +327,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
         const int rl = ro + 4 * h;
         const int64_t gi = row0 + ro;
         const double kv = gi == gj ? 1.0 : ex[q];
-        if (interior || (gi < n && gj < n)) __builtin_nontemporal_store(kv, kp + int64_t(ro) * ldk);
+        if (interior || (gi < n && gj < ncol)) __builtin_nontemporal_store(kv, kp + int64_t(ro) * ldk);
         if (mirror) im[l32 * 33 + rl] = kv;  // im[col][row]
       }
     }
@@ -529,13 +539,61 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
   if (const char* v = getenv("SVM355_IGRAM_BK")) bk = atoi(v) == 64 || P.kq % 128 ? 64 : 128;
 #define SVM_IGRAM(EX, B)                                                                                    \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, \
-                     WN, stw, P.w0, -gamma, K, ldk, tiles)
+                     WN, stw, P.w0, -gamma, K, ldk, tiles, int64_t(0))
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM(true, 128); else SVM_IGRAM(true, 64);
   } else {
     if (bk == 128) SVM_IGRAM(false, 128); else SVM_IGRAM(false, 64);
   }
 #undef SVM_IGRAM
+  SVMD_LAUNCH_CHECK();
+  *used = true;
+  return SVM_OK;
+}
+
+// K(rows [0, n), rows [0, ncols)) of the same (scaled) rows on the exact-integer path, ncols <= n,
+// into K (n x ldk, ldk >= ncols): bit-identical to those entries of run_igram's Gram.  ws holds
+// igram_workspace(n, P) bytes; *used = false (nothing written) when the data are not integer-valued.
+int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64_t ncols, const QuantPlan& P,
+                    double gamma, double* K, int64_t ldk, void* ws, bool* used) {
+  *used = false;
+  if (!P.ok || n <= 0 || ncols <= 0) return SVM_OK;
+  if (ncols > n || ldk < ncols) {
+    set_error("igram block: need ncols <= n and ldk >= ncols");
+    return SVM_ERR_ARG;
+  }
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
+  auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
+  auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
+  auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
+  auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
+  bool ok = false;
+  int rc = quantize_rows(s, X, n, ld, P, p, Q, N0, WN, &ok);
+  if (rc) return rc;
+  if (!ok) return SVM_OK;
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
+  const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (ncols + QBM - 1) / QBM;
+  const int64_t nwg = 2 * tiles * ctiles;  // two 128x64 halves per tile
+  if (nwg > 0x7FFFFFFF) {
+    set_error("igram block: problem too large for one launch");
+    return SVM_ERR_ARG;
+  }
+  const int bk = P.kq % 128 == 0 ? 128 : 64;
+#define SVM_IGRAM_BLOCK(EX, B)                                                                                 \
+  hipLaunchKernelGGL((igram_tri_kernel<EX, B, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, \
+                     N0, WN, stw, P.w0, -gamma, K, ldk, tiles, ncols)
+  if (P.main0 > 0) {
+    if (bk == 128) SVM_IGRAM_BLOCK(true, 128); else SVM_IGRAM_BLOCK(true, 64);
+  } else {
+    if (bk == 128) SVM_IGRAM_BLOCK(false, 128); else SVM_IGRAM_BLOCK(false, 64);
+  }
+#undef SVM_IGRAM_BLOCK
   SVMD_LAUNCH_CHECK();
   *used = true;
   return SVM_OK;

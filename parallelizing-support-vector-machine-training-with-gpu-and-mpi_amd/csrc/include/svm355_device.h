@@ -122,6 +122,14 @@ SVM_API int svmd_decision(void* ctx, const double* Xs_d, const double* ns_d, con
                           int64_t nsv, int64_t lds, const double* Xq_d, const double* nq_d, int64_t m,
                           int64_t ldq, int64_t kdim, double gamma, double b, double* out_d);
 
+// out_d[i] = sum_{k < nz} coef_d[k] * K(X_i, X_k) for the k (scaled) rows X_d whose first nz rows are
+// the terms, on the exact-integer path (the Gram's kernel values; mn_h / mx_h: host column
+// statistics the rows were scaled with).  *used = 0 (nothing written) when the rows are not
+// integer-valued pixels: the caller then takes svmd_decision.
+SVM_API int svmd_decision_int(void* ctx, const double* X_d, int64_t k, int64_t ldx, int64_t d, const double* mn_h,
+                              const double* mx_h, const double* coef_d, int64_t nz, double gamma, double* out_d,
+                              int32_t* used);
+
 // *correct = #{i : sign(dec_d[i]) == y_d[i]} on the device (prediction accuracy numerator);
 // zero_positive = 1 maps s >= 0 to +1 (cascade programs), 0 maps s > 0 to +1 (serial / GPU programs).
 SVM_API int svmd_count_correct(void* ctx, const double* dec_d, const int32_t* y_d, int64_t m,

@@ -366,6 +366,23 @@ def decision(Xs: torch.Tensor, ns: torch.Tensor, coef: torch.Tensor, Xq: torch.T
     return out
 
 
+def decision_int(X: torch.Tensor, d: int, mn: torch.Tensor, mx: torch.Tensor, coef: torch.Tensor, gamma: float):
+    """out[i] = sum_{k < nz} coef[k] K(X_i, X_k), nz = len(coef), on the exact-integer path (the
+    Gram's own kernel values) for scaled pixel rows X; None when the rows are not integer pixels."""
+    _check_rows(X, "X")
+    coef = coef.contiguous()
+    k, nz = X.shape[0], coef.numel()
+    out = torch.empty(k, dtype=torch.float64, device=X.device)
+    used = ctypes.c_int32(0)
+    mn_h = np.ascontiguousarray(mn.detach().cpu().numpy(), dtype=np.float64)
+    mx_h = np.ascontiguousarray(mx.detach().cpu().numpy(), dtype=np.float64)
+    ctx = _ctx_for(X)
+    N.check(ctx.lib.svmd_decision_int(ctx.bind(), N.ptr(X), k, X.shape[1], int(d), N.ptr(mn_h), N.ptr(mx_h),
+                                      N.ptr(coef), nz, float(gamma), N.ptr(out), ctypes.byref(used)),
+            "svmd_decision_int")
+    return out if used.value else None
+
+
 def count_correct(dec: torch.Tensor, y, zero_is_positive: bool = False) -> int:
     """#{i : sign(dec[i]) == y[i]} counted on the device (the reference's predict flag + reduce_sum,
     gpu_svm_main3.cu:277-315); s >= 0 -> +1 if zero_is_positive (cascade rule) else s > 0 -> +1."""

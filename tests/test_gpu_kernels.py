@@ -416,6 +416,31 @@ def test_near_integer_rows_take_the_fp64_gram(dev, mn_data):
     assert b.timings_["gram_path"] == "int8-exact"
 
 
+def test_decision_int_block_is_the_grams_columns(dev, D):
+    """svmd_decision_int (the cascade's warm-start check): the exact-integer block K(X, X[0:nz]) is
+    bit-identical to those columns of the resident exact-integer Gram (unit coefficient vectors pick
+    single columns), and its GEMV matches K[:, :nz] @ coef; real-valued rows are refused (None)."""
+    n, nz = 3000, 700
+    tr = synthetic_mnist(n, seed=41)
+    Xd = D.upload_rows(tr.compact().X, dev)
+    mn, mx, sqn = D.minmax_scale_(Xd, 784)
+    K, path = D.rbf_gram_sym(Xd, sqn, 0.00125, mn=mn, mx=mx)
+    assert path == "int8-exact"
+    for j in (0, 129, nz - 1):
+        e = torch.zeros(nz, dtype=torch.float64, device=dev)
+        e[j] = 1.0
+        out = D.decision_int(Xd, 784, mn, mx, e, 0.00125)
+        assert out is not None and torch.equal(out, K[:n, j])
+    g = torch.Generator(device="cpu").manual_seed(3)
+    coef = torch.randn(nz, dtype=torch.float64, generator=g).to(dev)
+    out = D.decision_int(Xd, 784, mn, mx, coef, 0.00125)
+    torch.testing.assert_close(out, K[:n, :nz] @ coef, rtol=1e-13, atol=1e-11)
+    rng = np.random.default_rng(2)
+    Xr = D.upload_rows(rng.normal(size=(300, 20)), dev)
+    mnr, mxr, _ = D.minmax_scale_(Xr, 20)
+    assert D.decision_int(Xr, 20, mnr, mxr, coef[:50], 0.05) is None
+
+
 def test_svc_int_gram_matches_fp64_gram(dev, mn_data):
     tr, te = mn_data
     a = SVC(device="cuda:0", gram="int").fit(tr.X, tr.y)
