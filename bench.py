@@ -53,8 +53,9 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=60000, help="training rows (MNIST-60k config)")
-    ap.add_argument("--m", type=int, default=10000, help="test rows for the parity fields")
+    # --rows / --test-rows: spellings torchrun's own parser does not take for an abbreviation of its options
+    ap.add_argument("--n", "--rows", dest="n", type=int, default=60000, help="training rows (MNIST-60k config)")
+    ap.add_argument("--m", "--test-rows", dest="m", type=int, default=10000, help="test rows for the parity fields")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
@@ -70,6 +71,9 @@ def main(argv=None):
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N > 1: seconds any rank waits on an exchange before every rank aborts its communicator "
                          "(a fit takes well under a second; a dead peer must not hang the run)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: the same launch paths on the C++ oracle (CPU tests of the torchrun / thread-rank "
+                         "plumbing; N > 1 under torchrun exchanges over gloo); not a benchmark")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
 
@@ -82,7 +86,8 @@ def main(argv=None):
     if multiproc and world_env != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
-    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    cpu = a.device == "cpu"
+    ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
     if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
         print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, {ndev} visible "
               "(use --transport loopback for a one-GPU rehearsal)", file=sys.stderr)
@@ -96,8 +101,10 @@ def main(argv=None):
     from svm355.utils.data import synthetic_mnist
 
     dev_index = local_rank if multiproc else 0
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
+    if not cpu:
+        torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
+    sync = (lambda: torch.cuda.synchronize(dev)) if not cpu else (lambda: None)
     use_cascade = a.gpus > 1 or a.cascade
     dist = None
     if multiproc:
@@ -118,22 +125,26 @@ def main(argv=None):
 
     group = crank = None
     if use_cascade:
-        if multiproc:
+        if multiproc and cpu:
+            from svm355.parallel.hostcomm import HostCommRank
+
+            crank = HostCommRank()
+        elif multiproc:
             from svm355.parallel.rccl import RcclRank
 
             crank = RcclRank.from_torch_dist(dev_index, a.comm_timeout)
-        else:
+        elif not cpu:
             from svm355.parallel.rccl import DeviceGroup
 
             group = DeviceGroup(a.gpus, a.transport, a.comm_timeout)
 
     def barrier_sync():
-        torch.cuda.synchronize(dev)
+        sync()
         if crank is not None:
             crank.barrier()  # RCCL all-reduce over the cascade's own communicators
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
 
     model = None
 
@@ -146,13 +157,13 @@ def main(argv=None):
                 crank, tr.X, tr.y, np.arange(lo, hi), a.n)
         else:
             model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit(
-                tr.X, tr.y, world=a.gpus, device="cuda", group=group)
+                tr.X, tr.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
 
     warm_ms = []
     for _ in range(a.warmup):
         tw = time.perf_counter()
         step()
-        torch.cuda.synchronize(dev)
+        sync()
         warm_ms.append(round((time.perf_counter() - tw) * 1e3, 3))
     barrier_sync()
     t0 = time.perf_counter()
@@ -179,10 +190,10 @@ def main(argv=None):
         # Prediction on the 10k test rows (outside the timed region): H2D, scaling with the training
         # statistics, MFMA cross-kernel against the SVs, decision values back to the host.  The
         # reference's GPU "prediction" (38.3 s at 60k) also parses the test CSV.
-        torch.cuda.synchronize(dev)
+        sync()
         tp = time.perf_counter()
         model.decision_function(te.X)
-        torch.cuda.synchronize(dev)
+        sync()
         pred_ms = (time.perf_counter() - tp) * 1e3
         acc = model.score(te.X, te.y)
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
@@ -232,10 +243,10 @@ def main(argv=None):
                 SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)  # warm
                 ts = []
                 for _ in range(a.baseline_1gpu):
-                    torch.cuda.synchronize(dev)
+                    sync()
                     tb = time.perf_counter()
                     SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
-                    torch.cuda.synchronize(dev)
+                    sync()
                     ts.append(time.perf_counter() - tb)
                 one = float(np.median(ts))
                 extra["single_gpu_s"] = round(one, 6)
@@ -264,6 +275,7 @@ def main(argv=None):
             },
             "launch": "torchrun (one rank per process)" if multiproc else
                       ("in-process thread ranks" if use_cascade else "single process"),
+            **({"device": "cpu (C++ oracle; launch-path check, not a benchmark)"} if cpu else {}),
             "host_rows": "uint8 (widened to fp64 on device)" if a.input == "u8" else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),

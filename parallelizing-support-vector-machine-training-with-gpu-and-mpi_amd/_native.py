@@ -149,6 +149,8 @@ _CORE_SIGS = {
     "svm_cascade_default_cfg": (None, [POINTER(SvmCascadeCfg)]),
     "svm_cascade_fit_cpu": (POINTER(SvmCascadeOut), [_P, _P, c_int64, c_int64, c_int32, POINTER(SvmCascadeCfg)]),
     "svm_cascade_free": (None, [POINTER(SvmCascadeOut)]),
+    "svm_cascade_rank_fit_cpu": (POINTER(SvmCascadeOut), [_P, _P, _P, _P, c_int64, c_int64, c_int64,
+                                                          POINTER(SvmCascadeCfg)]),
 }
 
 _HIP_SIGS = {

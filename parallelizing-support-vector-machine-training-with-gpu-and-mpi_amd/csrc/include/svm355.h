@@ -176,6 +176,26 @@ SVM_API svm_cascade_out* svm_cascade_fit_cpu(const double* X, const int32_t* y, 
                                              int32_t world, const svm_cascade_cfg* cfg);
 SVM_API void svm_cascade_free(svm_cascade_out* o);
 
+// One cascade rank per process on the CPU oracle backend, exchanging through caller-supplied
+// collectives (e.g. a torch.distributed gloo group: svm355.parallel.hostcomm) -- the CPU twin of
+// the per-process RCCL rank, svmd_cascade_rank_fit.  Buffers are host memory; every callback
+// returns 0 on success.  gather's recv is NULL on non-root ranks (root: world * bytes, rank order).
+typedef struct svm_host_comm {
+  void* ctx;
+  int32_t rank, world;
+  int (*bcast)(void* ctx, void* buf, int64_t bytes, int32_t root);
+  int (*allgather)(void* ctx, const void* send, int64_t bytes, void* recv);  // recv: world * bytes
+  int (*allreduce_f64)(void* ctx, double* buf, int64_t n, int32_t op);       // op 0 = min, 1 = max
+  int (*gather)(void* ctx, const void* send, int64_t bytes, void* recv, int32_t root);
+  int (*send)(void* ctx, const void* buf, int64_t bytes, int32_t peer);
+  int (*recv)(void* ctx, void* buf, int64_t bytes, int32_t peer);
+  int (*barrier)(void* ctx);
+} svm_host_comm;
+// This process's rank trains on its partition (n_part x d float64 host rows, labels, global ids).
+SVM_API svm_cascade_out* svm_cascade_rank_fit_cpu(const svm_host_comm* comm, const double* X, const int32_t* y,
+                                                  const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
+                                                  const svm_cascade_cfg* cfg);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,7 @@ ID-set convergence, checkpoint/resume, abort on failure).
 * ``fit(X, y, world=P)`` on ``device="cuda"``: P thread-ranks on P GPUs of this process
   (``DeviceGroup``: ncclCommInitAll, RCCL over xGMI) or a loopback rehearsal on fewer GPUs.
 * ``fit_rank(rank, X_part, y_part, ids, n_total)``: one rank per process (``RcclRank``, e.g. under
-  torchrun).
+  torchrun; ``HostCommRank``: the same on the CPU oracle over a gloo group).
 """
 from __future__ import annotations
 
@@ -113,8 +113,13 @@ class CascadeSVM:
         return self
 
     def fit_rank(self, rank, X_part, y_part, ids, n_total: int) -> "CascadeSVM":
-        """This process's rank (``RcclRank``) trains on its partition (raw rows, global ids)."""
+        """This process's rank trains on its partition (raw rows, global ids): ``RcclRank`` (its GPU,
+        RCCL) or ``HostCommRank`` (the CPU oracle over a gloo group, the multi-process CPU tests)."""
         self._check_world(rank.world)
+        if rank.device == "cpu":
+            self.device = "cpu"
+            self.result = CascadeResult.take(rank.fit(self.cfg, X_part, y_part, ids, n_total))
+            return self
         X = np.ascontiguousarray(X_part, dtype=np.uint8 if X_part.dtype == np.uint8 else np.float64)
         y = np.ascontiguousarray(y_part, dtype=np.int32)
         ids = np.ascontiguousarray(ids, dtype=np.int64)

@@ -1,0 +1,100 @@
+"""The per-process cascade path (one rank per process, as the driver's torchrun launch of
+``bench.py --gpus N`` runs it on N GPUs) exercised on the CPU: ``HostCommRank`` gives the native
+driver gloo collectives instead of RCCL, everything else -- bench.py's torchrun branch, the
+partitioning by global ids, ``fit_rank``, the solve-log gather, the timing max over ranks -- is the
+code the GPUs run.  Results must be bit-identical to the same cascade on thread ranks (loopback)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+import time
+from pathlib import Path
+
+import pytest
+
+from svm355 import SVMParams
+from svm355.parallel.cascade import CascadeSVM
+from svm355.utils.data import synthetic_mnist
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=str(ROOT))
+    env.pop("WORLD_SIZE", None)
+    return env
+
+
+def _torchrun_bench(nproc, *args, timeout=240):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--gpus", str(nproc), "--device", "cpu", *args]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-4000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("topology,nproc", [("star", 2), ("star", 3), ("tree", 4)])
+def test_torchrun_ranks_match_thread_ranks(topology, nproc):
+    n = 1200
+    out = _torchrun_bench(nproc, "--rows", str(n), "--test-rows", "200", "--steps", "1", "--warmup", "0",
+                          "--baseline-1gpu", "0", "--topology", topology)
+    assert out["n_gpus"] == nproc and out["launch"].startswith("torchrun")
+    assert out["config"]["parallelism"] == f"cascade-{topology}-dp{nproc}"
+    assert out["transport"] == "hostcomm"
+    # the solve log of every rank reached rank 0 (dist.all_gather_object in bench.py)
+    assert out["max_rank_smo_iterations"] >= out["rank0_smo_iterations"] > 0
+    assert len(out["per_round_critical_path"]) == out["rounds"]
+
+    tr = synthetic_mnist(n, seed=2024)
+    ref = CascadeSVM(SVMParams(), topology=topology).fit(tr.X, tr.y, world=nproc).result
+    assert out["n_sv"] == len(ref.ids)
+    assert out["b"] == ref.b  # bit-identical: same driver, same arithmetic, different transport
+    assert out["rounds"] == ref.rounds and out["sv_history"] == ref.sv_history
+
+
+_FAIL_SCRIPT = textwrap.dedent("""
+    import datetime, sys
+    import torch.distributed as dist
+    from svm355 import SVMParams
+    from svm355.parallel.cascade import CascadeSVM, partition_bounds
+    from svm355.parallel.hostcomm import HostCommRank
+    from svm355.utils.data import synthetic_mnist
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=30))
+    r, P, n = dist.get_rank(), dist.get_world_size(), 800
+    lo, hi = partition_bounds(n, P, r)
+    tr = synthetic_mnist(hi - lo, seed=7, offset=lo)
+    import numpy as np
+    try:
+        CascadeSVM(SVMParams(), fail_rank=1, fail_round=1).fit_rank(HostCommRank(), tr.X, tr.y, np.arange(lo, hi), n)
+    except Exception as e:
+        print(f"rank {r} failed: {e}", flush=True)
+        sys.exit(3)
+    print(f"rank {r} finished", flush=True)
+""")
+
+
+def test_a_failing_process_rank_ends_every_rank():
+    """SURVEY §5.3 / mpi_svm_main3.cpp:420-428 (MPI_Abort): rank 1 throws at the start of round 1; rank
+    0, blocked in a collective, must get an error (not hang) and both processes exit non-zero."""
+    port, env = _port(), _env()
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _FAIL_SCRIPT], cwd=ROOT, env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    t0 = time.time()
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert time.time() - t0 < 100
+    assert [p.returncode for p in procs] == [3, 3], outs
+    assert "rank 1 failed" in outs[1], outs[1]
+    assert "rank 0 failed" in outs[0] and "hostcomm" in outs[0], outs[0]
