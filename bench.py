@@ -82,7 +82,9 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    multiproc = world_env > 1
+    # one rank per process under torchrun; with one process (--cascade) the same per-process path runs
+    # on a single GPU, so a one-GPU box rehearses the launch the N-GPU run takes
+    multiproc = world_env > 1 or ("LOCAL_RANK" in os.environ and a.cascade)
     if multiproc and world_env != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2

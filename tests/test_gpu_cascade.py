@@ -121,6 +121,34 @@ def test_rccl_rank_bootstrap_equals_group(data):
     assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
 
 
+def test_torchrun_bench_per_process_rccl_rank(data):
+    """bench.py launched by torchrun (the driver's N-GPU launch), here with one process: gloo bootstrap,
+    ncclUniqueId over the store, ncclCommInitRank, fit_rank, the solve-log gather and the timing max
+    over ranks -- the whole per-process branch on the GPU.  Same model as the thread-rank group."""
+    import os
+    import socket
+    import sys
+
+    root = Path(__file__).resolve().parents[1]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=str(root))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(root / "bench.py"), "--gpus", "1", "--cascade", "--rows", str(N),
+           "--test-rows", str(M), "--seed", "21", "--steps", "2", "--warmup", "1", "--baseline-1gpu", "1"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=180)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["launch"].startswith("torchrun") and out["transport"] == "rccl" and out["n_gpus"] == 1
+    tr, _ = data
+    ref = CascadeSVM(SVMParams()).fit(tr.compact().X, tr.y, world=1, device="cuda", transport="rccl").result
+    assert out["n_sv"] == len(ref.ids) and out["b"] == ref.b and out["rounds"] == ref.rounds
+    assert out["single_gpu_s"] > 0 and out["speedup_vs_1gpu"] > 0
+
+
 def test_group_keeps_working_after_a_loopback_failure(data):
     tr, _ = data
     X = tr.compact().X

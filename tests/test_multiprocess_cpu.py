@@ -43,11 +43,11 @@ def _torchrun_bench(nproc, *args, timeout=240):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("topology,nproc", [("star", 2), ("star", 3), ("tree", 4)])
+@pytest.mark.parametrize("topology,nproc", [("star", 1), ("star", 2), ("star", 3), ("tree", 4)])
 def test_torchrun_ranks_match_thread_ranks(topology, nproc):
     n = 1200
     out = _torchrun_bench(nproc, "--rows", str(n), "--test-rows", "200", "--steps", "1", "--warmup", "0",
-                          "--baseline-1gpu", "0", "--topology", topology)
+                          "--baseline-1gpu", "0", "--topology", topology, "--cascade")
     assert out["n_gpus"] == nproc and out["launch"].startswith("torchrun")
     assert out["config"]["parallelism"] == f"cascade-{topology}-dp{nproc}"
     assert out["transport"] == "hostcomm"
