@@ -138,16 +138,45 @@ def _cascade(argv) -> int:
     if tr.n == 0:
         print("Error: No data read from file.", file=sys.stderr)
         return 1
-    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // max(1, a.gpus)),
+    # Launched by torchrun (``torchrun --nproc-per-node P -m svm355 cascade ...``, the reference's
+    # ``mpirun -np P``): this process is one rank -- its GPU LOCAL_RANK over RCCL (ncclCommInitRank), or
+    # with --cpu the C++ oracle over the launcher's gloo group -- and trains on its contiguous partition.
+    per_process = "LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ
+    world = int(os.environ["WORLD_SIZE"]) if per_process else max(1, a.gpus)
+    params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // world),
                        wss=2 if a.wss == "second" else 1)
     model = CascadeSVM(params, topology=a.topology, max_rounds=a.max_rounds, verbose=a.verbose,
                        checkpoint_dir=a.checkpoint_dir, resume=a.resume, comm_timeout_s=a.comm_timeout)
     device = "cpu" if a.cpu else "cuda"
     X = tr.X if a.cpu else tr.compact().X
-    t0 = time.perf_counter()
-    model.fit(X, tr.y, world=max(1, a.gpus), device=device, transport=a.transport)
+    crank = None
+    if per_process:
+        import numpy as np
+        import torch.distributed as dist
+
+        from .parallel.cascade import partition_bounds
+
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(60.0, a.comm_timeout)))
+        if a.cpu:
+            from .parallel.hostcomm import HostCommRank
+
+            crank = HostCommRank()
+        else:
+            from .parallel.rccl import RcclRank
+
+            crank = RcclRank.from_torch_dist(int(os.environ["LOCAL_RANK"]), a.comm_timeout)
+        lo, hi = partition_bounds(tr.n, world, crank.rank)
+        t0 = time.perf_counter()
+        model.fit_rank(crank, X[lo:hi], tr.y[lo:hi], np.arange(lo, hi), tr.n)
+    else:
+        t0 = time.perf_counter()
+        model.fit(X, tr.y, world=world, device=device, transport=a.transport)
     t1 = time.perf_counter()
     res = model.result
+    if crank is not None and crank.rank != 0:  # the reference prints and saves on rank 0 only
+        crank.close()
+        dist.destroy_process_group()
+        return 0
     acc = None
     if te.n:
         correct = int(round(model.score(te.X, te.y) * te.n))
@@ -169,6 +198,9 @@ def _cascade(argv) -> int:
         Path(a.json).write_text(json.dumps(out) + "\n")
     if a.model_dir:
         model.save(a.model_dir)
+    if crank is not None:
+        crank.close()
+        dist.destroy_process_group()
     return 0
 
 

@@ -98,3 +98,25 @@ def test_a_failing_process_rank_ends_every_rank():
     assert [p.returncode for p in procs] == [3, 3], outs
     assert "rank 1 failed" in outs[1], outs[1]
     assert "rank 0 failed" in outs[0] and "hostcomm" in outs[0], outs[0]
+
+
+def test_torchrun_cascade_cli_is_mpirun_np(tmp_path):
+    """``torchrun --nproc-per-node P -m svm355 cascade`` = the reference's ``mpirun -np P`` launch
+    (code/mpi_svm3.sh): every process is one rank, rank 0 prints the reference lines and writes the
+    model; same model as the thread-rank CLI."""
+    a, b = tmp_path / "a.json", tmp_path / "b.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "-m", "svm355", "cascade", "--cpu", "--topology", "tree",
+           "--synthetic", "1000,200", "--json", str(a), "--model-dir", str(tmp_path / "m")]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert p.stdout.count("[rank 0] Running CascadeSVM with 2 processes") == 1  # mpi_svm_main3.cpp:430, rank 0 only
+    assert "[rank 0] Cascade finished in" in p.stdout
+    assert (tmp_path / "m" / "final_sv_ids.txt").exists()
+    q = subprocess.run([sys.executable, "-m", "svm355", "cascade", "--cpu", "--gpus", "2", "--topology", "tree",
+                        "--synthetic", "1000,200", "--json", str(b)], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=240)
+    assert q.returncode == 0, q.stderr[-3000:]
+    ja, jb = json.loads(a.read_text()), json.loads(b.read_text())
+    assert ja["transport"] == "hostcomm" and ja["world"] == 2
+    assert ja["b"] == jb["b"] and ja["n_sv"] == jb["n_sv"] and ja["rounds"] == jb["rounds"]
