@@ -353,6 +353,36 @@ static int gram_any(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int6
   return launch_rbf_gram(ctx->stream, X_d, sqn_d, n, ld, X_d, sqn_d, n, ld, kdim, gamma, K, ldk, true);
 }
 
+// The library-owned Gram (DeviceCtx::gram, grow-only) sized for n rows; ldk = its row stride.
+static int ensure_gram(DeviceCtx* ctx, int64_t n, int64_t* ldk_out) {
+  const int64_t ldk = (n + 1) / 2 * 2;  // keep rows 16-byte aligned
+  const size_t bytes = size_t(n) * size_t(ldk) * 8;
+  *ldk_out = ldk;
+  if (bytes <= ctx->gram_bytes) return SVM_OK;
+  if (ctx->gram) {
+    SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+    SVMD_CHECK(hipFree(ctx->gram));
+    ctx->gram = nullptr;
+    ctx->gram_bytes = 0;
+  }
+  hipError_t e = hipMalloc(&ctx->gram, bytes);
+  if (e != hipSuccess && ctx->rc_cache) {  // give back an idle row-cache slab and retry
+    (void)hipGetLastError();
+    SVMD_CHECK(hipFree(ctx->rc_cache));
+    ctx->rc_cache = nullptr;
+    ctx->rc_cache_bytes = 0;
+    e = hipMalloc(&ctx->gram, bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s", double(bytes) * 1e-9,
+              hipGetErrorString(e));
+    return SVM_ERR_OOM;
+  }
+  ctx->gram_bytes = bytes;
+  return SVM_OK;
+}
+
 static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,
                       const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params& q, svm_result* r,
                       double* K_d, int64_t ldk, svmd_timing* timing, const double* mn_h, const double* mx_h,
@@ -362,30 +392,8 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
   if (rc) return rc;
   double* K = K_d;
   if (!K) {  // library-owned Gram, cached in the context (see DeviceCtx::gram)
-    ldk = (n + 1) / 2 * 2;  // keep rows 16-byte aligned
-    const size_t bytes = size_t(n) * size_t(ldk) * 8;
-    if (bytes > ctx->gram_bytes) {
-      if (ctx->gram) {
-        SVMD_CHECK(hipStreamSynchronize(ctx->stream));
-        SVMD_CHECK(hipFree(ctx->gram));
-        ctx->gram = nullptr;
-        ctx->gram_bytes = 0;
-      }
-      hipError_t e = hipMalloc(&ctx->gram, bytes);
-      if (e != hipSuccess && ctx->rc_cache) {  // give back an idle row-cache slab and retry
-        (void)hipGetLastError();
-        SVMD_CHECK(hipFree(ctx->rc_cache));
-        ctx->rc_cache = nullptr;
-        ctx->rc_cache_bytes = 0;
-        e = hipMalloc(&ctx->gram, bytes);
-      }
-      if (e != hipSuccess) {
-        set_error("svmd_train: cannot allocate the %.1f GB RBF Gram matrix: %s", double(bytes) * 1e-9,
-                  hipGetErrorString(e));
-        return SVM_ERR_OOM;
-      }
-      ctx->gram_bytes = bytes;
-    }
+    rc = ensure_gram(ctx, n, &ldk);
+    if (rc) return rc;
     K = ctx->gram;
   }
   rc = gram_any(ctx, X_d, sqn_d, n, ld, kdim, mn_h, mx_h, d, gram_mode, q.gamma, K, ldk, gram_used);
@@ -413,6 +421,13 @@ static int train_impl(DeviceCtx* ctx, const double* X_d, const double* sqn_d, in
     timing->smo_ms = timing->total_ms - t_gram;
   }
   return ctx->end();
+}
+
+// Size the context's Gram for an n-row solve ahead of it (SVM_ERR_OOM if it does not fit).
+SVM_API int svmd_reserve_gram(void* h, int64_t n) {
+  SVMD_CTX(h);
+  int64_t ldk = 0;
+  return n > 0 ? ensure_gram(ctx, n, &ldk) : SVM_OK;
 }
 
 SVM_API int svmd_train(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t kdim,

@@ -261,7 +261,13 @@ class HipBackend final : public Backend {
     d2h(ids, ids_d_, k * 8);
   }
   SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
-    return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
+    if (!(serial_ && release_gram_)) return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
+    // Large-n rehearsals of P ranks on one GPU (SVM355_CASCADE_RELEASE_GRAM=1 with serial solves):
+    // P resident Grams do not fit together, so each solve's Gram is sized before its timed region
+    // (the grow-only buffer a rank keeps on its own GPU) and handed back after it, under the lock.
+    return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); },
+                [&] { (void)svmd_reserve_gram(ctx_, S.k); },
+                [&] { check(svmd_release_cache(ctx_), "svmd_release_cache"); });
   }
   bool warm_start_converged(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h,
                             const double* mx_h) override {
@@ -285,16 +291,19 @@ class HipBackend final : public Backend {
     static std::mutex m;
     return m;
   }
-  template <class F>
-  decltype(std::declval<F&>()()) solo(F&& f) {
+  // pre / post run under the lock, outside the timed region.
+  template <class F, class Pre = void (*)(), class Post = void (*)()>
+  decltype(std::declval<F&>()()) solo(F&& f, Pre&& pre = [] {}, Post&& post = [] {}) {
     if (!serial_) return f();
     std::lock_guard<std::mutex> lk(solo_mutex());
+    pre();
     sync();
     const auto t0 = std::chrono::steady_clock::now();
     auto r = f();
     sync();
     solo_acc_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     solo_any_ = true;
+    post();
     return r;
   }
   SolveStats solve_impl(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
@@ -399,6 +408,10 @@ class HipBackend final : public Backend {
   size_t idx_cap_ = 0, ids_cap_ = 0, sqn_cap_ = 0, kkt_cap_ = 0;
   const bool serial_ = [] {
     const char* v = getenv("SVM355_CASCADE_SERIAL_SOLVES");
+    return v && atoi(v) != 0;
+  }();
+  const bool release_gram_ = [] {
+    const char* v = getenv("SVM355_CASCADE_RELEASE_GRAM");
     return v && atoi(v) != 0;
   }();
   double solo_acc_ = 0.0;

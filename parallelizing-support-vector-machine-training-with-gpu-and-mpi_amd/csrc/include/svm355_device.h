@@ -41,6 +41,8 @@ SVM_API void svmd_destroy(void* ctx);
 // Free the Gram matrix the library allocated for svmd_train* with K_d == NULL (it is kept in the
 // context between calls so repeated fits of the same size do not re-allocate it).
 SVM_API int svmd_release_cache(void* ctx);
+// Size the context-owned Gram for an n-row solve ahead of it (SVM_ERR_OOM if it does not fit).
+SVM_API int svmd_reserve_gram(void* ctx, int64_t n);
 // Self-test of the Gram epilogue's exp: lib_d[i] = device libm exp(x_d[i]), batch_d[i] = the
 // batched evaluation the Gram kernel uses (they must agree bit for bit).
 SVM_API int svmd_selftest_exp(void* ctx, const double* x_d, int64_t n, double* lib_d, double* batch_d);
