@@ -150,7 +150,9 @@ def build_sanitized(force=False, verbose=False) -> Path:
     srcs = [*CORE_SRCS, CSRC / "apps" / "svm_serial.cpp"]
     if force or _stale(exe, [*srcs, *CORE_HDRS, CSRC / "apps" / "cli_common.h"]):
         flags = [f for f in CXXFLAGS if f != "-O3"] + SANITIZE
-        _run(["g++", *flags, *srcs, "-o", exe], verbose)
+        tmp = out_dir / f".svm_serial.{os.getpid()}"  # link aside, then rename: a concurrent run of the
+        _run(["g++", *flags, *srcs, "-o", tmp], verbose)  # old file keeps its inode (no ETXTBSY)
+        os.replace(tmp, exe)
     return exe
 
 
