@@ -7,8 +7,11 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+( while true; do date >> gpurun_out/lnc_tick.txt; sleep 50; done ) &  # progress for the silence watchdog
+TICK=$!
+trap "kill $TICK 2>/dev/null" EXIT
 for n in ${NS:-500000 1000000}; do
-  SVM355_CASCADE_SERIAL_SOLVES=1 SVM355_CASCADE_RELEASE_GRAM=1 timeout -k 10 ${TL:-500} python -u bench.py --gpus 8 \
+  SVM355_RC_VERBOSE=1 SVM355_CASCADE_SERIAL_SOLVES=1 SVM355_CASCADE_RELEASE_GRAM=1 timeout -k 10 ${TL:-500} python -u bench.py --gpus 8 \
     --transport loopback --n $n --m 2000 --steps 1 --warmup 1 --baseline-1gpu 2 --out gpurun_out/lnc_$n.json \
     > gpurun_out/lnc_$n.log 2>&1 || { tail -30 gpurun_out/lnc_$n.log; exit 1; }
   python -c "
