@@ -77,6 +77,26 @@ def test_optimal_warm_start_skip_changes_nothing(data, monkeypatch, topology, wo
     assert all(ref[(s["rank"], s["round"], s["layer"])] == 1 for s in skipped)
 
 
+def test_serial_solve_rehearsal_with_released_grams_changes_nothing(data, monkeypatch):
+    """The large-n rehearsal mode (SVM355_CASCADE_SERIAL_SOLVES=1 + SVM355_CASCADE_RELEASE_GRAM=1: each
+    solve's Gram sized before its timed region and released after it, svmd_reserve_gram) times every
+    solve alone and produces the same model bit for bit."""
+    tr, _ = data
+    X = tr.compact().X
+    a = CascadeSVM(SVMParams()).fit(X, tr.y, world=3, device="cuda", transport="loopback").result
+    monkeypatch.setenv("SVM355_CASCADE_SERIAL_SOLVES", "1")
+    monkeypatch.setenv("SVM355_CASCADE_RELEASE_GRAM", "1")
+    g = DeviceGroup(3, "loopback")  # backends read the knobs when they are created
+    try:
+        b = CascadeSVM(SVMParams()).fit(X, tr.y, world=3, device="cuda", group=g).result
+    finally:
+        g.close()
+    assert a.ids.tolist() == b.ids.tolist() and a.b == b.b and a.rounds == b.rounds
+    np.testing.assert_array_equal(a.alpha, b.alpha)
+    assert all(s["solo_ms"] >= 0 for s in b.solves if not s["skipped"])
+    assert not any(s["row_cache"] for s in b.solves)
+
+
 @pytest.mark.parametrize("topology,world", [("star", 2), ("tree", 2)])
 def test_row_cache_solves_equal_gram_solves(data, monkeypatch, topology, world):
     """A partition whose Gram does not fit is solved on the HBM row cache (cascade_dev.hip
