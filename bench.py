@@ -230,7 +230,12 @@ def main(argv=None):
                                                 for q in range(max(1, r.world))),
                  "note": "per_round_critical_path = [round, slowest local solve ms (tree: first layer), rank-0 "
                          "merge ms (tree: slowest rank of each later layer), their SMO iterations]; "
-                         "the single-GPU trainer solves the same 60k problem in one 12,793-iteration SMO"}
+                         "the single-GPU trainer solves the same 60k problem in one 12,793-iteration SMO",
+                 # recorded one-GPU rehearsal (solo-timed solves), not measured by this run: where the cascade
+                 # overtakes one GPU -- partitions with resident Grams vs one SMO on the row cache
+                 "large_n_crossover_rehearsal": {"n": 1000000, "star_p8_critical_path_s": 1.670,
+                                                 "single_gpu_s": 2.072,
+                                                 "source": "profiles/r2_largen_cascade_vs_1gpu.txt"}}
         if rank == 0:
             extra["accuracy"] = model.score(te.X, te.y)
         ref = (REF_STAR_S if a.topology == "star" else REF_TREE_S).get(a.gpus)
