@@ -101,6 +101,67 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
   if (__any(bad) && lane == 0) atomicOr(fail, 1u);
 }
 
+// Same quantisation with the column tables staged once per workgroup in LDS (perm; range and offset
+// as one packed int32 -- both are small integers, exact as doubles; the extra-group weights) and the
+// workgroup walking many rows: the per-element table loads of quantize_rows_kernel become LDS reads.
+// Every lane handles the same k in the same order with the same arithmetic, so N0 / WN / Q are
+// bit-identical.  kq <= kQuantLdsMaxKq.
+constexpr int kQuantLdsMaxKq = 2048;
+__global__ __launch_bounds__(256) void quantize_rows_lds_kernel(
+    const double* __restrict__ X, int64_t n, int64_t ld, const int32_t* __restrict__ perm,
+    const double* __restrict__ rmul, const double* __restrict__ off, const double* __restrict__ wx, int main0,
+    int kq, int8_t* __restrict__ Q, int32_t* __restrict__ N0, double* __restrict__ WN, unsigned* __restrict__ fail) {
+  extern __shared__ __attribute__((aligned(16))) char qsm[];
+  int32_t* sp = reinterpret_cast<int32_t*>(qsm);
+  int32_t* sro = sp + kq;
+  double* swx = reinterpret_cast<double*>(sro + kq);
+  for (int k = threadIdx.x; k < kq; k += 256) {
+    sp[k] = perm[k];
+    sro[k] = int32_t(rmul[k]) | (int32_t(off[k]) << 16);
+    if (k < main0) swx[k] = wx[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  bool bad = false;
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < n; row += int64_t(gridDim.x) * 4) {
+    const double* xr = X + row * ld;
+    int32_t* qr = reinterpret_cast<int32_t*>(Q + row * int64_t(kq));
+    int32_t nacc = 0;
+    double wacc = 0.0;
+    for (int w = lane; w < kq / 4; w += 64) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int k = 4 * w + b;
+        const int j = sp[k];
+        int qq = 0;
+        if (j >= 0) {
+          const int32_t ro = sro[k];
+          const double rk = double(ro & 0xFFFF), ok = double(ro >> 16);
+          const double v = xr[j] * rk;
+          const double q = rint(v);
+          bad |= !(fabs(v - q) <= 64.0 * __DBL_EPSILON__ * fmax(1.0, rk)) || q < 0.0 || q > 255.0;
+          qq = int(q - ok);
+          if (k >= main0)
+            nacc += qq * qq;
+          else
+            wacc += swx[k] * double(qq * qq);
+        }
+        word |= uint32_t(uint8_t(int8_t(qq))) << (8 * b);
+      }
+      qr[w] = int32_t(word);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o, kWave);
+    wacc = wave_sum(wacc);
+    if (lane == 0) {
+      N0[row] = nacc;
+      WN[row] = wacc;
+    }
+  }
+  if (__any(bad) && lane == 0) atomicOr(fail, 1u);
+}
+
 // ---- exp over a batch of lanes' values, bit-identical to the device libm exp (same operation
 // sequence: x*log2e, round-to-even, two-part ln2 reduction, degree-11 polynomial in 12 FMAs,
 // ldexp, overflow/underflow clamps).  Evaluating B values per coefficient lets one VGPR copy of
@@ -484,7 +545,13 @@ int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const Q
   SVMD_CHECK(hipMemcpyAsync(off, P.off.data(), P.off.size() * 8, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemcpyAsync(wx, P.wx.data(), P.wx.size() * 8, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemsetAsync(fail, 0, 4, s));
-  if (n > 0) {
+  if (n > 0 && P.kq <= kQuantLdsMaxKq) {
+    const size_t lds = size_t(P.kq) * 8 + size_t(P.main0) * 8;
+    const unsigned blocks = unsigned(std::min<int64_t>((n + 3) / 4, 2048));
+    hipLaunchKernelGGL(quantize_rows_lds_kernel, dim3(blocks), dim3(256), lds, s, X, n, ld, perm, rmul, off, wx,
+                       P.main0, P.kq, Q, N0, WN, fail);
+    SVMD_LAUNCH_CHECK();
+  } else if (n > 0) {
     hipLaunchKernelGGL(quantize_rows_kernel, dim3(unsigned((n + 3) / 4)), dim3(256), 0, s, X, n, ld, perm, rmul, off,
                        wx, P.main0, P.kq, Q, N0, WN, fail);
     SVMD_LAUNCH_CHECK();

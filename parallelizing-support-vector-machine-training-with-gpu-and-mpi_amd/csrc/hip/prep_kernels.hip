@@ -51,7 +51,22 @@ __global__ __launch_bounds__(256) void minmax_final_kernel(const double* __restr
   const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= d) return;
   double lo = pmin[c], hi = pmax[c];
-  for (int p = 1; p < parts; ++p) {
+  // 8 partials' loads in flight ahead of the in-order folds (same order, same result)
+  int p = 1;
+  for (; p + 8 <= parts; p += 8) {
+    double a[8], z[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = pmin[int64_t(p + u) * d + c];
+      z[u] = pmax[int64_t(p + u) * d + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      lo = fmin(lo, a[u]);
+      hi = fmax(hi, z[u]);
+    }
+  }
+  for (; p < parts; ++p) {
     lo = fmin(lo, pmin[int64_t(p) * d + c]);
     hi = fmax(hi, pmax[int64_t(p) * d + c]);
   }
