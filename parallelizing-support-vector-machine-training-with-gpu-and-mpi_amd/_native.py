@@ -191,6 +191,10 @@ _HIP_SIGS = {
     "svmd_decision_int": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, c_int64, c_double, _P,
                                     POINTER(c_int32)]),
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
+    "svmd_train_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, _P, _P, c_int32, POINTER(SvmParams),
+                                POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming), POINTER(c_int32)]),
+    "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
+    "svmd_sv_rows_u8": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P]),
     "svmd_count_correct": (c_int32, [c_void_p, _P, _P, c_int64, c_int32, POINTER(c_int64)]),
     "svmd_cascade_group_create": (c_void_p, [c_int32, c_char_p, c_double]),
     "svmd_cascade_group_world": (c_int32, [c_void_p]),

@@ -447,6 +447,88 @@ SVM_API int svmd_train_q(void* h, const double* X_d, const double* sqn_d, int64_
                     d, gram_mode, gram_used);
 }
 
+// Training straight from uint8 pixel rows (n x d contiguous, device): the exact-integer Gram is
+// quantised from the bytes (no FP64 rows), then the SMO.  mn_h / mx_h: the rows' column min / max
+// (svmd_minmax_u8).  *used = 0 and nothing trained when the plan does not apply (the caller then
+// takes the FP64-row path); K: n x ldk Gram storage.  Same Gram, trajectory and result as
+// svmd_train_q on the scaled FP64 rows.
+SVM_API int svmd_train_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                          const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
+                          double* K_d, int64_t ldk, svmd_timing* timing, int32_t* used_out) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!Xu_d || n <= 0 || d <= 0 || !mn_h || !mx_h || !K_d || ldk < n) {
+    set_error("svmd_train_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  const svm_params q = resolve(p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ctx->begin();
+  if (rc) return rc;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P)) return ctx->end();
+  bool used = false;
+  {
+    TraceRange tr("svm355:gram");
+    rc = ctx->ensure_ws(igram_u8_workspace(n, P));
+    if (rc) return rc;
+    rc = run_igram_u8(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, q.gamma, K_d, ldk, ctx->ws, &used);
+    if (rc) return rc;
+  }
+  if (!used) return ctx->end();
+  if (timing) SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+  const double t_gram = ms_since(t0);
+  {
+    TraceRange ts("svm355:smo");
+    rc = run_smo(ctx, K_d, ldk, y_d, n, alpha_d, warm, q, r, nullptr, 0);
+  }
+  if (!rc && r) {
+    int64_t c = 0;
+    rc = count_sv(ctx, alpha_d, n, 1, q.sv_tol, &c);
+    if (!rc) r->n_sv = c;
+  }
+  if (rc) return rc;
+  if (timing) {
+    timing->gram_ms = t_gram;
+    timing->total_ms = ms_since(t0);
+    timing->smo_ms = timing->total_ms - t_gram;
+  }
+  if (used_out) *used_out = 1;
+  return ctx->end();
+}
+
+SVM_API int svmd_minmax_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d) {
+  SVMD_CTX(h);
+  if (n <= 0 || d <= 0 || !Xu_d || !mn_d || !mx_d) {
+    set_error("svmd_minmax_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  TraceRange tr("svm355:preprocess");
+  int rc = ctx->begin();
+  if (rc) return rc;
+  const size_t scratch = size_t(2) * size_t(d) * 2048;
+  rc = ctx->ensure_ws(scratch * 8);
+  if (rc) return rc;
+  rc = launch_minmax_u8(ctx->stream, Xu_d, n, d, mn_d, mx_d, static_cast<double*>(ctx->ws), scratch);
+  if (rc) return rc;
+  return ctx->end();
+}
+
+// Scaled FP64 rows idx[0..k) (k x ld, zero padded) and their squared norms from uint8 pixel rows.
+SVM_API int svmd_sv_rows_u8(void* h, const uint8_t* Xu_d, int64_t d, const int64_t* idx_d, int64_t k,
+                            const double* mn_d, const double* mx_d, double* out_d, int64_t ld, double* sqn_d) {
+  SVMD_CTX(h);
+  if (k < 0 || d <= 0 || ld < d || (k && (!Xu_d || !idx_d || !mn_d || !mx_d || !out_d || !sqn_d))) {
+    set_error("svmd_sv_rows_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  rc = launch_sv_rows_u8(ctx->stream, Xu_d, d, idx_d, k, mn_d, mx_d, out_d, ld, sqn_d);
+  if (rc) return rc;
+  return ctx->end();
+}
+
 SVM_API int svmd_train_rows(void* h, const double* X_d, const double* sqn_d, int64_t n, int64_t ld, int64_t d,
                             const int32_t* y_d, double* alpha_d, int32_t warm, const svm_params* p, svm_result* r,
                             const double* mn_h, const double* mx_h, int32_t gram_mode, int64_t cache_bytes,

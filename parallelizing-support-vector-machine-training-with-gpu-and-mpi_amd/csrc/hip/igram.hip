@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(
 // workgroup walking many rows: the per-element table loads of quantize_rows_kernel become LDS reads.
 // Every lane handles the same k in the same order with the same arithmetic, so N0 / WN / Q are
 // bit-identical.  kq <= kQuantLdsMaxKq.
-constexpr int kQuantLdsMaxKq = 2048;
+constexpr int kQuantLdsMaxKq = 32 * kMaxSteps;  // tables <= 64 KB of LDS
 __global__ __launch_bounds__(256) void quantize_rows_lds_kernel(
     const double* __restrict__ X, int64_t n, int64_t ld, const int32_t* __restrict__ perm,
     const double* __restrict__ rmul, const double* __restrict__ off, const double* __restrict__ wx, int main0,
@@ -142,6 +142,64 @@ __global__ __launch_bounds__(256) void quantize_rows_lds_kernel(
           const double q = rint(v);
           bad |= !(fabs(v - q) <= 64.0 * __DBL_EPSILON__ * fmax(1.0, rk)) || q < 0.0 || q > 255.0;
           qq = int(q - ok);
+          if (k >= main0)
+            nacc += qq * qq;
+          else
+            wacc += swx[k] * double(qq * qq);
+        }
+        word |= uint32_t(uint8_t(int8_t(qq))) << (8 * b);
+      }
+      qr[w] = int32_t(word);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o, kWave);
+    wacc = wave_sum(wacc);
+    if (lane == 0) {
+      N0[row] = nacc;
+      WN[row] = wacc;
+    }
+  }
+  if (__any(bad) && lane == 0) atomicOr(fail, 1u);
+}
+
+// Quantisation straight from the uint8 pixel rows (n x d, contiguous) -- no FP64 rows at all.  For a
+// column j of range r_j in a group of range R (r_j divides R), the FP64 path rounds
+// ((p - mn_j) / r_j) * R to the integer (p - mn_j) * (R / r_j); this kernel forms that integer
+// directly, so Q, N0 and WN are bit-identical (same k per lane, same accumulation order).  Tables:
+// perm, one packed int32 per k (mn_j | R / r_j << 8 | offset << 16), the extra-group weights.
+__global__ __launch_bounds__(256) void quantize_u8_lds_kernel(
+    const uint8_t* __restrict__ Xu, int64_t n, int64_t d, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ pack, const double* __restrict__ wx, int main0, int kq, int8_t* __restrict__ Q,
+    int32_t* __restrict__ N0, double* __restrict__ WN, unsigned* __restrict__ fail) {
+  extern __shared__ __attribute__((aligned(16))) char qsm[];
+  int32_t* sp = reinterpret_cast<int32_t*>(qsm);
+  int32_t* spk = sp + kq;
+  double* swx = reinterpret_cast<double*>(spk + kq);
+  for (int k = threadIdx.x; k < kq; k += 256) {
+    sp[k] = perm[k];
+    spk[k] = pack[k];
+    if (k < main0) swx[k] = wx[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  bool bad = false;
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < n; row += int64_t(gridDim.x) * 4) {
+    const uint8_t* xr = Xu + row * d;
+    int32_t* qr = reinterpret_cast<int32_t*>(Q + row * int64_t(kq));
+    int32_t nacc = 0;
+    double wacc = 0.0;
+    for (int w = lane; w < kq / 4; w += 64) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int k = 4 * w + b;
+        const int j = sp[k];
+        int qq = 0;
+        if (j >= 0) {
+          const int32_t pk = spk[k];
+          const int q = (int(xr[j]) - (pk & 0xFF)) * ((pk >> 8) & 0xFF);
+          bad |= q < 0 || q > 255;
+          qq = q - (pk >> 16);
           if (k >= main0)
             nacc += qq * qq;
           else
@@ -595,6 +653,16 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
   int rc = quantize_rows(s, X, n, ld, P, p, Q, N0, WN, &ok);
   if (rc) return rc;
   if (!ok) return SVM_OK;  // not integer-valued: caller uses the FP64 path
+  rc = launch_igram_sym(s, Q, N0, WN, stw, n, P, gamma, K, ldk);
+  if (rc) return rc;
+  *used = true;
+  return SVM_OK;
+}
+
+// The symmetric exact-integer Gram of quantised rows (Q, N0, WN); stw: device scratch for the step
+// weights.
+int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, double* stw, int64_t n,
+                     const QuantPlan& P, double gamma, double* K, int64_t ldk) {
   SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
   const int64_t tiles = (n + QBM - 1) / QBM;
   const int64_t nwg = tiles * (tiles + 1);  // two 128x64 halves per upper-triangular 128x128 tile
@@ -614,8 +682,68 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
   }
 #undef SVM_IGRAM
   SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
+
+// run_igram on uint8 pixel rows Xu (n x d, contiguous, device) whose column min / max (host, d
+// values) the plan was built from: quantised without FP64 rows.  *used = false (nothing written)
+// when the plan does not apply to these statistics (non-integer minima or ranges).
+int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                 const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used) {
+  *used = false;
+  if (!P.ok || n <= 0 || P.kq > kQuantLdsMaxKq) return SVM_OK;
+  if (ldk < n) {
+    set_error("igram: ldk < n");
+    return SVM_ERR_ARG;
+  }
+  std::vector<int32_t> pack(P.perm.size(), 0);
+  for (size_t k = 0; k < P.perm.size(); ++k) {
+    const int32_t j = P.perm[k];
+    if (j < 0) continue;
+    const double mn = mn_h[j], rj = mx_h[j] - mn_h[j], fac = P.rmul[k] / rj;
+    if (mn != std::floor(mn) || mn < 0 || mn > 255 || fac != std::floor(fac) || fac < 1 || fac > 255 ||
+        P.off[k] > 255)
+      return SVM_OK;
+    pack[k] = int32_t(mn) | (int32_t(fac) << 8) | (int32_t(P.off[k]) << 16);
+  }
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
+  auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
+  auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
+  auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
+  auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
+  auto* perm = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
+  auto* pk = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
+  auto* wx = reinterpret_cast<double*>(take(P.wx.size() * 8));
+  auto* fail = reinterpret_cast<unsigned*>(take(4));
+  SVMD_CHECK(hipMemcpyAsync(perm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(pk, pack.data(), pack.size() * 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(wx, P.wx.data(), P.wx.size() * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemsetAsync(fail, 0, 4, s));
+  const size_t lds = size_t(P.kq) * 8 + size_t(P.main0) * 8;
+  const unsigned blocks = unsigned(std::min<int64_t>((n + 3) / 4, 2048));
+  hipLaunchKernelGGL(quantize_u8_lds_kernel, dim3(blocks), dim3(256), lds, s, Xu, n, d, perm, pk, wx, P.main0, P.kq,
+                     Q, N0, WN, fail);
+  SVMD_LAUNCH_CHECK();
+  unsigned hfail = 1;
+  SVMD_CHECK(hipMemcpyAsync(&hfail, fail, 4, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  if (hfail) return SVM_OK;
+  int rc = launch_igram_sym(s, Q, N0, WN, stw, n, P, gamma, K, ldk);
+  if (rc) return rc;
   *used = true;
   return SVM_OK;
+}
+
+size_t igram_u8_workspace(int64_t n, const QuantPlan& P) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  return al(size_t(n) * size_t(P.kq)) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
+         2 * al(P.perm.size() * 4) + al(P.wx.size() * 8) + 256;
 }
 
 // K(rows [0, n), rows [0, ncols)) of the same (scaled) rows on the exact-integer path, ncols <= n,

@@ -120,7 +120,94 @@ __global__ __launch_bounds__(256) void widen_u8_kernel(const uint8_t* __restrict
   }
 }
 
+// minmax_partial_kernel on uint8 pixel rows (n x d contiguous): min / max of the widened values are
+// the widened min / max, so the statistics equal those of the FP64 rows exactly.
+__global__ __launch_bounds__(256) void minmax_u8_partial_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
+                                                                double* __restrict__ pmin, double* __restrict__ pmax) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = int64_t(blockIdx.x) * kColsPerBlock + lane;
+  const int64_t rstride = int64_t(gridDim.y) * kRowLanes;
+  int lo = 255, hi = 0;
+  bool any = false;
+  if (c < d) {
+    for (int64_t r = int64_t(blockIdx.y) * kRowLanes + wv; r < n; r += rstride) {
+      const int v = X[r * d + c];
+      lo = min(lo, v);
+      hi = max(hi, v);
+      any = true;
+    }
+  }
+  __shared__ int smin[kRowLanes][kColsPerBlock], smax[kRowLanes][kColsPerBlock];
+  __shared__ bool sany[kRowLanes][kColsPerBlock];
+  smin[wv][lane] = lo;
+  smax[wv][lane] = hi;
+  sany[wv][lane] = any;
+  __syncthreads();
+  if (wv == 0 && c < d) {
+#pragma unroll
+    for (int w = 1; w < kRowLanes; ++w) {
+      lo = min(lo, smin[w][lane]);
+      hi = max(hi, smax[w][lane]);
+      any = any || sany[w][lane];
+    }
+    pmin[int64_t(blockIdx.y) * d + c] = any ? double(lo) : __builtin_inf();
+    pmax[int64_t(blockIdx.y) * d + c] = any ? double(hi) : -__builtin_inf();
+  }
+}
+
+// Scaled FP64 rows idx[0..k) of uint8 pixel rows, zero padded to ld, and their squared norms: the
+// widen + scale_norm arithmetic per row (same per-lane column order, same wave_sum), so the rows and
+// norms equal those of the scaled FP64 matrix bit for bit.  One wave per output row.
+__global__ __launch_bounds__(256) void sv_rows_u8_kernel(const uint8_t* __restrict__ X, int64_t d,
+                                                         const int64_t* __restrict__ idx, int64_t k,
+                                                         const double* __restrict__ mn, const double* __restrict__ mx,
+                                                         double* __restrict__ out, int64_t ld, double* __restrict__ sqn) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= k) return;
+  const uint8_t* xr = X + idx[row] * d;
+  double* o = out + row * ld;
+  double acc = 0.0;
+  for (int64_t c = lane; c < d; c += 64) {
+    double range = mx[c] - mn[c];
+    if (range < 1e-12) range = 1.0;
+    const double v = (double(xr[c]) - mn[c]) / range;
+    o[c] = v;
+    acc += v * v;
+  }
+  for (int64_t c = d + lane; c < ld; c += 64) o[c] = 0.0;
+  acc = wave_sum(acc);
+  if (lane == 0) sqn[row] = acc;
+}
+
 }  // namespace
+
+int launch_minmax_u8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, double* mn, double* mx, double* scratch,
+                     size_t scratch_doubles) {
+  const int gx = int((d + kColsPerBlock - 1) / kColsPerBlock);
+  int parts = int(std::min<int64_t>((n + kRowLanes - 1) / kRowLanes, std::max(1, 2048 / gx)));
+  parts = int(std::min<int64_t>(parts, int64_t(scratch_doubles / size_t(2 * d))));
+  if (parts < 1) {
+    set_error("launch_minmax_u8: scratch too small");
+    return SVM_ERR_INTERNAL;
+  }
+  double* pmin = scratch;
+  double* pmax = scratch + size_t(parts) * size_t(d);
+  hipLaunchKernelGGL(minmax_u8_partial_kernel, dim3(gx, parts), dim3(256), 0, s, X, n, d, pmin, pmax);
+  SVMD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(minmax_final_kernel, dim3(int((d + 255) / 256)), dim3(256), 0, s, pmin, pmax, parts, d, mn, mx);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
+
+int launch_sv_rows_u8(hipStream_t s, const uint8_t* X, int64_t d, const int64_t* idx, int64_t k, const double* mn,
+                      const double* mx, double* out, int64_t ld, double* sqn) {
+  if (k <= 0) return SVM_OK;
+  hipLaunchKernelGGL(sv_rows_u8_kernel, dim3(unsigned((k + 3) / 4)), dim3(256), 0, s, X, d, idx, k, mn, mx, out, ld,
+                     sqn);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
 
 int launch_widen_u8(hipStream_t s, const uint8_t* src, int64_t n, int64_t d, int64_t ld, double* dst) {
   if (n <= 0) return SVM_OK;

@@ -43,6 +43,15 @@ SVM_API void svmd_destroy(void* ctx);
 SVM_API int svmd_release_cache(void* ctx);
 // Size the context-owned Gram for an n-row solve ahead of it (SVM_ERR_OOM if it does not fit).
 SVM_API int svmd_reserve_gram(void* ctx, int64_t n);
+// Exact-integer training straight from uint8 pixel rows (n x d contiguous, device): *used = 0 and
+// nothing done when the rows' statistics do not admit the integer plan (use the FP64-row path).
+SVM_API int svmd_train_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                          const double* mx_h, const int32_t* y_d, double* alpha_d, int32_t warm,
+                          const svm_params* p, svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing,
+                          int32_t* used);
+SVM_API int svmd_minmax_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d);
+SVM_API int svmd_sv_rows_u8(void* ctx, const uint8_t* Xu_d, int64_t d, const int64_t* idx_d, int64_t k,
+                            const double* mn_d, const double* mx_d, double* out_d, int64_t ld, double* sqn_d);
 // Self-test of the Gram epilogue's exp: lib_d[i] = device libm exp(x_d[i]), batch_d[i] = the
 // batched evaluation the Gram kernel uses (they must agree bit for bit).
 SVM_API int svmd_selftest_exp(void* ctx, const double* x_d, int64_t n, double* lib_d, double* batch_d);

@@ -107,6 +107,9 @@ class SVC:
         from ..ops import device as D
 
         device = torch.device(dev)
+        if (X.dtype == np.uint8 and self.scale and self.gram in ("auto", "int") and self.kcache in ("auto", "full")
+                and os.environ.get("SVM355_U8_TRAIN", "1") != "0" and self._fit_cuda_u8(X, y, alpha0, device)):
+            return
         t0 = time.perf_counter()
         Xd = D.upload_rows(X, device)
         yd = torch.from_numpy(y).to(device)
@@ -142,6 +145,42 @@ class SVC:
             self.scaler_ = None
         self._sv_host = None  # scaled SV rows stay on the device; copied to the host on first access
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
+
+    def _fit_cuda_u8(self, X, y, alpha0, device) -> bool:
+        """uint8 pixel rows, resident Gram: the rows stay bytes on the device -- min/max, the exact-integer
+        quantisation and the Gram read them directly, and only the support vectors are ever widened
+        to scaled FP64 (for prediction).  Same Gram, trajectory and model as the FP64-row path, minus
+        its widen / scale / FP64-quantise passes.  False (nothing fitted) when it does not apply."""
+        import torch
+
+        from ..ops import device as D
+
+        n, d = X.shape
+        if self.kcache == "auto" and not D.gram_fits(n, device):
+            return False
+        t0 = time.perf_counter()
+        Xu = D.upload_u8(X, device)
+        yd = torch.from_numpy(y).to(device)
+        mn, mx = D.minmax_u8(Xu)
+        if alpha0 is not None:
+            alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
+        else:
+            alpha = torch.zeros(n, dtype=torch.float64, device=device)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        out = D.train_u8(Xu, yd, alpha, self.params, mn, mx, warm=alpha0 is not None)
+        if out is None:
+            return False
+        res, tm = out
+        self._finish(alpha.cpu().numpy(), y, res)
+        idx = torch.from_numpy(self.support_).to(device)
+        Xs, ns = D.sv_rows_u8(Xu, idx, mn, mx)
+        self._dev = {"Xs": Xs, "ns": ns, "coef": torch.from_numpy(self.dual_coef_).to(device), "mn": mn, "mx": mx,
+                     "d": d, "device": device}
+        self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
+        self._sv_host = None
+        self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
+        return True
 
     @property
     def support_vectors_(self) -> np.ndarray:

@@ -335,6 +335,66 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
                                       "gram_alloc_ms": alloc_ms, "kcache": "full", "gram_path": "int8-exact" if used.value else "fp64"}
 
 
+# ---- the byte path of SVC.fit for uint8 pixel rows: no FP64 copy of the training rows at all
+def upload_u8(X: np.ndarray, device) -> torch.Tensor:
+    """Host uint8 pixel rows (n, d) -> the same bytes on the device (n, d) uint8."""
+    X = np.ascontiguousarray(X, dtype=np.uint8)
+    out = torch.empty(X.shape, dtype=torch.uint8, device=device)
+    ctx = DeviceContext.get(out.device)
+    N.check(ctx.lib.svmd_memcpy_h2d(ctx.bind(), N.ptr(out), N.ptr(X), X.nbytes), "svmd_memcpy_h2d")
+    return out
+
+
+def minmax_u8(Xu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Column min / max (FP64) of device uint8 rows: equal to those of the widened FP64 rows."""
+    n, d = Xu.shape
+    mn = torch.empty(d, dtype=torch.float64, device=Xu.device)
+    mx = torch.empty(d, dtype=torch.float64, device=Xu.device)
+    ctx = _ctx_for(Xu)
+    N.check(ctx.lib.svmd_minmax_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(mn), N.ptr(mx)), "svmd_minmax_u8")
+    return mn, mx
+
+
+def train_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn: torch.Tensor,
+             mx: torch.Tensor, warm: bool = False) -> Optional[Tuple[SMOResult, dict]]:
+    """Exact-integer Gram quantised straight from the bytes + SMO (svmd_train_u8): the same Gram,
+    trajectory and result as ``train`` on the scaled FP64 rows.  None when the integer plan does not
+    apply (the caller takes the FP64-row path)."""
+    import time as _t
+
+    n, d = Xu.shape
+    ctx = _ctx_for(Xu)
+    a, b, _ = _host_stats(mn, mx)
+    ta = _t.perf_counter()
+    K = gram_buffer(n, Xu.device)
+    alloc_ms = (_t.perf_counter() - ta) * 1e3
+    r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_train_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(a), N.ptr(b), N.ptr(y), N.ptr(alpha), int(warm),
+                                  ctypes.byref(p), ctypes.byref(r), N.ptr(K), K.stride(0), ctypes.byref(tm),
+                                  ctypes.byref(used)), "svmd_train_u8")
+    if not used.value:
+        return None
+    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
+                                      "gram_alloc_ms": alloc_ms, "kcache": "full", "gram_path": "int8-exact",
+                                      "rows": "uint8"}
+
+
+def sv_rows_u8(Xu: torch.Tensor, idx: torch.Tensor, mn: torch.Tensor, mx: torch.Tensor,
+               ld: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Scaled FP64 rows idx (zero padded to ld) and their squared norms from device uint8 rows."""
+    d = Xu.shape[1]
+    ld = padded_dim(d) if ld is None else ld
+    idx = idx.to(torch.int64).contiguous()
+    k = idx.numel()
+    out = torch.empty((k, ld), dtype=torch.float64, device=Xu.device)
+    sqn = torch.empty(k, dtype=torch.float64, device=Xu.device)
+    ctx = _ctx_for(Xu)
+    N.check(ctx.lib.svmd_sv_rows_u8(ctx.bind(), N.ptr(Xu), d, N.ptr(idx) if k else None, k, N.ptr(mn), N.ptr(mx),
+                                    N.ptr(out), ld, N.ptr(sqn)), "svmd_sv_rows_u8")
+    return out, sqn
+
+
 def rbf_gram_sym(X: torch.Tensor, sqn: Optional[torch.Tensor], gamma: float, mn=None, mx=None,
                  gram: str = "auto", out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, str]:
     """Symmetric RBF Gram of preprocessed rows with the svmd_train_q path selection.

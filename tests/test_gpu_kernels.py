@@ -474,6 +474,24 @@ def test_svc_u8_rows_bit_identical_to_fp64_rows(dev, mn_data):
     np.testing.assert_array_equal(a.decision_function(te.compact().X), b.decision_function(te.X))
 
 
+def test_svc_byte_path_equals_fp64_row_path(dev, mn_data, monkeypatch):
+    """uint8 rows take the byte path (min/max, quantisation and Gram straight from the bytes, only the
+    SVs widened; SVC._fit_cuda_u8); with SVM355_U8_TRAIN=0 the same rows go through the FP64-row path.
+    The models -- alphas, b, SV rows and norms, decisions -- must be identical bit for bit."""
+    tr, te = mn_data
+    Xc = tr.compact().X
+    a = SVC(device="cuda:0").fit(Xc, tr.y)
+    assert a.timings_.get("rows") == "uint8" and a.timings_["gram_path"] == "int8-exact"
+    monkeypatch.setenv("SVM355_U8_TRAIN", "0")
+    b = SVC(device="cuda:0").fit(Xc, tr.y)
+    assert "rows" not in b.timings_
+    assert a.b_ == b.b_ and a.n_iter_ == b.n_iter_
+    np.testing.assert_array_equal(a.alpha_, b.alpha_)
+    assert torch.equal(a._dev["Xs"], b._dev["Xs"]) and torch.equal(a._dev["ns"], b._dev["ns"])
+    assert torch.equal(a._dev["mn"], b._dev["mn"]) and torch.equal(a._dev["mx"], b._dev["mx"])
+    np.testing.assert_array_equal(a.decision_function(te.compact().X), b.decision_function(te.compact().X))
+
+
 # ---------------------------------------------------------------- on-demand row cache (rowcache.hip)
 @pytest.mark.parametrize("cache_rows", [6, 64, 100000])
 def test_row_cache_smo_bit_identical_to_full_gram(dev, D, cache_rows):
