@@ -249,6 +249,7 @@ def test_headline_shape_60k_default_solver_equals_graph_replay(dev, D, monkeypat
     m = SVC(device="cuda:0").fit(tr.X, tr.y)
     assert m.n_iter_ == r1.iterations and m.b_ == r1.b
     assert m.timings_["gram_path"] == "int8-exact" and m.timings_["kcache"] == "full"
+    assert m.timings_.get("rows") == "uint8"  # bench.py's byte path (SVC._fit_cuda_u8)
 
 
 def test_device_smo_warm_start_bit_identical(dev, D, mn_data):
