@@ -166,9 +166,10 @@ class SVC:
             alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
         else:
             alpha = torch.zeros(n, dtype=torch.float64, device=device)
-        torch.cuda.synchronize(device)
+        mm = torch.cat([mn, mx]).cpu().numpy()  # one D2H (synchronises) for the plan and the scaler
+        mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
         t1 = time.perf_counter()
-        out = D.train_u8(Xu, yd, alpha, self.params, mn, mx, warm=alpha0 is not None)
+        out = D.train_u8(Xu, yd, alpha, self.params, mn_h, mx_h, warm=alpha0 is not None)
         if out is None:
             return False
         res, tm = out
@@ -177,7 +178,7 @@ class SVC:
         Xs, ns = D.sv_rows_u8(Xu, idx, mn, mx)
         self._dev = {"Xs": Xs, "ns": ns, "coef": torch.from_numpy(self.dual_coef_).to(device), "mn": mn, "mx": mx,
                      "d": d, "device": device}
-        self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
+        self.scaler_ = MinMaxScaler(mn_h, mx_h)
         self._sv_host = None
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
         return True
