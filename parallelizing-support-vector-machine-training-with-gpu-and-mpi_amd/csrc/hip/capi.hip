@@ -497,6 +497,30 @@ SVM_API int svmd_train_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, co
   return ctx->end();
 }
 
+// The exact-integer RBF Gram of uint8 pixel rows (n x d contiguous, device) straight from the bytes,
+// into K (n x ldk).  *used = 0 (nothing written) when the statistics do not admit the integer plan.
+SVM_API int svmd_rbf_gram_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                             const double* mx_h, double gamma, double* K_d, int64_t ldk, int32_t* used_out) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!Xu_d || n <= 0 || d <= 0 || !mn_h || !mx_h || !K_d || ldk < n) {
+    set_error("svmd_rbf_gram_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  TraceRange tr("svm355:gram");
+  int rc = ctx->begin();
+  if (rc) return rc;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P)) return ctx->end();
+  rc = ctx->ensure_ws(igram_u8_workspace(n, P));
+  if (rc) return rc;
+  bool used = false;
+  rc = run_igram_u8(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, gamma, K_d, ldk, ctx->ws, &used);
+  if (rc) return rc;
+  if (used_out) *used_out = used ? 1 : 0;
+  return ctx->end();
+}
+
 SVM_API int svmd_minmax_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d) {
   SVMD_CTX(h);
   if (n <= 0 || d <= 0 || !Xu_d || !mn_d || !mx_d) {

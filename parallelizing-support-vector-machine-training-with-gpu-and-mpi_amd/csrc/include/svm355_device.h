@@ -50,6 +50,8 @@ SVM_API int svmd_train_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, 
                           const svm_params* p, svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing,
                           int32_t* used);
 SVM_API int svmd_minmax_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d);
+SVM_API int svmd_rbf_gram_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                             const double* mx_h, double gamma, double* K_d, int64_t ldk, int32_t* used);
 SVM_API int svmd_sv_rows_u8(void* ctx, const uint8_t* Xu_d, int64_t d, const int64_t* idx_d, int64_t k,
                             const double* mn_d, const double* mx_d, double* out_d, int64_t ld, double* sqn_d);
 // Self-test of the Gram epilogue's exp: lib_d[i] = device libm exp(x_d[i]), batch_d[i] = the

@@ -22,6 +22,7 @@ dependency inside a solve.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List, Optional
 
@@ -131,13 +132,26 @@ class OneVsRestSVC:
 
         device = torch.device(self._dev())
         t0 = time.perf_counter()
-        Xd = D.upload_rows(X, device)
         d = X.shape[1]
-        mn, mx, sqn = D.minmax_scale_(Xd, d)
-        torch.cuda.synchronize(device)
-        t1 = time.perf_counter()
-        K, path = D.rbf_gram_sym(Xd, sqn, self.params.gamma, mn=mn, mx=mx, gram=self.gram,
-                                 out=D.gram_buffer(X.shape[0], device))
+        Xu = K = None
+        if X.dtype == np.uint8 and self.gram in ("auto", "int") and os.environ.get("SVM355_U8_TRAIN", "1") != "0":
+            # byte path (as SVC._fit_cuda_u8): min/max, quantisation and Gram from the device bytes
+            Xu = D.upload_u8(X, device)
+            mn, mx = D.minmax_u8(Xu)
+            mm = torch.cat([mn, mx]).cpu().numpy()
+            mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
+            t1 = time.perf_counter()
+            K = D.rbf_gram_u8(Xu, self.params.gamma, mn_h, mx_h, out=D.gram_buffer(X.shape[0], device))
+            path = "int8-exact"
+        if K is None:
+            Xu = None
+            t0 = time.perf_counter()
+            Xd = D.upload_rows(X, device)
+            mn, mx, sqn = D.minmax_scale_(Xd, d)
+            torch.cuda.synchronize(device)
+            t1 = time.perf_counter()
+            K, path = D.rbf_gram_sym(Xd, sqn, self.params.gamma, mn=mn, mx=mx, gram=self.gram,
+                                     out=D.gram_buffer(X.shape[0], device))
         torch.cuda.synchronize(device)
         t2 = time.perf_counter()
         n = X.shape[0]
@@ -187,7 +201,8 @@ class OneVsRestSVC:
         sup = np.flatnonzero((a > self.params.sv_tol).any(0)).astype(np.int64)
         self._finish(sup, (a * Y).T, bs, iters, stops)
         idx = torch.from_numpy(self.support_).to(device)
-        self._dev_model = {"Xs": D.gather_rows(Xd, idx), "ns": sqn[idx].contiguous(),
+        Xs, ns = D.sv_rows_u8(Xu, idx, mn, mx) if Xu is not None else (D.gather_rows(Xd, idx), sqn[idx].contiguous())
+        self._dev_model = {"Xs": Xs, "ns": ns,
                            "coef": torch.from_numpy(np.ascontiguousarray(self.dual_coef_)).to(device),
                            "b": torch.tensor(self.intercepts_b_, dtype=torch.float64, device=device),
                            "mn": mn, "mx": mx, "d": d, "device": device}

@@ -380,6 +380,20 @@ def train_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVM
                                       "rows": "uint8"}
 
 
+def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Exact-integer RBF Gram straight from device uint8 rows (equal to ``rbf_gram_sym`` on the scaled
+    FP64 rows); None when the integer plan does not apply."""
+    n, d = Xu.shape
+    if out is None:
+        out = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=Xu.device)
+    a, b, _ = _host_stats(mn, mx)
+    used = ctypes.c_int32(0)
+    ctx = _ctx_for(Xu)
+    N.check(ctx.lib.svmd_rbf_gram_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(a), N.ptr(b), float(gamma), N.ptr(out),
+                                     out.stride(0), ctypes.byref(used)), "svmd_rbf_gram_u8")
+    return out if used.value else None
+
+
 def sv_rows_u8(Xu: torch.Tensor, idx: torch.Tensor, mn: torch.Tensor, mx: torch.Tensor,
                ld: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Scaled FP64 rows idx (zero padded to ld) and their squared norms from device uint8 rows."""

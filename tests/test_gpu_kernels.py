@@ -682,6 +682,26 @@ def test_ovr_batched_xcd_teams_equal_per_class_solves(dev, n):
     np.testing.assert_array_equal(b.dual_coef_, s.dual_coef_)
 
 
+def test_ovr_byte_path_equals_fp64_row_path(dev, monkeypatch):
+    """One-vs-rest on uint8 rows: the Gram straight from the device bytes (svmd_rbf_gram_u8) and SVs
+    widened alone give the FP64-row path's models bit for bit (SVM355_U8_TRAIN=0 forces the latter)."""
+    from svm355 import OneVsRestSVC
+
+    tr = synthetic_mnist(3000, seed=34)
+    te = synthetic_mnist(400, seed=34, offset=3000)
+    X = tr.compact().X
+    a = OneVsRestSVC(device="cuda:0").fit(X, tr.labels)
+    monkeypatch.setenv("SVM355_U8_TRAIN", "0")
+    b = OneVsRestSVC(device="cuda:0").fit(X, tr.labels)
+    assert a.timings_["gram_path"] == b.timings_["gram_path"] == "int8-exact"
+    np.testing.assert_array_equal(a.n_iter_, b.n_iter_)
+    np.testing.assert_array_equal(a.intercepts_b_, b.intercepts_b_)
+    np.testing.assert_array_equal(a.support_, b.support_)
+    np.testing.assert_array_equal(a.dual_coef_, b.dual_coef_)
+    assert torch.equal(a._dev_model["Xs"], b._dev_model["Xs"]) and torch.equal(a._dev_model["ns"], b._dev_model["ns"])
+    np.testing.assert_array_equal(a.predict(te.compact().X), b.predict(te.compact().X))
+
+
 def test_gram_epilogue_exp_is_bit_identical_to_libm(dev):
     """The Gram kernel's batched exp (SGPR-sourced FMAs, igram.hip exp_batch) must equal the device
     libm exp bit for bit, so the Gram -- and every SMO trajectory -- is unchanged by it."""
