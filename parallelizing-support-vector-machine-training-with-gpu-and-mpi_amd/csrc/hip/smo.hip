@@ -1379,7 +1379,7 @@ constexpr int kMultiTeams = 8;
 constexpr int kMultiQueue = 4 * kMultiTeams, kMultiErr = kMultiQueue + 1, kMultiCtlWords = 64;
 constexpr unsigned long long kMailTicks = 10000000ull;  // 100 ms: a team member gives up waiting for a class
 
-template <int NT, int E>
+template <int NT, int E, bool WSS2 = false>
 __global__ __launch_bounds__(NT) void smo_multi_kernel(
     const double* __restrict__ K, int64_t ldk, const int32_t* __restrict__ Y, double* __restrict__ A,
     double* __restrict__ F, int64_t n, int64_t slice, unsigned long long* __restrict__ slots,
@@ -1424,7 +1424,8 @@ __global__ __launch_bounds__(NT) void smo_multi_kernel(
     __syncthreads();
     const int cls = s_cls;
     if (cls >= nclass) break;
-    epoch = persist_solve<NT, E, false, true>(sh, glocal, g, epoch, ResidentRows{K, ldk}, Y + int64_t(cls) * n,
+    epoch = persist_solve<NT, E, false, true, ResidentRows, 1, WSS2>(sh, glocal, g, epoch, ResidentRows{K, ldk},
+                                                                     Y + int64_t(cls) * n,
                                               A + int64_t(cls) * n,
                                               F + int64_t(cls) * n, n, slice, tslots, st + cls, C, eps, tau, max_iter,
                                               nullptr, 0, err, spin_limit, nullptr);
@@ -2162,6 +2163,13 @@ void launch_multi_e(hipStream_t s, int grid, const double* K, int64_t ldk, const
                     int64_t n, unsigned long long* slots, SmoState* st, int nclass, const svm_params& p, unsigned* ctl,
                     int G) {
   const size_t lds = xcd_lds_pad(NT);
+  if (p.wss == 2) {  // opt-in second-order selection: the same persist_solve as the single-class solver
+    allow_lds(smo_multi_kernel<NT, E, true>, lds);
+    hipLaunchKernelGGL((smo_multi_kernel<NT, E, true>), dim3(grid), dim3(NT), lds, s, K, ldk, Y, A, F, n,
+                       int64_t(NT) * E, slots, st, nclass, p.C, p.eps, p.tau, p.max_iter, ctl, int64_t(1) << 22, G,
+                       register_ticks());
+    return;
+  }
   allow_lds(smo_multi_kernel<NT, E>, lds);
   hipLaunchKernelGGL((smo_multi_kernel<NT, E>), dim3(grid), dim3(NT), lds, s, K, ldk, Y, A, F, n, int64_t(NT) * E,
                      slots, st, nclass, p.C, p.eps, p.tau, p.max_iter, ctl, int64_t(1) << 22, G, register_ticks());
@@ -2180,7 +2188,6 @@ int run_smo_multi(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* Y
   int G = 0, E = 0, NT = 0;
   bool ok = nclass < 1000 && n < int64_t(kSentinel) && persistent_grid(n, &G, &E, &NT, kXcdMaxG);
   ok = ok && ((NT == 256 && E <= 2) || (NT == 512 && E <= 4));
-  ok = ok && p.wss != 2;  // second-order selection: per-class persistent solves
   if (const char* v = getenv("SVM355_SMO_MULTI"); v && atoi(v) == 0) ok = false;
   if (batched) *batched = 0;
   if (ok) {

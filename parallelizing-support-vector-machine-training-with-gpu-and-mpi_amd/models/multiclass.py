@@ -35,17 +35,21 @@ from ..utils.data import MinMaxScaler
 class OneVsRestSVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 gram: str = "auto", concurrent_solves: int = 8, solver: str = "auto"):
+                 gram: str = "auto", concurrent_solves: int = 8, solver: str = "auto", wss: str = "first"):
         """``solver``: "batched" (default via "auto") runs all class solves in ONE kernel launch, a team
         of workgroups per XCD pulling classes from a queue; "streams" runs one persistent solve per
-        class on ``concurrent_solves`` streams.  Results are identical either way."""
+        class on ``concurrent_solves`` streams.  Results are identical either way.  ``wss="second"``:
+        the opt-in second-order working-set selection (as ``SVC(wss="second")``) in every class solve."""
         if solver not in ("auto", "batched", "streams"):
             raise ValueError("solver must be auto, batched or streams")
+        if wss not in ("first", "second"):
+            raise ValueError("wss must be 'first' or 'second'")
         self.solver = solver
         self.concurrent_solves = concurrent_solves
         self._transport = None
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
-                                n_threads=n_threads if n_threads > 0 else default_threads())
+                                n_threads=n_threads if n_threads > 0 else default_threads(),
+                                wss=2 if wss == "second" else 1)
         self.device = device
         self.gram = gram
 

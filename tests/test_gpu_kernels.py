@@ -682,6 +682,23 @@ def test_ovr_batched_xcd_teams_equal_per_class_solves(dev, n):
     np.testing.assert_array_equal(b.dual_coef_, s.dual_coef_)
 
 
+def test_ovr_second_order_batched_equals_per_class_solves(dev):
+    """wss="second" in the batched one-launch solver (smo_multi_kernel<..., WSS2>) gives the per-class
+    second-order persistent solves' models bit for bit, in fewer iterations than first order."""
+    from svm355 import OneVsRestSVC
+
+    tr = synthetic_mnist(6000, seed=35)
+    X = tr.compact().X
+    b = OneVsRestSVC(device="cuda:0", solver="batched", wss="second").fit(X, tr.labels)
+    s = OneVsRestSVC(device="cuda:0", solver="streams", wss="second").fit(X, tr.labels)
+    f = OneVsRestSVC(device="cuda:0", solver="batched").fit(X, tr.labels)
+    assert b.timings_["smo_solver"] == "batched" and all(r == "converged" for r in b.stop_reasons_)
+    np.testing.assert_array_equal(b.n_iter_, s.n_iter_)
+    np.testing.assert_array_equal(b.intercepts_b_, s.intercepts_b_)
+    np.testing.assert_array_equal(b.dual_coef_, s.dual_coef_)
+    assert b.n_iter_.sum() < f.n_iter_.sum()
+
+
 def test_ovr_byte_path_equals_fp64_row_path(dev, monkeypatch):
     """One-vs-rest on uint8 rows: the Gram straight from the device bytes (svmd_rbf_gram_u8) and SVs
     widened alone give the FP64-row path's models bit for bit (SVM355_U8_TRAIN=0 forces the latter)."""
