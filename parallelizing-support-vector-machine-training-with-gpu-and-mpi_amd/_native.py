@@ -151,6 +151,8 @@ _CORE_SIGS = {
     "svm_cascade_free": (None, [POINTER(SvmCascadeOut)]),
     "svm_cascade_rank_fit_cpu": (POINTER(SvmCascadeOut), [_P, _P, _P, _P, c_int64, c_int64, c_int64,
                                                           POINTER(SvmCascadeCfg)]),
+    "svm_loopback_exercise": (c_int32, [c_int32, c_char_p, c_int32, c_double, POINTER(c_double)]),
+    "svm_preflight_script": (c_int32, [c_int32, c_int64, c_char_p, c_int64]),
 }
 
 _HIP_SIGS = {
@@ -174,6 +176,8 @@ _HIP_SIGS = {
     "svmd_smo": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
                            POINTER(SvmResult), _P, c_int64]),
     "svmd_release_cache": (c_int32, [c_void_p]),
+    "svmd_release_slab": (c_int32, [c_void_p]),
+    "svmd_cache_bytes": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),
     "svmd_selftest_exp": (c_int32, [c_void_p, _P, c_int64, _P, _P]),
     "svmd_smo_multi": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, c_int32, _P, POINTER(SvmParams),
                                  POINTER(SvmResult), POINTER(c_int32)]),
@@ -208,6 +212,10 @@ _HIP_SIGS = {
     "svmd_cascade_rank_fit": (POINTER(SvmCascadeOut), [c_void_p, _P, c_int32, _P, _P, c_int64, c_int64, c_int64,
                                                        POINTER(SvmCascadeCfg)]),
     "svmd_cascade_rank_barrier": (c_int32, [c_void_p]),
+    "svmd_cascade_group_exercise": (c_int32, [c_void_p, c_char_p, c_double]),
+    "svmd_cascade_rank_exercise": (c_int32, [c_void_p, c_char_p, c_double]),
+    "svmd_cascade_group_broken": (c_int32, [c_void_p]),
+    "svmd_rccl_info": (c_int32, [POINTER(c_int32), POINTER(c_int32), c_char_p, c_int64]),
     "svmd_cascade_rank_destroy": (None, [c_void_p]),
     "svmd_trace_push": (None, [c_char_p]),
     "svmd_trace_pop": (None, []),

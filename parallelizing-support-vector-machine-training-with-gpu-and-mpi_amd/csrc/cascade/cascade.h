@@ -211,25 +211,71 @@ class Transport {
 
 // P thread-ranks of one process exchanging through host memory (staged with the backend's copies),
 // so any P runs on one GPU (RCCL refuses two ranks on one device) or on the CPU.
+//
+// Strict mode (the default) holds every call sequence to RCCL's rules, so a sequence that would
+// deadlock or mismatch over RCCL fails here too, with both ranks named:
+//   * collectives: every rank records (op, root, bytes) before the first barrier of the call and
+//     every rank compares all records after it -- any difference throws TransportError on every rank;
+//   * send is a rendezvous (ncclSend completes once matched): it returns only when the peer's recv
+//     has taken the message, and a byte-count mismatch fails on both sides;
+//   * every wait checks the wait-for graph of the blocked ranks (a collective waits for the ranks
+//     that have not arrived, send / recv for the peer): a cycle is a deadlock and throws at once
+//     instead of at the deadline.
+// Non-strict mode (strict = false) keeps the old mailbox semantics (send returns after posting).
 class LoopbackGroup {
  public:
-  LoopbackGroup(int world, WaitPolicy wp);
+  enum OpKind : int { kIdle = 0, kBcastI64, kAllgatherI64, kAllreduceMin, kAllreduceMax, kBcast, kGather, kBarrier,
+                      kSend, kRecv };
+  struct OpDesc {
+    int kind = kIdle;
+    int root = -1;       // collectives with a root
+    int64_t bytes = -1;  // payload per rank (-1: not part of the op's signature)
+    int peer = -1;       // send / recv
+  };
+  LoopbackGroup(int world, WaitPolicy wp, bool strict = true);
   int world() const { return world_; }
-  void arrive_and_wait();  // reusable (generation-counted) barrier, honours the wait policy
+  bool strict() const { return strict_; }
+  // One collective call of `rank`: records op, waits for every rank (first barrier), checks the
+  // records (strict), then runs `between` (reads of the peers' slots), and waits again.
+  void collective(int rank, const OpDesc& op, const std::function<void()>& between);
+  void arrive_and_wait(int rank = -1);  // reusable (generation-counted) barrier, honours the wait policy
   std::vector<char>& slot(int r) { return slots_[size_t(r)]; }
+  // Point-to-point: post enqueues (strict: and waits until the receiver took it); take dequeues the
+  // next message src -> dst, checking its size against `expect` (< 0: any size).
   void post(int src, int dst, std::vector<char> msg);
-  std::vector<char> take(int src, int dst);
+  std::vector<char> take(int src, int dst, int64_t expect = -1);
   const WaitPolicy& policy() const { return wp_; }
+  static const char* op_name(int kind);
 
  private:
+  struct Msg {
+    std::vector<char> data;
+    uint64_t seq = 0;
+  };
+  struct RankState {
+    OpDesc op;         // the call the rank is inside (kIdle: none)
+    uint64_t gen = 0;  // collectives: barrier generation it waits on
+    uint64_t seq = 0;  // send: sequence number of its message on the channel
+  };
+  void wait_until(std::unique_lock<std::mutex>& lk, int rank, const char* what, const std::function<bool()>& done);
+  bool blocked(int r) const;                  // under mu_
+  std::vector<int> waits_for(int r) const;    // under mu_
+  std::string deadlock_cycle(int r) const;    // under mu_: "" or a description of the cycle through r
+  std::string describe(int r) const;          // under mu_
   int world_;
   WaitPolicy wp_;
+  bool strict_;
   std::mutex mu_;
   std::condition_variable cv_;
   int waiting_ = 0;
   uint64_t gen_ = 0;
   std::vector<std::vector<char>> slots_;
-  std::vector<std::deque<std::vector<char>>> mail_;  // [src * world + dst] FIFO
+  std::vector<std::deque<Msg>> mail_;  // [src * world + dst] FIFO
+  std::vector<uint64_t> sent_, taken_;  // per channel: messages posted / taken
+  std::vector<int64_t> rejected_;       // per channel: seq + 1 of a message the receiver refused (size)
+  std::vector<RankState> st_;
+  std::vector<OpDesc> coll_;            // per rank: the descriptor of its current collective
+  std::string mismatch_;                // strict: the first rank-pair mismatch of the current generation
 };
 
 class LoopbackTransport : public Transport {
@@ -247,7 +293,7 @@ class LoopbackTransport : public Transport {
   int64_t recv_i64(int peer) override;
   void send(const void* buf, int64_t bytes, int peer) override;
   void recv(void* buf, int64_t bytes, int peer) override;
-  void barrier() override { g_->arrive_and_wait(); }
+  void barrier() override;
   const char* name() const override { return "loopback"; }
 
  private:

@@ -1,6 +1,7 @@
 // Helpers shared by the C ABIs of the cascade (CPU group in libsvm355_core, device groups and
 // ranks in libsvm355_hip).
 #pragma once
+#include <string>
 #include <vector>
 
 #include "cascade.h"
@@ -14,5 +15,12 @@ svm_cascade_out* build_cascade_out(const std::vector<const CascadeOutput*>& outs
                                    int first_rank, const char* transport, const char* backend);
 // Row-major host rows of rank r's partition (contiguous ceil(n / P) chunks) and their global ids.
 std::vector<int64_t> partition_ids(int64_t n, int P, int r, int64_t* lo, int64_t* hi);
+
+// Transport exerciser (exercise.cpp): runs this rank's op list of `script` with checked payloads;
+// throws TransportError naming the rank, the op and what differed.
+void exercise_transport(Transport& t, Backend& B, const std::string& script);
+// Every op the cascade driver issues over P ranks (tree pairs per level included), bulk payloads of
+// bulk_bytes: the RCCL preflight of the device groups and ranks.
+std::string preflight_script(int P, int64_t bulk_bytes);
 
 }  // namespace svm355

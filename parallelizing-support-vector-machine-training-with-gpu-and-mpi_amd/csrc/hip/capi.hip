@@ -154,6 +154,18 @@ SVM_API int svmd_release_cache(void* h) {  // the library-owned Gram and the row
   SVMD_CTX(h);
   int rc = release_gram(ctx);
   if (rc) return rc;
+  return svmd_release_slab(h);
+}
+
+SVM_API int svmd_cache_bytes(void* h, int64_t* gram, int64_t* slab) {
+  SVMD_CTX(h);
+  if (gram) *gram = int64_t(ctx->gram_bytes);
+  if (slab) *slab = int64_t(ctx->rc_cache_bytes);
+  return SVM_OK;
+}
+
+SVM_API int svmd_release_slab(void* h) {  // the row-cache slab only (the resident Gram stays)
+  SVMD_CTX(h);
   if (ctx->rc_cache) {
     SVMD_CHECK(hipSetDevice(ctx->device));
     SVMD_CHECK(hipStreamSynchronize(ctx->stream));

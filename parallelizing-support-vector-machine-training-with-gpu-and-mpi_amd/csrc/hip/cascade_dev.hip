@@ -13,6 +13,7 @@
 //                                         (ncclCommInitAll) or a loopback rehearsal;
 //                  svmd_cascade_rank_*  : one rank per process (ncclCommInitRank with an id the
 //                                         launcher distributes, e.g. torchrun + a TCP store).
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <chrono>
@@ -337,7 +338,17 @@ class HipBackend final : public Backend {
   // the Gram the solve would build) for pixel data, else the MFMA f64 decision path, whose values
   // agree with the Gram's to a few ulps, so f agrees to ~1e-9 here (nz <= a few thousand,
   // alpha <= C); a 1e-7 margin on the stop test covers either.
+  // The check is an optimisation only: a failure of its own (e.g. its k x nz workspace does not fit
+  // next to a large partition) answers "not converged" and the normal solve runs.
   bool kkt_check(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
+    try {
+      return kkt_check_impl(S, nz, d, p, mn_h, mx_h);
+    } catch (const CascadeError&) {
+      (void)hipGetLastError();  // clear a sticky launch / allocation error of the failed attempt
+      return false;
+    }
+  }
+  bool kkt_check_impl(DSet& S, int64_t nz, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
     const char* e = getenv("SVM355_CASCADE_SKIP");  // =0 disables the check (A/B runs, tests)
     if ((e && atoi(e) == 0) || nz <= 0 || nz > S.k) return false;
     const int64_t ldd = ld(d), k = S.k;
@@ -560,6 +571,45 @@ class RcclTransport final : public Transport {
 
 double timeout_or_default(double s) { return s > 0 ? s : 600.0; }
 
+// ---- RCCL runtime identity.  Inside a PyTorch process the librccl this library resolves is the one
+// torch already loaded (its bundled copy), not necessarily the /opt/rocm one the header came from.
+// Every entry point called here (CommInitAll / InitRank / Abort / Destroy / GetAsyncError / UserRank /
+// Count, Broadcast, AllReduce, AllGather, Gather, Send, Recv, GetUniqueId, GetErrorString) has kept
+// its signature since RCCL 2.12, and ncclUniqueId its 128 bytes, so a runtime of the header's major
+// version and at least kMinRcclCode is accepted; an older minor than the header's is recorded as a
+// skew, and the preflight (exercise.cpp) checks every op on the live communicators anyway.
+constexpr int kMinRcclCode = 21200;
+struct RcclInfo {
+  int header = NCCL_VERSION_CODE;
+  int runtime = 0;
+  std::string path;
+};
+const RcclInfo& rccl_info() {
+  static const RcclInfo info = [] {
+    RcclInfo r;
+    if (ncclGetVersion(&r.runtime) != ncclSuccess) r.runtime = 0;
+    Dl_info di{};
+    if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname) r.path = di.dli_fname;
+    return r;
+  }();
+  return info;
+}
+void require_rccl_runtime() {
+  const RcclInfo& i = rccl_info();
+  if (i.runtime / 10000 != NCCL_MAJOR || i.runtime < kMinRcclCode)
+    throw CascadeError("RCCL runtime " + std::to_string(i.runtime) + " (" + i.path + ") is not usable: need major " +
+                       std::to_string(NCCL_MAJOR) + " and at least " + std::to_string(kMinRcclCode) +
+                       " (built against " + std::to_string(i.header) + ")");
+}
+
+// Preflight: the driver's whole op set over the live communicators (SVM355_RCCL_PREFLIGHT=0 skips it).
+constexpr double kPreflightTimeout = 20.0;
+constexpr int64_t kPreflightBytes = 1 << 20;
+bool preflight_enabled() {
+  const char* e = getenv("SVM355_RCCL_PREFLIGHT");
+  return !(e && atoi(e) == 0);
+}
+
 // ------------------------------------------------------------------------- thread-rank group
 struct Group {
   int world = 0;
@@ -584,12 +634,80 @@ struct ProcRank {
   std::unique_ptr<RcclTransport> tr;
 };
 
+// Runs `script` (exercise.cpp) on every rank of a group; "" on success, else the first error (the
+// group is then broken: its communicators were aborted).
+std::string group_exercise(Group& g, const std::string& script, double timeout_s) {
+  const int P = g.world;
+  auto token = std::make_shared<AbortToken>();
+  const WaitPolicy wp{token, timeout_s};
+  std::vector<Transport*> tr(static_cast<size_t>(P));
+  std::vector<std::unique_ptr<LoopbackTransport>> ltr;
+  std::shared_ptr<LoopbackGroup> lg = g.rccl ? nullptr : std::make_shared<LoopbackGroup>(P, wp);
+  for (int r = 0; r < P; ++r) {
+    if (g.rccl) {
+      g.rtr[size_t(r)]->set_policy(wp);
+      tr[size_t(r)] = g.rtr[size_t(r)].get();
+    } else {
+      ltr.push_back(std::make_unique<LoopbackTransport>(lg, r, g.be[size_t(r)].get()));
+      tr[size_t(r)] = ltr.back().get();
+    }
+  }
+  try {
+    g.pool->run(
+        token,
+        [&](int r) {
+          if (hipSetDevice(g.devices[size_t(r)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
+          exercise_transport(*tr[size_t(r)], *g.be[size_t(r)], script);
+        },
+        [&](int r) {
+          (void)hipSetDevice(g.devices[size_t(r)]);
+          tr[size_t(r)]->abort();
+        });
+  } catch (const std::exception& e) {
+    if (g.rccl) g.broken = true;
+    return e.what();
+  }
+  return "";
+}
+
 }  // namespace
 }  // namespace svm355
 
 using namespace svm355;
 
 extern "C" {
+
+SVM_API int svmd_rccl_info(int32_t* header_code, int32_t* runtime_code, char* path, int64_t cap) {
+  const RcclInfo& i = rccl_info();
+  if (header_code) *header_code = i.header;
+  if (runtime_code) *runtime_code = i.runtime;
+  if (path && cap > 0) {
+    std::strncpy(path, i.path.c_str(), size_t(cap) - 1);
+    path[cap - 1] = 0;
+  }
+  return SVM_OK;
+}
+
+SVM_API int svmd_cascade_group_exercise(void* h, const char* script, double timeout_s) {
+  auto* g = static_cast<Group*>(h);
+  if (!g || !script) {
+    set_error("svmd_cascade_group_exercise: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->broken) {
+    set_error("svmd_cascade_group_exercise: the group's communicators were aborted by an earlier failure");
+    return SVM_ERR_ARG;
+  }
+  const std::string err = group_exercise(*g, script, timeout_s > 0 ? timeout_s : kPreflightTimeout);
+  if (!err.empty()) {
+    set_error("%s", err.c_str());
+    return SVM_ERR_DEVICE;
+  }
+  return SVM_OK;
+}
+
+SVM_API int svmd_cascade_group_broken(void* h) { return h && static_cast<Group*>(h)->broken ? 1 : 0; }
 
 SVM_API void* svmd_cascade_group_create(int32_t world, const char* transport, double comm_timeout_s) {
   try {
@@ -620,6 +738,17 @@ SVM_API void* svmd_cascade_group_create(int32_t world, const char* transport, do
                                                          g->be[size_t(r)]->stream(), WaitPolicy{}));
     }
     g->pool = std::make_unique<RankPool>(world);
+    if (g->rccl) {
+      require_rccl_runtime();
+      if (preflight_enabled()) {
+        const std::string err = group_exercise(*g, preflight_script(world, kPreflightBytes), kPreflightTimeout);
+        if (!err.empty()) {
+          Group* raw = g.release();
+          svmd_cascade_group_destroy(raw);  // communicators were aborted by the failed exercise
+          throw CascadeError("RCCL preflight failed: " + err);
+        }
+      }
+    }
     return g.release();
   } catch (const std::exception& e) {
     set_error("svmd_cascade_group_create: %s", e.what());
@@ -755,6 +884,20 @@ SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32
     const ncclResult_t rc = ncclCommInitRank(&p->comm, world, id, rank);
     if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
     p->tr = std::make_unique<RcclTransport>(p->comm, device, p->be->stream(), WaitPolicy{nullptr, p->timeout_s});
+    require_rccl_runtime();
+    if (preflight_enabled()) {
+      p->tr->set_policy(WaitPolicy{nullptr, kPreflightTimeout});
+      try {
+        exercise_transport(*p->tr, *p->be, preflight_script(world, kPreflightBytes));
+      } catch (const std::exception& e) {
+        p->tr->abort();  // the peers' preflight waits fail too
+        p->broken = true;
+        ProcRank* raw = p.release();
+        svmd_cascade_rank_destroy(raw);
+        throw CascadeError(std::string("RCCL preflight failed: ") + e.what());
+      }
+      p->tr->set_policy(WaitPolicy{nullptr, p->timeout_s});
+    }
     return p.release();
   } catch (const std::exception& e) {
     set_error("svmd_cascade_rank_create: %s", e.what());
@@ -802,6 +945,26 @@ SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* h, const void* X, int32_t u
   } catch (const std::exception& e) {
     set_error("cascade: %s", e.what());
     return nullptr;
+  }
+}
+
+SVM_API int svmd_cascade_rank_exercise(void* h, const char* script, double timeout_s) {
+  auto* p = static_cast<ProcRank*>(h);
+  if (!p || p->broken || !script) {
+    set_error("svmd_cascade_rank_exercise: no usable communicator");
+    return SVM_ERR_ARG;
+  }
+  try {
+    (void)hipSetDevice(p->device);
+    p->tr->set_policy(WaitPolicy{nullptr, timeout_s > 0 ? timeout_s : kPreflightTimeout});
+    exercise_transport(*p->tr, *p->be, script);
+    p->tr->set_policy(WaitPolicy{nullptr, p->timeout_s});
+    return SVM_OK;
+  } catch (const std::exception& e) {
+    p->tr->abort();
+    p->broken = true;
+    set_error("%s", e.what());
+    return SVM_ERR_DEVICE;
   }
 }
 

@@ -196,6 +196,15 @@ SVM_API svm_cascade_out* svm_cascade_rank_fit_cpu(const svm_host_comm* comm, con
                                                   const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
                                                   const svm_cascade_cfg* cfg);
 
+// Transport exerciser (tests): world CPU-backend thread-ranks over a loopback group (strict = RCCL
+// rules: matched collectives, rendezvous sends, deadlock detection) run `script` (exercise.cpp) with
+// checked payloads.  SVM_OK, or an error naming the ranks / op within timeout_s.
+SVM_API int svm_loopback_exercise(int32_t world, const char* script, int32_t strict, double timeout_s,
+                                  double* elapsed_s);
+// The preflight op list the device groups run on their RCCL communicators (needs cap bytes; returns
+// the size needed when cap is too small, else 0).
+SVM_API int svm_preflight_script(int32_t world, int64_t bulk_bytes, char* out, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,10 @@ SVM_API void svmd_destroy(void* ctx);
 // Free the Gram matrix the library allocated for svmd_train* with K_d == NULL (it is kept in the
 // context between calls so repeated fits of the same size do not re-allocate it).
 SVM_API int svmd_release_cache(void* ctx);
+// Free only the row-cache slab the context keeps after a row-cache fit (see svmd_train_rows).
+SVM_API int svmd_release_slab(void* ctx);
+// Bytes the context holds for its library-owned Gram and row-cache slab.
+SVM_API int svmd_cache_bytes(void* ctx, int64_t* gram, int64_t* slab);
 // Size the context-owned Gram for an n-row solve ahead of it (SVM_ERR_OOM if it does not fit).
 SVM_API int svmd_reserve_gram(void* ctx, int64_t n);
 // Exact-integer training straight from uint8 pixel rows (n x d contiguous, device): *used = 0 and
@@ -172,6 +176,17 @@ SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* rank, const void* X, int32_
                                                const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
                                                const svm_cascade_cfg* cfg);
 SVM_API int svmd_cascade_rank_barrier(void* rank);
+// RCCL preflight / transport exerciser (csrc/cascade/exercise.cpp script syntax): run `script` with
+// checked payloads on every rank of a group (rccl or loopback), or on this process's rank (every
+// rank of the communicator calls it collectively).  Group and rank creation already run the
+// driver's op set (svm_preflight_script) on RCCL communicators (SVM355_RCCL_PREFLIGHT=0 skips it).
+// A failure aborts the communicators (the group / rank is then unusable).
+SVM_API int svmd_cascade_group_exercise(void* group, const char* script, double timeout_s);
+SVM_API int svmd_cascade_rank_exercise(void* rank, const char* script, double timeout_s);
+SVM_API int svmd_cascade_group_broken(void* group);  // 1 once a failure aborted its communicators
+// RCCL the library was compiled against (NCCL_VERSION_CODE) and the one it runs on (ncclGetVersion),
+// with the path of the loaded librccl (in a PyTorch process: usually torch's bundled copy).
+SVM_API int svmd_rccl_info(int32_t* header_code, int32_t* runtime_code, char* path, int64_t cap);
 SVM_API void svmd_cascade_rank_destroy(void* rank);
 
 // roctx ranges (rocprofv3 --marker-trace); the library already brackets preprocess / gram / smo /

@@ -267,14 +267,34 @@ def gram_buffer(n: int, device) -> torch.Tensor:
 
 
 def release_gram_buffers() -> None:
-    """Drop the calling thread's cached Gram buffers (``gram_buffer``)."""
+    """Drop the calling thread's cached Gram buffers (``gram_buffer``) and the library-owned device
+    memory of its contexts (the row-cache slab and Gram the C ABI keeps between fits, which would
+    otherwise hold up to 60 % of the HBM and push later fits onto the slower row cache)."""
     _gram_bufs().clear()
+    for ctx in list((getattr(DeviceContext._tls, "ctxs", None) or {}).values()):
+        if ctx.handle:
+            N.check(ctx.lib.svmd_release_cache(ctx.handle), "svmd_release_cache")
 
 
 def gram_fits(n: int, device, fraction: float = 0.8) -> bool:
-    """Does the full n x n float64 Gram fit in `fraction` of the free device memory?"""
-    free, _ = torch.cuda.mem_get_info(torch.device(device))
-    return n * ((n + 1) // 2 * 2) * 8 <= fraction * (free + torch.cuda.memory_reserved(torch.device(device)))
+    """Does the full n x n float64 Gram fit in `fraction` of the free device memory?  A row-cache slab
+    an earlier fit left in this thread's context counts as free: when the Gram fits only with that
+    memory the slab is handed back (it is rebuilt on demand), so it cannot push this fit onto the row
+    cache; otherwise it is kept for the next row-cache fit."""
+    device = torch.device(device)
+    need = n * ((n + 1) // 2 * 2) * 8
+    free, _ = torch.cuda.mem_get_info(device)
+    avail = free + torch.cuda.memory_reserved(device)
+    ctx = (getattr(DeviceContext._tls, "ctxs", None) or {}).get(
+        device.index if device.index is not None else torch.cuda.current_device())
+    if ctx is None or not ctx.handle or need <= fraction * avail:
+        return need <= fraction * avail
+    slab = ctypes.c_int64(0)
+    N.check(ctx.lib.svmd_cache_bytes(ctx.handle, None, ctypes.byref(slab)), "svmd_cache_bytes")
+    if slab.value and need <= fraction * (avail + slab.value):
+        N.check(ctx.lib.svmd_release_slab(ctx.handle), "svmd_release_slab")
+        return True
+    return False
 
 
 def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams,

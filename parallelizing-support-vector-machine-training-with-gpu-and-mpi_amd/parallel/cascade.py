@@ -108,6 +108,12 @@ class CascadeSVM:
             g = group or DeviceGroup.shared(world, transport)
             p = N.hip().svmd_cascade_group_fit(g.handle, N.ptr(X), int(X.dtype == np.uint8), N.ptr(y), X.shape[0],
                                                X.shape[1], ctypes.byref(self.cfg))
+            if not p:
+                err = N.last_error()
+                if group is None and g.broken:  # aborted communicators: the next fit builds a new group
+                    DeviceGroup._shared.pop((world, transport), None)
+                    g.close()
+                raise N.NativeError(err)
         self.device = device
         self.result = CascadeResult.take(p)
         return self
@@ -208,3 +214,24 @@ def critical_path(solves, topology: str):
         tot += lm + mm
     return out, round(tot, 3)
 
+
+
+def loopback_exercise(world: int, script: str, strict: bool = True, timeout_s: float = 20.0):
+    """Run a transport call script (csrc/cascade/exercise.cpp syntax) on ``world`` CPU thread-ranks
+    over the loopback transport, every received byte checked.  Returns the elapsed seconds; raises
+    ``NativeError`` naming the ranks / op on a mismatch, deadlock, wrong payload or timeout."""
+    el = ctypes.c_double(0.0)
+    rc = N.core().svm_loopback_exercise(int(world), script.encode(), int(bool(strict)), float(timeout_s),
+                                         ctypes.byref(el))
+    if rc != 0:
+        raise N.NativeError(f"{N.last_error()} (after {el.value:.2f} s)")
+    return el.value
+
+
+def preflight_script(world: int, bulk_bytes: int = 1 << 20) -> str:
+    """The op list the device groups / ranks run on their RCCL communicators before any fit."""
+    lib = N.core()
+    need = lib.svm_preflight_script(int(world), int(bulk_bytes), None, 0)
+    buf = ctypes.create_string_buffer(need)
+    N.check(lib.svm_preflight_script(int(world), int(bulk_bytes), buf, need), "svm_preflight_script")
+    return buf.value.decode()

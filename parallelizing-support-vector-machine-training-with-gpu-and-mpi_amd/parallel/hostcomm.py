@@ -9,6 +9,7 @@ cpu`` and the multi-process CPU tests exercise the per-process path the 8-GPU ru
 from __future__ import annotations
 
 import ctypes
+import datetime
 from ctypes import CFUNCTYPE, POINTER, c_double, c_int, c_int32, c_int64, c_void_p
 
 import numpy as np
@@ -38,16 +39,26 @@ def _bytes(ptr, nbytes: int) -> torch.Tensor:
 
 
 class HostCommRank:
-    """This process's rank of an initialised ``torch.distributed`` group (gloo) as a cascade rank."""
+    """This process's rank of an initialised ``torch.distributed`` group (gloo) as a cascade rank.
+
+    Every exchange is issued asynchronously and waited on with the fit's ``comm_timeout_s`` (the
+    native driver's WaitPolicy deadline): a peer that failed -- and stays alive -- or stopped
+    responding makes this rank's wait fail within that deadline instead of the process group's own
+    (much longer) timeout, the MPI_Abort contract of the reference (mpi_svm_main3.cpp:420-428)."""
 
     device = "cpu"
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, comm_timeout_s: float = 600.0):
         import torch.distributed as dist
 
         self.dist, self.group = dist, group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.timeout_s = float(comm_timeout_s)
         self.error: BaseException | None = None  # first exception raised inside a callback
+
+        def done(work):
+            if not work.wait(timeout=datetime.timedelta(seconds=self.timeout_s)):
+                raise TimeoutError(f"collective did not complete within {self.timeout_s} s")
 
         def guard(fn):
             def wrapped(*a):
@@ -63,29 +74,30 @@ class HostCommRank:
         g = self.group
 
         def bcast(_ctx, buf, nbytes, root):
-            dist.broadcast(_bytes(buf, nbytes), src=dist.get_global_rank(g, root) if g else root, group=g)
+            done(dist.broadcast(_bytes(buf, nbytes), src=dist.get_global_rank(g, root) if g else root, group=g,
+                                async_op=True))
 
         def allgather(_ctx, send, nbytes, recv):
             out = _bytes(recv, nbytes * self.world)
-            dist.all_gather(list(out.split(int(nbytes))), _bytes(send, nbytes).clone(), group=g)
+            done(dist.all_gather(list(out.split(int(nbytes))), _bytes(send, nbytes).clone(), group=g, async_op=True))
 
         def allreduce(_ctx, buf, n, op):
             t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(int(n),)))
-            dist.all_reduce(t, op=dist.ReduceOp.MIN if op == 0 else dist.ReduceOp.MAX, group=g)
+            done(dist.all_reduce(t, op=dist.ReduceOp.MIN if op == 0 else dist.ReduceOp.MAX, group=g, async_op=True))
 
         def gather(_ctx, send, nbytes, recv, root):
             dst = dist.get_global_rank(g, root) if g else root
             parts = list(_bytes(recv, nbytes * self.world).split(int(nbytes))) if self.rank == root else None
-            dist.gather(_bytes(send, nbytes).clone(), gather_list=parts, dst=dst, group=g)
+            done(dist.gather(_bytes(send, nbytes).clone(), gather_list=parts, dst=dst, group=g, async_op=True))
 
         def send(_ctx, buf, nbytes, peer):
-            dist.send(_bytes(buf, nbytes), dst=dist.get_global_rank(g, peer) if g else peer, group=g)
+            done(dist.isend(_bytes(buf, nbytes), dst=dist.get_global_rank(g, peer) if g else peer, group=g))
 
         def recv(_ctx, buf, nbytes, peer):
-            dist.recv(_bytes(buf, nbytes), src=dist.get_global_rank(g, peer) if g else peer, group=g)
+            done(dist.irecv(_bytes(buf, nbytes), src=dist.get_global_rank(g, peer) if g else peer, group=g))
 
         def barrier(_ctx):
-            dist.barrier(group=g)
+            done(dist.barrier(group=g, async_op=True))
 
         # The CFUNCTYPE objects must outlive every native call: they are attributes of self.
         self._cbs = (_BCAST(guard(bcast)), _ALLGATHER(guard(allgather)), _ALLREDUCE(guard(allreduce)),
@@ -98,6 +110,8 @@ class HostCommRank:
     def fit(self, cfg, X, y, ids, n_total: int):
         """run_cascade on this rank's partition; returns the native svm_cascade_out pointer."""
         self.error = None
+        if getattr(cfg, "comm_timeout_s", 0) > 0:
+            self.timeout_s = float(cfg.comm_timeout_s)
         X = np.ascontiguousarray(X, dtype=np.float64)
         y = np.ascontiguousarray(y, dtype=np.int32)
         ids = np.ascontiguousarray(ids, dtype=np.int64)

@@ -3,16 +3,33 @@
 ``DeviceGroup``  P thread-ranks over GPUs 0..P-1 of THIS process: one ``ncclCommInitAll``, one
                  communicator + device context per GPU, kept between fits (buffers stay warm).
                  ``transport="loopback"`` runs the same ranks on fewer GPUs with host-staged
-                 exchanges (rehearsals on one GPU).
+                 exchanges (rehearsals on one GPU).  Creating an RCCL group runs the preflight
+                 (every op of the cascade driver with checked payloads, csrc/cascade/exercise.cpp).
 ``RcclRank``     one rank per process (torchrun): rank 0 draws the ncclUniqueId, the launcher's
                  store (``torch.distributed``, any backend, e.g. gloo) distributes it, every process
                  calls ``ncclCommInitRank`` on its own GPU.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from .. import _native as N
+
+
+def rccl_info() -> dict:
+    """RCCL the device library was built against and the one it runs on (with the library path:
+    inside PyTorch usually torch's bundled librccl)."""
+    h, r = ctypes.c_int32(0), ctypes.c_int32(0)
+    path = ctypes.create_string_buffer(512)
+    N.hip().svmd_rccl_info(ctypes.byref(h), ctypes.byref(r), path, 512)
+
+    def ver(c):
+        return f"{c // 10000}.{c // 100 % 100}.{c % 100}" if c else "unknown"
+
+    return {"rccl_header": ver(h.value), "rccl_runtime": ver(r.value), "rccl_path": path.value.decode(),
+            "rccl_skew": h.value // 100 != r.value // 100}
 
 
 class DeviceGroup:
@@ -25,10 +42,25 @@ class DeviceGroup:
             raise N.NativeError(N.last_error())
         self.transport = transport
 
+    @property
+    def broken(self) -> bool:
+        """True once a failed fit / exercise aborted the communicators (the group cannot be used)."""
+        return bool(self.handle) and bool(N.hip().svmd_cascade_group_broken(self.handle))
+
+    def exercise(self, script: str, timeout_s: float = 20.0) -> None:
+        """Run a transport script (exercise.cpp syntax) with checked payloads on every rank."""
+        rc = N.hip().svmd_cascade_group_exercise(self.handle, script.encode(), float(timeout_s))
+        if rc != 0:
+            raise N.NativeError(N.last_error())
+
     @classmethod
     def shared(cls, world: int, transport: str = "auto") -> "DeviceGroup":
-        """A process-wide group per (world, transport): communicators are created once."""
+        """A process-wide group per (world, transport): communicators are created once, and again
+        after a failure aborted them."""
         g = cls._shared.get((world, transport))
+        if g is not None and (not g.handle or g.broken):
+            g.close()
+            g = None
         if g is None:
             g = cls._shared[(world, transport)] = cls(world, transport)
         return g
@@ -79,6 +111,12 @@ class RcclRank:
 
     def barrier(self) -> None:
         N.check(N.hip().svmd_cascade_rank_barrier(self.handle), "svmd_cascade_rank_barrier")
+
+    def exercise(self, script: str, timeout_s: float = 20.0) -> None:
+        """Collective: run a transport script (exercise.cpp syntax) with checked payloads."""
+        rc = N.hip().svmd_cascade_rank_exercise(self.handle, script.encode(), float(timeout_s))
+        if rc != 0:
+            raise N.NativeError(N.last_error())
 
     def close(self) -> None:
         if self.handle:

@@ -100,6 +100,54 @@ def test_a_failing_process_rank_ends_every_rank():
     assert "rank 0 failed" in outs[0] and "hostcomm" in outs[0], outs[0]
 
 
+_FAIL_ALIVE_SCRIPT = textwrap.dedent("""
+    import datetime, os, sys, time
+    import numpy as np
+    import torch.distributed as dist
+    from svm355 import SVMParams
+    from svm355.parallel.cascade import CascadeSVM, partition_bounds
+    from svm355.parallel.hostcomm import HostCommRank
+    from svm355.utils.data import synthetic_mnist
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+    r, P, n = dist.get_rank(), dist.get_world_size(), 800
+    lo, hi = partition_bounds(n, P, r)
+    tr = synthetic_mnist(hi - lo, seed=7, offset=lo)
+    t0 = time.time()
+    try:
+        CascadeSVM(SVMParams(), fail_rank=1, fail_round=1, comm_timeout_s=4.0).fit_rank(
+            HostCommRank(), tr.X, tr.y, np.arange(lo, hi), n)
+    except Exception as e:
+        print(f"rank {r} failed after {time.time() - t0:.1f} s: {e}", flush=True)
+        if r == 1:
+            time.sleep(90)  # the failed rank stays alive: its socket stays open
+        os._exit(3)  # MPI_Abort-like: an orderly exit would wait for the process group's teardown
+    print(f"rank {r} finished", flush=True)
+""")
+
+
+def test_a_failing_rank_that_stays_alive_releases_its_peers():
+    """The failed rank does not exit (its gloo socket stays open): its peer, blocked in a collective,
+    must still leave within the fit's comm_timeout_s (4 s here), not the 300 s process-group timeout
+    -- HostCommRank waits on every collective with the WaitPolicy deadline."""
+    port, env = _port(), _env()
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _FAIL_ALIVE_SCRIPT], cwd=ROOT, env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    try:
+        t0 = time.time()
+        out0 = procs[0].communicate(timeout=120)[0]
+        elapsed = time.time() - t0
+        assert procs[0].returncode == 3, out0
+        assert "rank 0 failed" in out0, out0
+        assert procs[1].poll() is None  # rank 1 is still alive (sleeping after its failure)
+        assert elapsed < 60, (elapsed, out0)
+    finally:
+        procs[1].kill()
+        procs[1].communicate()
+
+
 def test_torchrun_cascade_cli_is_mpirun_np(tmp_path):
     """``torchrun --nproc-per-node P -m svm355 cascade`` = the reference's ``mpirun -np P`` launch
     (code/mpi_svm3.sh): every process is one rank, rank 0 prints the reference lines and writes the
