@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark: SMO train time on the MNIST-60k one-vs-rest RBF config (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 60000] [--topology star|tree]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 60000] [--parallel auto|smo|cascade]
 
 One "step" is one complete training run on the fixed synthetic 60k x 784 MNIST-shaped matrix
 (an SVM has no random init; the data are a deterministic synthetic draw of MNIST's shape and value
@@ -9,17 +9,19 @@ domain because MNIST itself is not available offline):
 
 * N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's GPU
   "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram, device
-  SMO to convergence.  Rows are held as uint8 (what MNIST is) and widened to FP64 on the device,
-  where every value is exact (``--input f64`` ships FP64 rows like the reference, same results).
-* N > 1: the Cascade SVM (modified two-layer star, mpi_svm_main2.cpp, default; ``--topology tree`` =
-  classical mpi_svm_main3.cpp) on N GPUs, one rank per GPU, RCCL over xGMI, all on the ONE native
-  driver (csrc/cascade):
-    - launched directly (``python bench.py --gpus N``): N thread-ranks of this process, one GPU and
-      one communicator each (ncclCommInitAll) — nothing is re-launched;
-    - launched by torchrun (WORLD_SIZE = N): one rank per process on GPU LOCAL_RANK; the
-      ncclUniqueId travels over the launcher's store (gloo group), ncclCommInitRank.
-  Timed scope = a whole cascade fit: each rank's H2D of its partition, global scaling, all rounds to
-  convergence, the final model on the host.
+  SMO to convergence.  Rows are held as uint8 (what MNIST is); the Gram is quantised straight from
+  the bytes, every value exact (``--input f64`` ships FP64 rows like the reference, same results).
+* N > 1, ``--parallel smo`` (the default for pixel data): ONE first-order SMO over the N GPUs
+  (csrc/hip/dsmo.hip): each GPU owns 1/N of the points and its slab K(:, own) of the exact-integer
+  Gram, and the per-iteration arg-min / arg-max candidates cross the GPUs over xGMI -- the same
+  problem, the same stop test and the same model as one GPU, bit for bit (strong scaling).
+* N > 1, ``--parallel cascade``: the reference's multi-processor algorithm, the Cascade SVM (modified
+  two-layer star, mpi_svm_main2.cpp, default; ``--topology tree`` = classical mpi_svm_main3.cpp), one
+  rank per GPU over RCCL.  ``auto`` falls back to it when the distributed SMO is not applicable
+  (non-pixel data) or its preflight fails.
+Launch: directly (``python bench.py --gpus N``: N thread-ranks of this process, one GPU each) or by
+torchrun (WORLD_SIZE = N: one rank per process on GPU LOCAL_RANK; the distributed SMO exchanges the
+receive arrays' IPC handles, the cascade the ncclUniqueId, over the launcher's store).
 
 The timed region is bracketed by a barrier + device synchronisation on both sides and the maximum
 over ranks is reported.  value = seconds per training run (lower is better); vs_baseline = value /
@@ -36,7 +38,7 @@ import time
 
 import numpy as np
 
-# RCCL between processes (torchrun ranks) needs dmabuf IPC; the legacy IPC mode fails with
+# RCCL / IPC between processes (torchrun ranks) needs dmabuf IPC; the legacy IPC mode fails with
 # "hipIpcGetMemHandle: invalid argument" on these hosts.  Must be set before the HSA runtime starts.
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
@@ -46,6 +48,11 @@ REF_GPU_PRED_S = 38.297  # GPU prediction time, 60k train /
 REF_STAR_S = {4: 886.733, 8: 649.773, 16: 440.705, 32: 333.696, 64: 301.263}
 REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
 METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
+PREFLIGHT_ROWS = 4096
+
+
+class FallBack(Exception):
+    """The distributed SMO cannot run here: the bench continues with the cascade."""
 
 
 def main(argv=None):
@@ -57,20 +64,26 @@ def main(argv=None):
     ap.add_argument("--n", "--rows", dest="n", type=int, default=60000, help="training rows (MNIST-60k config)")
     ap.add_argument("--m", "--test-rows", dest="m", type=int, default=10000, help="test rows for the parity fields")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--parallel", choices=["auto", "smo", "cascade"], default="auto",
+                    help="N > 1: one distributed SMO over the GPUs (smo), the reference's Cascade SVM (cascade), "
+                         "or smo with a fallback to the cascade when it does not apply (auto)")
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
-                    help="direct launch, N > 1: rccl (one GPU per rank) or loopback (a rehearsal of N ranks "
-                         "sharing the visible GPUs, host-staged exchanges)")
+                    help="direct launch, N > 1: one GPU per rank (auto / rccl), or loopback = a rehearsal of N ranks "
+                         "on the visible GPU (cascade: host-staged exchanges; smo: N teams in one launch)")
     ap.add_argument("--input", choices=["u8", "f64"], default="u8",
                     help="host row format: uint8 pixels (default) or FP64 as in the reference")
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
     ap.add_argument("--baseline-1gpu", type=int, default=3,
-                    help="N > 1: single-GPU fits timed after the cascade for speedup_vs_1gpu (0 = skip)")
+                    help="N > 1: single-GPU fits timed after the run for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference; the headline) or the opt-in second-order")
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N > 1: seconds any rank waits on an exchange before every rank aborts its communicator "
                          "(a fit takes well under a second; a dead peer must not hang the run)")
+    ap.add_argument("--f64-fits", type=int, default=3,
+                    help="N = 1: steady-state fits with FP64 host rows (the reference's H2D), reported next to the "
+                         "headline (0 = skip)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: the same launch paths on the C++ oracle (CPU tests of the torchrun / thread-rank "
                          "plumbing; N > 1 under torchrun exchanges over gloo); not a benchmark")
@@ -107,7 +120,7 @@ def main(argv=None):
         torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
     sync = (lambda: torch.cuda.synchronize(dev)) if not cpu else (lambda: None)
-    use_cascade = a.gpus > 1 or a.cascade
+    distributed = a.gpus > 1 or a.cascade
     dist = None
     if multiproc:
         import torch.distributed as dist
@@ -116,21 +129,75 @@ def main(argv=None):
 
     params = SVMParams(wss=2 if a.wss == "second" else 1)
     te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
-    if multiproc:
-        lo, hi = partition_bounds(a.n, world_env, rank)
-        tr = synthetic_mnist(hi - lo, seed=a.seed, offset=lo)
-    else:
-        tr = synthetic_mnist(a.n, seed=a.seed)
+    full = synthetic_mnist(a.n, seed=a.seed)  # every rank: the distributed SMO holds all rows on every GPU
+    lo, hi = partition_bounds(a.n, world_env, rank) if multiproc else (0, a.n)
+    part = full.subset(lo, hi)
     if a.input == "u8":
-        tr = tr.compact()
+        full, part = full.compact(), part.compact()
         te = te.compact() if te is not None else None
+    pixel = full.X.dtype == np.uint8 and full.X.dtype == part.X.dtype
 
-    group = crank = None
-    if use_cascade:
+    mode = "single" if not distributed else a.parallel
+    fallback_reason = None
+    if mode == "auto":
+        mode = "smo" if (pixel and not cpu and a.wss == "first" and not a.cascade and a.gpus <= 8) else "cascade"
+        if mode == "cascade":
+            fallback_reason = ("not pixel rows" if not pixel else "cpu device" if cpu else "second-order selection"
+                               if a.wss != "first" else "cascade requested" if a.cascade else "more than 8 GPUs")
+    elif mode == "smo" and (cpu or not pixel):
+        print("bench.py: --parallel smo needs uint8 pixel rows on GPUs", file=sys.stderr)
+        return 2
+
+    def agree(ok: bool) -> bool:
+        """Every rank learns whether every rank succeeded (multi-process); the same bool otherwise."""
+        if dist is None:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    # ---- distributed SMO set-up + preflight: a 4096-row solve must equal the single-GPU solve
+    group = crank = dgroup = drank = None
+    if mode == "smo":
+        from svm355.parallel.dsmo import DistributedSVC, DsmoGroup, DsmoRank
+
+        err = ""
+        try:
+            if multiproc:
+                drank = DsmoRank.from_torch_dist(dev_index, timeout_s=a.comm_timeout)
+            else:
+                dgroup = DsmoGroup(a.gpus, rehearsal=a.transport == "loopback", timeout_s=a.comm_timeout)
+        except Exception as e:  # noqa: BLE001 - reported, then the cascade runs
+            err = f"set-up: {e}"
+        if not agree(not err):
+            fallback_reason = err or "set-up failed on another rank"
+        else:
+            pre = full.subset(0, min(PREFLIGHT_ROWS, a.n))
+            try:
+                m = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(pre.X, pre.y)
+                ref = SVC(device=str(dev)).fit(pre.X, pre.y)
+                if not (m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)):
+                    err = (f"preflight differs from the single-GPU solve (iterations {m.n_iter_} vs {ref.n_iter_}, "
+                           f"b {m.b_!r} vs {ref.b_!r})")
+            except Exception as e:  # noqa: BLE001
+                err = f"preflight: {e}"
+            if not agree(not err):
+                fallback_reason = err or "preflight failed on another rank"
+        if fallback_reason:
+            if rank == 0:
+                print(f"bench.py: distributed SMO unavailable ({fallback_reason}); running the cascade",
+                      file=sys.stderr, flush=True)
+            mode = "cascade"
+            for h in (dgroup, drank):
+                if h is not None:
+                    h.close()
+            dgroup = drank = None
+
+    if mode == "cascade":
         if multiproc and cpu:
             from svm355.parallel.hostcomm import HostCommRank
 
-            crank = HostCommRank()
+            crank = HostCommRank(comm_timeout_s=a.comm_timeout)
         elif multiproc:
             from svm355.parallel.rccl import RcclRank
 
@@ -152,31 +219,46 @@ def main(argv=None):
 
     def step():
         nonlocal model
-        if not use_cascade:
-            model = SVC(device=str(dev), wss=a.wss).fit(tr.X, tr.y)
+        if mode == "single":
+            model = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
+        elif mode == "smo":
+            model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
         elif multiproc:
             model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit_rank(
-                crank, tr.X, tr.y, np.arange(lo, hi), a.n)
+                crank, part.X, part.y, np.arange(lo, hi), a.n)
         else:
             model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit(
-                tr.X, tr.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
+                full.X, full.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
+
+    def guarded_step():
+        try:
+            step()
+        except Exception as e:  # noqa: BLE001
+            if multiproc:  # an orderly exit would wait for the process group's teardown on the peers
+                print(f"bench.py rank {rank}: {mode} fit failed: {e}", file=sys.stderr, flush=True)
+                os._exit(1)
+            raise
 
     warm_ms = []
     for _ in range(a.warmup):
         tw = time.perf_counter()
-        step()
+        guarded_step()
         sync()
         warm_ms.append(round((time.perf_counter() - tw) * 1e3, 3))
     barrier_sync()
     t0 = time.perf_counter()
     marks, parts = [], []
     for _ in range(a.steps):
-        step()
+        guarded_step()
         marks.append(time.perf_counter())  # host-side step boundaries (diagnostic only)
-        if not use_cascade:  # per-step upload / Gram / SMO split (diagnostic only)
+        if mode == "single":  # per-step upload / Gram / SMO split (diagnostic only)
             parts.append([round(model.timings_.get(k, 0.0), 2) for k in ("upload_preprocess_ms", "gram_alloc_ms",
                                                                            "gram_ms", "smo_ms")]
                          + [round(model.fit_time_ * 1e3, 2)])
+        elif mode == "smo":
+            t = model.timings_
+            parts.append([round(t["upload_minmax_ms"], 2), round(t["quantise_slab_ms"], 2), round(t["smo_ms"], 2),
+                          round(model.fit_time_ * 1e3, 2)])
     barrier_sync()
     elapsed = time.perf_counter() - t0
     step_ms = [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + marks[:-1], marks)]
@@ -188,7 +270,7 @@ def main(argv=None):
     ms = elapsed / a.steps * 1e3
     value = ms / 1e3
     extra = {}
-    if not use_cascade:
+    if mode == "single":
         # Prediction on the 10k test rows (outside the timed region): H2D, scaling with the training
         # statistics, MFMA cross-kernel against the SVs, decision values back to the host.  The
         # reference's GPU "prediction" (38.3 s at 60k) also parses the test CSV.
@@ -198,14 +280,39 @@ def main(argv=None):
         sync()
         pred_ms = (time.perf_counter() - tp) * 1e3
         acc = model.score(te.X, te.y)
+        f64_ms = []
+        if a.f64_fits > 0 and not cpu and a.input == "u8":  # the reference's FP64 host rows, same model
+            X64 = full.X.astype(np.float64)
+            m64 = SVC(device=str(dev), wss=a.wss).fit(X64, full.y)
+            for _ in range(a.f64_fits):
+                sync()
+                tf = time.perf_counter()
+                m64 = SVC(device=str(dev), wss=a.wss).fit(X64, full.y)
+                sync()
+                f64_ms.append((time.perf_counter() - tf) * 1e3)
+            extra["f64_input_fit_ms"] = round(float(np.median(f64_ms)), 3)
+            extra["f64_input_same_model"] = bool(m64.b_ == model.b_ and m64.n_iter_ == model.n_iter_)
+        extra.update({
+            "n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
+            "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
+            "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S,
+            "cold_fit_ms": warm_ms[0] if warm_ms else None, "warmup_fit_ms": warm_ms,
+            "caveats": "timed fits reuse the library's grow-only Gram buffer and device context, allocated by the "
+                       "first (cold) fit, whose time is cold_fit_ms; host rows are uint8 pixels: min/max, the "
+                       "exact-integer quantisation and the Gram read the bytes on the device and only the support "
+                       "vectors are widened to scaled fp64 (f64_input_fit_ms: the same fit from the reference's fp64 "
+                       "host rows); the data are a synthetic MNIST-shaped draw, not MNIST"})
+    elif mode == "smo":
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
-                 "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
-                 "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S,
-                 "warmup_fit_ms": warm_ms,
-                 "caveats": "timed fits reuse the library's grow-only Gram buffer and device context, allocated by "
-                            "the first (warm-up) fit, whose time is warmup_fit_ms[0]; host rows are uint8 pixels "
-                            "widened to fp64 on the device (bit-identical results to --input f64, which ships fp64 "
-                            "rows like the reference); the data are a synthetic MNIST-shaped draw, not MNIST"}
+                 "stop_reason": model.stop_reason_, "timings_ms": model.timings_, "team_shape": model.shape_,
+                 "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
+                 "launch_form": "one team per GPU" if a.transport != "loopback" else
+                                f"rehearsal: {a.gpus} teams on one GPU",
+                 "note": "one first-order SMO over all GPUs: each GPU holds 1/N of the points and its slab K(:, own) "
+                         "of the exact-integer Gram; every iteration's candidates cross the GPUs over xGMI; same "
+                         "iterations, alphas and b as the single-GPU trainer (bit_identical_to_1gpu)"}
+        if rank == 0:
+            extra["accuracy"] = model.score(te.X, te.y)
     else:
         r = model.result
         solves = r.solves
@@ -230,37 +337,48 @@ def main(argv=None):
                                                 for q in range(max(1, r.world))),
                  "note": "per_round_critical_path = [round, slowest local solve ms (tree: first layer), rank-0 "
                          "merge ms (tree: slowest rank of each later layer), their SMO iterations]; "
-                         "the single-GPU trainer solves the same 60k problem in one 12,793-iteration SMO",
-                 # recorded one-GPU rehearsal (solo-timed solves), not measured by this run: where the cascade
-                 # overtakes one GPU -- partitions with resident Grams vs one SMO on the row cache
-                 "large_n_crossover_rehearsal": {"n": 1000000, "star_p8_critical_path_s": 1.670,
-                                                 "single_gpu_s": 2.072,
-                                                 "source": "profiles/r2_largen_cascade_vs_1gpu.txt"}}
+                         "the single-GPU trainer solves the same 60k problem in one 12,793-iteration SMO"}
         if rank == 0:
             extra["accuracy"] = model.score(te.X, te.y)
         ref = (REF_STAR_S if a.topology == "star" else REF_TREE_S).get(a.gpus)
         if ref:
             extra["speedup_vs_ref_cascade_same_P"] = round(ref / value, 2)
-        if a.baseline_1gpu > 0:  # the single-GPU trainer on this rank's GPU, same data, same process
-            if dist is not None:
-                dist.barrier()
-            if rank == 0:
-                full = tr if not multiproc else synthetic_mnist(a.n, seed=a.seed)
-                full = full.compact() if a.input == "u8" else full
-                SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)  # warm
-                ts = []
-                for _ in range(a.baseline_1gpu):
-                    sync()
-                    tb = time.perf_counter()
-                    SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
-                    sync()
-                    ts.append(time.perf_counter() - tb)
-                one = float(np.median(ts))
-                extra["single_gpu_s"] = round(one, 6)
-                extra["speedup_vs_1gpu"] = round(one / value, 4)
-            if dist is not None:
-                dist.barrier()
+        if fallback_reason:
+            extra["fallback_reason"] = fallback_reason
+    if mode in ("smo", "cascade") and a.baseline_1gpu > 0:  # the single-GPU trainer, same data, rank 0's GPU
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            one = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)  # warm
+            ts = []
+            for _ in range(a.baseline_1gpu):
+                sync()
+                tb = time.perf_counter()
+                one = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
+                sync()
+                ts.append(time.perf_counter() - tb)
+            t1 = float(np.median(ts))
+            extra["single_gpu_s"] = round(t1, 6)
+            extra["speedup_vs_1gpu"] = round(t1 / value, 4)
+            if mode == "smo":
+                extra["bit_identical_to_1gpu"] = bool(one.n_iter_ == model.n_iter_ and one.b_ == model.b_ and
+                                                      np.array_equal(one.alpha_, model.alpha_))
+        if dist is not None:
+            dist.barrier()
+    if distributed and not cpu:
+        try:
+            from svm355.parallel.rccl import rccl_info
+
+            extra.update(rccl_info())
+        except Exception as e:  # noqa: BLE001 - informative only
+            extra["rccl_info_error"] = str(e)
     if rank == 0:
+        if mode == "single":
+            parallelism = "single-gpu"
+        elif mode == "smo":
+            parallelism = f"distributed-smo-dp{a.gpus}"
+        else:
+            parallelism = f"cascade-{a.topology}-dp{a.gpus}"
         line = {
             "metric": METRIC,
             "value": round(value, 6),
@@ -278,16 +396,17 @@ def main(argv=None):
                 "model": f"RBF SVM, {a.wss}-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,
-                "parallelism": "single-gpu" if not use_cascade else f"cascade-{a.topology}-dp{a.gpus}",
+                "parallelism": parallelism,
             },
             "launch": "torchrun (one rank per process)" if multiproc else
-                      ("in-process thread ranks" if use_cascade else "single process"),
+                      ("in-process thread ranks" if distributed else "single process"),
             **({"device": "cpu (C++ oracle; launch-path check, not a benchmark)"} if cpu else {}),
-            "host_rows": "uint8 (widened to fp64 on device)" if a.input == "u8" else "fp64",
+            "host_rows": "uint8 (the device reads the bytes; only the SVs are widened to fp64)" if a.input == "u8"
+                         else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
             "step_ms": step_ms,
-            "step_upload_alloc_gram_smo_fit_ms": parts,
+            ("step_upload_alloc_gram_smo_fit_ms" if mode != "smo" else "step_upload_slab_smo_fit_ms"): parts,
             **extra,
         }
         s = json.dumps(line)
@@ -295,10 +414,9 @@ def main(argv=None):
         if a.out:
             with open(a.out, "w") as f:
                 f.write(s + "\n")
-    if crank is not None:
-        crank.close()
-    if group is not None:
-        group.close()
+    for h in (crank, group, dgroup, drank):
+        if h is not None:
+            h.close()
     if dist is not None:
         dist.destroy_process_group()
     return 0

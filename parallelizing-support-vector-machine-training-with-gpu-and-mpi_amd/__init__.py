@@ -9,6 +9,9 @@ re-designed for gfx950:
 * ``svm355.parallel.CascadeSVM``     classical tree and modified two-layer star Cascade SVM: one native
                                      driver over RCCL (a thread per GPU, or one rank per process under
                                      torchrun) or the loopback transport (CPU oracle / one-GPU rehearsal)
+* ``svm355.parallel.DistributedSVC`` ONE SMO over the GPUs of a node: points and Gram slabs split over
+                                     GPUs, per-iteration candidates exchanged over xGMI; the single-GPU
+                                     trajectory bit for bit (``--parallel smo``)
 * ``svm355.utils.data``              CSV I/O, one-vs-rest labels, min-max scaling, synthetic MNIST
 * ``svm355.ops``                     device kernels (exact-integer int8-MFMA and f64-MFMA RBF Grams,
                                      persistent SMO solvers, HBM row cache, predict)
@@ -26,7 +29,7 @@ from .models.multiclass import OneVsRestSVC
 from .models.svc import SVC
 
 __all__ = ["SVMParams", "Dataset", "MinMaxScaler", "load_csv", "one_vs_rest", "synthetic_mnist", "write_csv",
-           "SVC", "OneVsRestSVC", "CascadeSVM"]
+           "SVC", "OneVsRestSVC", "CascadeSVM", "DistributedSVC"]
 __version__ = "0.1.0"
 
 
@@ -35,4 +38,8 @@ def __getattr__(name):
         from .parallel.cascade import CascadeSVM
 
         return CascadeSVM
+    if name == "DistributedSVC":
+        from .parallel.dsmo import DistributedSVC
+
+        return DistributedSVC
     raise AttributeError(name)

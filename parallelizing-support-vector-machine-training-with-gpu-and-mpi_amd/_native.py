@@ -217,6 +217,18 @@ _HIP_SIGS = {
     "svmd_cascade_group_broken": (c_int32, [c_void_p]),
     "svmd_rccl_info": (c_int32, [POINTER(c_int32), POINTER(c_int32), c_char_p, c_int64]),
     "svmd_cascade_rank_destroy": (None, [c_void_p]),
+    "svmd_dsmo_create": (c_void_p, [c_int32, c_int32, c_double]),
+    "svmd_dsmo_destroy": (None, [c_void_p]),
+    "svmd_dsmo_world": (c_int32, [c_void_p]),
+    "svmd_dsmo_plan": (c_int32, [c_int64, c_int32, c_int32, c_int32, _P]),
+    "svmd_dsmo_fit": (c_int32, [c_void_p, _P, c_int32, _P, c_int64, c_int64, POINTER(SvmParams), _P,
+                                POINTER(SvmResult), _P, _P, c_int64, _P, _P, _P]),
+    "svmd_dsmo_rank_create": (c_void_p, [c_int32, c_int32, c_int32, c_double]),
+    "svmd_dsmo_handle_bytes": (c_int64, []),
+    "svmd_dsmo_rank_handle": (c_int32, [c_void_p, _P, c_int64]),
+    "svmd_dsmo_rank_connect": (c_int32, [c_void_p, _P]),
+    "svmd_dsmo_rank_prepare": (c_int32, [c_void_p, _P, c_int32, _P, c_int64, c_int64, POINTER(SvmParams)]),
+    "svmd_dsmo_rank_solve": (c_int32, [c_void_p, _P, POINTER(SvmResult), _P, _P, _P, _P, _P]),
     "svmd_trace_push": (None, [c_char_p]),
     "svmd_trace_pop": (None, []),
 }

@@ -139,9 +139,15 @@ int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const Q
                   int32_t* N0, double* WN, bool* ok);
 int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, double* stw, int64_t n,
                      const QuantPlan& P, double gamma, double* K, int64_t ldk);
+int launch_igram_slab(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+                      int64_t n, int64_t col0, int64_t ncols, const QuantPlan& P, double gamma, double* K,
+                      int64_t ldk);
 int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
                  const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used);
 size_t igram_u8_workspace(int64_t n, const QuantPlan& P);
+size_t quantize_u8_aux_bytes(const QuantPlan& P);
+int quantize_u8_rows(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                     const QuantPlan& P, void* aux, int8_t* Q, int32_t* N0, double* WN, bool* ok);
 int launch_minmax_u8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, double* mn, double* mx, double* scratch,
                      size_t scratch_doubles);
 int launch_sv_rows_u8(hipStream_t s, const uint8_t* X, int64_t d, const int64_t* idx, int64_t k, const double* mn,

@@ -285,14 +285,15 @@ __global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict
 // off-diagonal tile also stored transposed.  kq = int8 columns (multiple of BK); columns
 // [0, main0) are the extra groups (main0 a multiple of 32), step_w[s] = weight of k-step s's group
 // if s is the LAST k-step of its group (flush), else 0.  BK = int8 columns per LDS stage.
-// RECT: the block K(rows [0, n), rows [0, ncols)) of the same quantised set instead of the
-// symmetric Gram (every 128 x 128 tile of the tiles x ctiles grid, no mirror), e.g. the kernel
-// values of a training set against its leading support vectors (the cascade's warm-start check).
+// RECT: the block K(rows [0, n), rows [col0, col0 + ncols)) of the same quantised set instead of the
+// symmetric Gram (every 128 x 128 tile of the tiles x ctiles grid, no mirror; column j of the block
+// at K[i * ldk + j]), e.g. the kernel values of a training set against its leading support vectors
+// (the cascade's warm-start check) or a distributed-SMO team's slab K(:, own) (dsmo.hip).
 template <bool EXTRA, int BK, bool RECT = false>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
-    double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols) {
+    double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols, int64_t col0 = 0) {
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
   constexpr int CPR = BK / 16;            // 16-byte chunks per staged row
@@ -309,7 +310,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   double* img = reinterpret_cast<double*>(smem + kTableBytes);  // epilogue: per-wave 32x33 images
 
   const int64_t ctiles = RECT ? (ncols + QBM - 1) / QBM : tiles;
-  const int64_t ncol = RECT ? ncols : n;  // column bound
+  const int64_t ncol = RECT ? ncols : n;  // column bound (block-local)
+  const int64_t c0 = RECT ? col0 : 0;      // global row index of block column 0
   const int64_t ntile = RECT ? tiles * ctiles : tiles * (tiles + 1) / 2;
   const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
   int64_t tm, tn;
@@ -331,8 +333,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     if (EXTRA) wn_r[t] = gi < n ? WN[gi] : 0.0;
   } else if (t < QBM + QBN) {
     const int64_t gj = bn + (t - QBM);
-    n0_c[t - QBM] = gj < ncol ? N0[gj] : 0;
-    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[gj] : 0.0;
+    n0_c[t - QBM] = gj < ncol ? N0[c0 + gj] : 0;
+    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[c0 + gj] : 0.0;
   }
 
   // Staging per BK-column stage: thread t copies 16-byte chunk t % CPR of rows t / CPR + RPP * p.
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 #pragma unroll
     for (int p = 0; p < BPASS; ++p) {
       const int64_t r = bn + srow + RPP * p;
-      gb[p] = r < n ? *reinterpret_cast<const i32x4*>(Q + r * kq + k0 + scol) : zero4;
+      gb[p] = r < (RECT ? ncol : n) ? *reinterpret_cast<const i32x4*>(Q + (c0 + r) * kq + k0 + scol) : zero4;
     }
   };
   gload(0);
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
         const int ro = (r & 3) + 8 * (r >> 2);
         const int rl = ro + 4 * h;
         const int64_t gi = row0 + ro;
-        const double kv = gi == gj ? 1.0 : ex[q];
+        const double kv = gi == c0 + gj ? 1.0 : ex[q];
         if (interior || (gi < n && gj < ncol)) __builtin_nontemporal_store(kv, kp + int64_t(ro) * ldk);
         if (mirror) im[l32 * 33 + rl] = kv;  // im[col][row]
       }
@@ -685,17 +687,20 @@ int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const do
   return SVM_OK;
 }
 
-// run_igram on uint8 pixel rows Xu (n x d, contiguous, device) whose column min / max (host, d
-// values) the plan was built from: quantised without FP64 rows.  *used = false (nothing written)
-// when the plan does not apply to these statistics (non-integer minima or ranges).
-int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
-                 const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used) {
-  *used = false;
+// Quantise uint8 pixel rows Xu (n x d, contiguous, device) straight from the bytes with the plan P
+// built from their column min / max (host, d values): Q (n x P.kq), N0, WN exactly as
+// quantize_rows on the scaled FP64 rows.  *ok = false (nothing usable) when the plan does not apply
+// to these statistics (non-integer minima or ranges) or a value fails the check.  aux holds
+// quantize_u8_aux_bytes(P) bytes.  Synchronises the stream (reads the flag).
+size_t quantize_u8_aux_bytes(const QuantPlan& P) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  return 2 * al(P.perm.size() * 4) + al(P.wx.size() * 8) + 256;
+}
+
+int quantize_u8_rows(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                     const QuantPlan& P, void* aux, int8_t* Q, int32_t* N0, double* WN, bool* ok) {
+  *ok = false;
   if (!P.ok || n <= 0 || P.kq > kQuantLdsMaxKq) return SVM_OK;
-  if (ldk < n) {
-    set_error("igram: ldk < n");
-    return SVM_ERR_ARG;
-  }
   std::vector<int32_t> pack(P.perm.size(), 0);
   for (size_t k = 0; k < P.perm.size(); ++k) {
     const int32_t j = P.perm[k];
@@ -707,16 +712,12 @@ int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const d
     pack[k] = int32_t(mn) | (int32_t(fac) << 8) | (int32_t(P.off[k]) << 16);
   }
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  char* p = static_cast<char*>(ws);
+  char* p = static_cast<char*>(aux);
   auto take = [&](size_t bytes) {
     char* q = p;
     p += al(bytes);
     return q;
   };
-  auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
-  auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
-  auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
-  auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
   auto* perm = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
   auto* pk = reinterpret_cast<int32_t*>(take(P.perm.size() * 4));
   auto* wx = reinterpret_cast<double*>(take(P.wx.size() * 8));
@@ -733,8 +734,37 @@ int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const d
   unsigned hfail = 1;
   SVMD_CHECK(hipMemcpyAsync(&hfail, fail, 4, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipStreamSynchronize(s));
-  if (hfail) return SVM_OK;
-  int rc = launch_igram_sym(s, Q, N0, WN, stw, n, P, gamma, K, ldk);
+  *ok = hfail == 0;
+  return SVM_OK;
+}
+
+// run_igram on uint8 pixel rows Xu (n x d, contiguous, device) whose column min / max (host, d
+// values) the plan was built from: quantised without FP64 rows.  *used = false (nothing written)
+// when the plan does not apply to these statistics (non-integer minima or ranges).
+int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                 const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used) {
+  *used = false;
+  if (!P.ok || n <= 0 || P.kq > kQuantLdsMaxKq) return SVM_OK;
+  if (ldk < n) {
+    set_error("igram: ldk < n");
+    return SVM_ERR_ARG;
+  }
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += al(bytes);
+    return q;
+  };
+  auto* Q = reinterpret_cast<int8_t*>(take(size_t(n) * size_t(P.kq)));
+  auto* N0 = reinterpret_cast<int32_t*>(take(size_t(n) * 4));
+  auto* WN = reinterpret_cast<double*>(take(size_t(n) * 8));
+  auto* stw = reinterpret_cast<double*>(take(P.step_w.size() * 8));
+  bool ok = false;
+  int rc = quantize_u8_rows(s, Xu, n, d, mn_h, mx_h, P, p, Q, N0, WN, &ok);
+  if (rc) return rc;
+  if (!ok) return SVM_OK;
+  rc = launch_igram_sym(s, Q, N0, WN, stw, n, P, gamma, K, ldk);
   if (rc) return rc;
   *used = true;
   return SVM_OK;
@@ -791,6 +821,37 @@ int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64
 #undef SVM_IGRAM_BLOCK
   SVMD_LAUNCH_CHECK();
   *used = true;
+  return SVM_OK;
+}
+
+// K(rows [0, n), rows [col0, col0 + ncols)) of already quantised rows (Q, N0, WN; step weights
+// on the device in stw) into K (n x ldk, ldk >= ncols): a distributed-SMO team's slab, bit-identical
+// to those entries of the symmetric Gram.
+int launch_igram_slab(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+                      int64_t n, int64_t col0, int64_t ncols, const QuantPlan& P, double gamma, double* K,
+                      int64_t ldk) {
+  if (n <= 0 || ncols <= 0) return SVM_OK;
+  if (col0 < 0 || col0 + ncols > n || ldk < ncols) {
+    set_error("igram slab: need 0 <= col0, col0 + ncols <= n and ldk >= ncols");
+    return SVM_ERR_ARG;
+  }
+  const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (ncols + QBM - 1) / QBM;
+  const int64_t nwg = 2 * tiles * ctiles;
+  if (nwg > 0x7FFFFFFF) {
+    set_error("igram slab: problem too large for one launch");
+    return SVM_ERR_ARG;
+  }
+  const int bk = P.kq % 128 == 0 ? 128 : 64;
+#define SVM_IGRAM_SLAB(EX, B)                                                                                  \
+  hipLaunchKernelGGL((igram_tri_kernel<EX, B, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, \
+                     N0, WN, stw, P.w0, -gamma, K, ldk, tiles, ncols, col0)
+  if (P.main0 > 0) {
+    if (bk == 128) SVM_IGRAM_SLAB(true, 128); else SVM_IGRAM_SLAB(true, 64);
+  } else {
+    if (bk == 128) SVM_IGRAM_SLAB(false, 128); else SVM_IGRAM_SLAB(false, 64);
+  }
+#undef SVM_IGRAM_SLAB
+  SVMD_LAUNCH_CHECK();
   return SVM_OK;
 }
 

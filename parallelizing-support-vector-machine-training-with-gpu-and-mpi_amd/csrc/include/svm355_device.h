@@ -189,6 +189,39 @@ SVM_API int svmd_cascade_group_broken(void* group);  // 1 once a failure aborted
 SVM_API int svmd_rccl_info(int32_t* header_code, int32_t* runtime_code, char* path, int64_t cap);
 SVM_API void svmd_cascade_rank_destroy(void* rank);
 
+// ---- Distributed SMO (csrc/hip/dsmo.hip): ONE first-order SMO whose training points are split
+// over `world` teams -- one per GPU (rehearsal = 0: GPUs 0..world-1 of this process, peer access
+// between them) or all on GPU 0 (rehearsal != 0, one launch) -- each holding its slab K(:, own) of
+// the exact-integer Gram and exchanging the per-iteration candidates over xGMI.  The trajectory
+// (every pair, alpha and b) is the single-GPU resident solve's.  X: n x d uint8 pixel rows (host).
+// alpha_out: n doubles (host); timing_out (optional, 4 doubles): slowest GPU's upload+min/max,
+// quantise+slabs, solve and total ms; trace (optional, host): (i_high, i_low) per update;
+// shape_out (optional, 4 ints): threads per workgroup, points per thread, workgroups per team,
+// records per sweep lane; mn_out / mx_out (optional, d doubles each): the column statistics.
+SVM_API void* svmd_dsmo_create(int32_t world, int32_t rehearsal, double timeout_s);
+SVM_API void svmd_dsmo_destroy(void* group);
+SVM_API int svmd_dsmo_world(void* group);
+// Team plan for n points over P teams (ncu CUs per GPU; one_launch != 0: every team co-resident on
+// one GPU): out[6] = {threads per workgroup, points per thread, workgroups per team, records per
+// sweep lane, points per workgroup, points per team}.  Host only (no device needed).
+SVM_API int svmd_dsmo_plan(int64_t n, int32_t P, int32_t ncu, int32_t one_launch, int64_t* out);
+SVM_API int svmd_dsmo_fit(void* group, const void* X, int32_t u8, const int32_t* y, int64_t n, int64_t d,
+                          const svm_params* p, double* alpha_out, svm_result* r, double* timing_out, int64_t* trace,
+                          int64_t trace_cap, int32_t* shape_out, double* mn_out, double* mx_out);
+// One team per process (e.g. torchrun): create on this rank's GPU, export the receive array
+// (svmd_dsmo_rank_handle, svmd_dsmo_handle_bytes() bytes), all-gather the handles through the
+// launcher, connect (opens the peers' arrays over IPC).  A fit = rank_prepare (rows, slab) on every
+// rank, a launcher barrier, then rank_solve on every rank (the launch; this rank's alpha slice,
+// range_out = its [col0, ncols)).
+SVM_API void* svmd_dsmo_rank_create(int32_t device, int32_t world, int32_t rank, double timeout_s);
+SVM_API int64_t svmd_dsmo_handle_bytes(void);
+SVM_API int svmd_dsmo_rank_handle(void* rank, uint8_t* out, int64_t cap);
+SVM_API int svmd_dsmo_rank_connect(void* rank, const uint8_t* handles);
+SVM_API int svmd_dsmo_rank_prepare(void* rank, const void* X, int32_t u8, const int32_t* y, int64_t n, int64_t d,
+                                   const svm_params* p);
+SVM_API int svmd_dsmo_rank_solve(void* rank, double* alpha_out, svm_result* r, double* timing_out, int32_t* shape_out,
+                                 double* mn_out, double* mx_out, int64_t* range_out);
+
 // roctx ranges (rocprofv3 --marker-trace); the library already brackets preprocess / gram / smo /
 // decision, these let callers mark their own phases (e.g. cascade rounds and exchanges).
 SVM_API void svmd_trace_push(const char* name);

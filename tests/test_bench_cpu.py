@@ -61,3 +61,34 @@ def test_cpu_solve_log_has_the_fields_the_critical_path_reads():
         assert s["row_cache"] is False and s["solo_ms"] < 0  # CPU backend: no row cache, no solo timing
     rows, tot = critical_path(r.solves, "star")
     assert len(rows) == r.rounds and tot > 0
+
+
+@pytest.mark.parametrize("topology,gpus", [("star", 2), ("tree", 4)])
+def test_bench_in_process_thread_ranks_json(capsys, topology, gpus):
+    """bench.main with N > 1 launched directly (no torchrun): N thread-ranks in this process (here on the
+    CPU oracle: the cascade, since the distributed SMO needs GPUs).  The JSON line carries the fields
+    the SCALE driver reads, and its timed region fits inside the call's wall time."""
+    import json
+    import time
+
+    t0 = time.time()
+    rc = bench.main(["--gpus", str(gpus), "--device", "cpu", "--rows", "1200", "--test-rows", "200", "--steps", "2",
+                     "--warmup", "1", "--topology", topology, "--baseline-1gpu", "1"])
+    wall = time.time() - t0
+    assert rc == 0
+    line = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == gpus and line["steps"] == 2 and line["warmup"] == 1
+    assert line["config"]["parallelism"] == f"cascade-{topology}-dp{gpus}"
+    assert line["scaling"] == "strong" and line["higher_is_better"] is False
+    assert line["launch"] == "in-process thread ranks"
+    assert 0 < line["ms_per_step"] * line["steps"] / 1e3 <= wall
+    assert line["value"] == pytest.approx(line["ms_per_step"] / 1e3, rel=1e-3)
+    assert line["speedup_vs_1gpu"] > 0 and line["single_gpu_s"] > 0
+    assert line["sv_history"] and len(line["per_round_critical_path"]) == line["rounds"]
+    assert line["fallback_reason"] == "cpu device"  # --parallel auto: no distributed SMO on the CPU
+    assert line["transport"] == "loopback"
+
+
+def test_bench_smo_refuses_cpu(capsys):
+    assert bench.main(["--gpus", "2", "--device", "cpu", "--parallel", "smo", "--rows", "600", "--steps", "1"]) == 2
+    assert "needs uint8 pixel rows on GPUs" in capsys.readouterr().err

@@ -17,8 +17,8 @@ import pytest
 
 from svm355 import SVC, SVMParams
 from svm355._native import NativeError
-from svm355.parallel.cascade import CascadeSVM
-from svm355.parallel.rccl import DeviceGroup, RcclRank
+from svm355.parallel.cascade import CascadeSVM, preflight_script
+from svm355.parallel.rccl import DeviceGroup, RcclRank, rccl_info
 from svm355.utils.data import synthetic_mnist
 
 pytestmark = pytest.mark.gpu
@@ -193,6 +193,52 @@ def test_rccl_failure_aborts_the_communicator(data):
             CascadeSVM(SVMParams()).fit(X, tr.y, world=1, device="cuda", group=g)
     finally:
         g.close()
+
+
+def test_rccl_preflight_and_runtime_identity():
+    """Group creation runs the preflight (every driver op with checked payloads); running it again
+    explicitly passes; the RCCL runtime is identified (version + path of the loaded librccl)."""
+    info = rccl_info()
+    assert info["rccl_runtime"].startswith("2.") and info["rccl_path"].endswith((".so", ".so.1")) or "librccl" in \
+        info["rccl_path"], info
+    g = DeviceGroup(1, "rccl")
+    try:
+        g.exercise(preflight_script(1, 1 << 20))
+        assert not g.broken
+    finally:
+        g.close()
+    rank = RcclRank(0, RcclRank.unique_id(), 1, 0, comm_timeout_s=60)  # ncclCommInitRank + preflight
+    try:
+        rank.exercise(preflight_script(1, 1 << 20))
+    finally:
+        rank.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_preflight_on_device_loopback_ranks(world):
+    """The preflight op set over P HIP-backend ranks sharing this GPU (strict loopback): device
+    buffers, host staging, every payload checked; a mismatched sequence fails naming the ranks."""
+    g = DeviceGroup(world, "loopback")
+    try:
+        g.exercise(preflight_script(world, 1 << 20), timeout_s=30)
+        with pytest.raises(NativeError, match="mismatch"):
+            g.exercise("|".join(["bc:64@0"] + ["bc:128@0"] * (world - 1)), timeout_s=10)
+        g.exercise(preflight_script(world, 4096))  # loopback groups stay usable after a failure
+    finally:
+        g.close()
+
+
+def test_shared_group_is_rebuilt_after_an_rccl_failure(data):
+    """a failed RCCL fit aborts the shared group's communicators; the next fit through
+    DeviceGroup.shared must build a new group instead of failing with 'create a new group'."""
+    tr, _ = data
+    X = tr.compact().X
+    DeviceGroup.release_shared()
+    with pytest.raises(NativeError, match="rank 0: injected failure"):
+        CascadeSVM(SVMParams(), fail_rank=0, fail_round=0).fit(X, tr.y, world=1, device="cuda", transport="rccl")
+    r = CascadeSVM(SVMParams()).fit(X, tr.y, world=1, device="cuda", transport="rccl").result
+    assert r.converged and r.transport == "rccl"
+    DeviceGroup.release_shared()
 
 
 def _cli(tmp_path, name, *extra):
