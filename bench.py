@@ -51,10 +51,6 @@ METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV pa
 PREFLIGHT_ROWS = 4096
 
 
-class FallBack(Exception):
-    """The distributed SMO cannot run here: the bench continues with the cascade."""
-
-
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,7 +93,7 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per process under torchrun; with one process (--cascade) the same per-process path runs
     # on a single GPU, so a one-GPU box rehearses the launch the N-GPU run takes
-    multiproc = world_env > 1 or ("LOCAL_RANK" in os.environ and a.cascade)
+    multiproc = world_env > 1 or ("LOCAL_RANK" in os.environ and (a.cascade or a.parallel == "smo"))
     if multiproc and world_env != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
@@ -120,7 +116,7 @@ def main(argv=None):
         torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
     sync = (lambda: torch.cuda.synchronize(dev)) if not cpu else (lambda: None)
-    distributed = a.gpus > 1 or a.cascade
+    distributed = a.gpus > 1 or a.cascade or a.parallel == "smo"
     dist = None
     if multiproc:
         import torch.distributed as dist
@@ -138,6 +134,7 @@ def main(argv=None):
     pixel = full.X.dtype == np.uint8 and full.X.dtype == part.X.dtype
 
     mode = "single" if not distributed else a.parallel
+    auto = mode == "auto"
     fallback_reason = None
     if mode == "auto":
         mode = "smo" if (pixel and not cpu and a.wss == "first" and not a.cascade and a.gpus <= 8) else "cascade"
@@ -193,7 +190,8 @@ def main(argv=None):
                     h.close()
             dgroup = drank = None
 
-    if mode == "cascade":
+    # auto with both applicable: the cascade is set up too and the faster measured fit runs (below)
+    if mode == "cascade" or (auto and mode == "smo"):
         if multiproc and cpu:
             from svm355.parallel.hostcomm import HostCommRank
 
@@ -238,6 +236,39 @@ def main(argv=None):
                 print(f"bench.py rank {rank}: {mode} fit failed: {e}", file=sys.stderr, flush=True)
                 os._exit(1)
             raise
+
+    auto_selection = None
+    if auto and mode == "smo":
+        # Both N-GPU trainers apply: time one warm fit of each (bracketed like the timed steps, max
+        # over ranks) and run the faster.  The distributed SMO's model is the single-GPU trainer's;
+        # the cascade's is the reference's multi-processor algorithm.
+        def once():
+            guarded_step()  # warm
+            barrier_sync()
+            tt = time.perf_counter()
+            guarded_step()
+            barrier_sync()
+            dt = torch.tensor([time.perf_counter() - tt], dtype=torch.float64)
+            if dist is not None:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            return float(dt.item()) * 1e3
+
+        t_smo = once()
+        mode = "cascade"
+        t_casc = once()
+        mode = "smo" if t_smo <= t_casc else "cascade"
+        auto_selection = {"smo_fit_ms": round(t_smo, 3), "cascade_fit_ms": round(t_casc, 3), "chosen": mode}
+        if mode == "smo":
+            for h in (crank, group):
+                if h is not None:
+                    h.close()
+            crank = group = None
+        else:
+            for h in (dgroup, drank):
+                if h is not None:
+                    h.close()
+            dgroup = drank = None
+            fallback_reason = "the cascade's measured fit was faster"
 
     warm_ms = []
     for _ in range(a.warmup):
@@ -365,6 +396,8 @@ def main(argv=None):
                                                       np.array_equal(one.alpha_, model.alpha_))
         if dist is not None:
             dist.barrier()
+    if auto_selection is not None:
+        extra["auto_selection"] = auto_selection
     if distributed and not cpu:
         try:
             from svm355.parallel.rccl import rccl_info

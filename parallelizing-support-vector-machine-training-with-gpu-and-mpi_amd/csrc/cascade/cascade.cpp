@@ -304,12 +304,12 @@ class Rank {
       }
     }
     auto tm = timer(kPhSelect);
-    std::vector<double> a(size_t(S.k));
-    B_.d2h(a.data(), S.a.get(), S.k * 8);
     std::vector<int64_t> keep;
-    for (int64_t i = 0; i < S.k; ++i)
-      if (a[size_t(i)] > cfg_.params.sv_tol) keep.push_back(i);
-    DSet out = assemble({Segment{&S, nullptr, 0, nullptr, &keep, false}});
+    const int64_t* keep_dev = nullptr;
+    B_.select_svs(S, cfg_.params.sv_tol, &keep, &keep_dev);
+    Segment seg{&S, nullptr, 0, nullptr, &keep, false};
+    seg.idx_dev = keep_dev;
+    DSet out = assemble({seg});
     log.push_back(
         SolveLog{t_.rank(), rnd, layer, S.k, st.iterations, ms_between(t0, Clock::now()), st.b, st.stop, st.gram_ms,
                               skipped_now, st.row_cache, B_.take_solo_ms()});
@@ -358,11 +358,16 @@ class Rank {
     t_.gather(pack_.get(), bytes, root ? recv_.get() : nullptr, 0);
     if (root) {
       g.ids.resize(size_t(t_.world()));
+      std::vector<const double*> recs;
+      std::vector<int64_t> ks;
+      std::vector<int64_t*> outs;
       for (int r = 1; r < t_.world(); ++r) {
         g.ids[size_t(r)].resize(size_t(g.counts[size_t(r)]));
-        if (g.counts[size_t(r)])
-          B_.record_ids(record(g, r), g.counts[size_t(r)], ld_, g.ids[size_t(r)].data());
+        recs.push_back(record(g, r));
+        ks.push_back(g.counts[size_t(r)]);
+        outs.push_back(g.ids[size_t(r)].data());
       }
+      B_.record_ids_batch(recs, ks, ld_, outs);  // one host round trip for all sources
     }
     return g;
   }

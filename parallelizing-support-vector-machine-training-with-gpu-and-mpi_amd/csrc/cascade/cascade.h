@@ -122,6 +122,9 @@ struct Segment {
   const int64_t* rec_ids = nullptr;  // host ids of the records
   const std::vector<int64_t>* idx = nullptr;
   bool zero_alpha = false;
+  // Optional backend-memory copy of *idx (already there, e.g. from select_svs): assemble uses it
+  // instead of staging idx again.
+  const int64_t* idx_dev = nullptr;
   int64_t rows() const { return idx ? int64_t(idx->size()) : (set ? set->k : rec_rows); }
 };
 
@@ -155,6 +158,24 @@ class Backend {
   virtual void pack(const DSet& S, int64_t ld, double* rec) = 0;
   // ids[i] = record i's id, i < k.
   virtual void record_ids(const double* rec, int64_t k, int64_t ld, int64_t* ids_host) = 0;
+  // Several record buffers at once (one host round trip on a device backend): ids_host[s][i] =
+  // record i's id of source s, i < ks[s].
+  virtual void record_ids_batch(const std::vector<const double*>& recs, const std::vector<int64_t>& ks, int64_t ld,
+                                const std::vector<int64_t*>& ids_host) {
+    for (size_t s = 0; s < recs.size(); ++s)
+      if (ks[s]) record_ids(recs[s], ks[s], ld, ids_host[s]);
+  }
+  // Ascending indices of S's rows with alpha > tol (SV extraction, main3.cpp:297-304) into keep;
+  // *keep_dev = a backend-memory copy of them valid until the next call (nullptr: none, assemble
+  // stages keep itself).  Default: alphas read back to the host.
+  virtual void select_svs(const DSet& S, double tol, std::vector<int64_t>* keep, const int64_t** keep_dev) {
+    std::vector<double> a(static_cast<size_t>(S.k));
+    if (S.k) d2h(a.data(), S.a.get(), S.k * 8);
+    keep->clear();
+    for (int64_t i = 0; i < S.k; ++i)
+      if (a[size_t(i)] > tol) keep->push_back(i);
+    *keep_dev = nullptr;
+  }
   // Warm-start SMO (SMO_train(..., init=false), mpi_svm_main3.cpp:155-290) on S: alphas in S.a
   // are updated in place.  mn_h/mx_h: the global scaling statistics (host, d values).
   virtual SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) = 0;

@@ -95,6 +95,41 @@ __global__ void record_ids_kernel(const double* __restrict__ rec, int64_t k, int
   if (i < k) out[i] = int64_t(rec[i * w + ld + 2]);
 }
 
+// SV extraction on the device (main3.cpp:297-304): the ascending indices i < k with a[i] > tol, to
+// keep_d (device) and keep_h (pinned host), and their count to *count_h.  One 1024-thread workgroup
+// walks the set in 1024-element chunks: per wave a ballot + prefix count, per chunk the wave totals.
+__global__ __launch_bounds__(1024) void select_svs_kernel(const double* __restrict__ a, int64_t k, double tol,
+                                                          int64_t* __restrict__ keep_d, int64_t* __restrict__ keep_h,
+                                                          int64_t* __restrict__ count_h) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t c0 = 0; c0 < k; c0 += 1024) {
+    const int64_t i = c0 + threadIdx.x;
+    const bool f = i < k && a[i] > tol;
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int64_t off = base;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    if (f) {
+      const int64_t pos = off + __popcll(m & ((1ull << lane) - 1ull));
+      keep_d[pos] = i;
+      keep_h[pos] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t t = 0;
+      for (int q = 0; q < 16; ++q) t += wsum[q];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count_h = base;
+}
+
 __global__ void coef_kernel(const double* __restrict__ a, const int32_t* __restrict__ y, int64_t nz,
                             double* __restrict__ coef) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -164,9 +199,9 @@ class HipBackend final : public Backend {
     (void)hipSetDevice(device_);
     (void)hipStreamSynchronize(stream_);
     for (auto& kv : cache_) (void)hipFree(kv.second);
-    for (auto& kv : live_) (void)hipFree(kv.first);
-    for (void* q : {idx_, ids_d_, sqn_, kkt_})
-      if (q) (void)hipFree(q);
+    for (auto& kv : live_) (void)hipFree(kv.first);  // includes the grow() scratch (allocator blocks)
+    if (pinned_) (void)hipHostFree(pinned_);
+    if (stage_ev_) (void)hipEventDestroy(stage_ev_);
     svmd_destroy(ctx_);
   }
   HipBackend(const HipBackend&) = delete;
@@ -234,7 +269,7 @@ class HipBackend final : public Backend {
     const int64_t m = s.rows();
     if (!m) return;
     const int64_t* idx = nullptr;
-    if (s.idx) idx = stage_idx(*s.idx);
+    if (s.idx) idx = s.idx_dev ? s.idx_dev : stage_idx(*s.idx);
     if (s.set) {
       hipLaunchKernelGGL(assemble_set_kernel, dim3(row_grid(m)), dim3(256), 0, stream_, s.set->X.as<double>(),
                          s.set->y.as<int32_t>(), s.set->a.as<double>(), s.set->id.as<int64_t>(), idx, m, ld,
@@ -260,6 +295,48 @@ class HipBackend final : public Backend {
                        static_cast<int64_t*>(ids_d_));
     hipcheck(hipGetLastError(), "record_ids kernel");
     d2h(ids, ids_d_, k * 8);
+  }
+  void record_ids_batch(const std::vector<const double*>& recs, const std::vector<int64_t>& ks, int64_t ld,
+                        const std::vector<int64_t*>& ids) override {
+    int64_t tot = 0;
+    for (int64_t k : ks) tot += k;
+    if (!tot) return;
+    grow(&ids_d_, &ids_cap_, size_t(tot) * 8);
+    int64_t off = 0;
+    for (size_t q = 0; q < recs.size(); ++q) {
+      if (!ks[q]) continue;
+      hipLaunchKernelGGL(record_ids_kernel, dim3(unsigned((ks[q] + 255) / 256)), dim3(256), 0, stream_, recs[q], ks[q],
+                         ld + 3, ld, static_cast<int64_t*>(ids_d_) + off);
+      hipcheck(hipGetLastError(), "record_ids kernel");
+      off += ks[q];
+    }
+    std::vector<int64_t> all(static_cast<size_t>(tot));
+    d2h(all.data(), ids_d_, tot * 8);  // one round trip for every source
+    off = 0;
+    for (size_t q = 0; q < recs.size(); ++q) {
+      std::copy(all.begin() + off, all.begin() + off + ks[q], ids[q]);
+      off += ks[q];
+    }
+  }
+  // Device-side SV selection: the indices land in device memory (for the assembly kernel) and in
+  // pinned host memory (for the host id mirror) with one synchronisation, instead of an alpha read
+  // back, a host scan and an index upload.
+  void select_svs(const DSet& S, double tol, std::vector<int64_t>* keep, const int64_t** keep_dev) override {
+    keep->clear();
+    *keep_dev = nullptr;
+    if (!S.k) return;
+    grow(&sel_d_, &sel_cap_, size_t(S.k) * 8);
+    grow_pinned(size_t(S.k) * 8 + 64);
+    auto* cnt = reinterpret_cast<int64_t*>(pinned_);
+    auto* kh = cnt + 8;
+    *cnt = -1;
+    hipLaunchKernelGGL(select_svs_kernel, dim3(1), dim3(1024), 0, stream_, S.a.as<double>(), S.k, tol,
+                       static_cast<int64_t*>(sel_d_), kh, cnt);
+    hipcheck(hipGetLastError(), "select kernel");
+    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (*cnt < 0 || *cnt > S.k) throw CascadeError("device SV selection returned no count");
+    keep->assign(kh, kh + *cnt);
+    *keep_dev = static_cast<const int64_t*>(sel_d_);
   }
   SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
     if (!(serial_ && release_gram_)) return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
@@ -386,22 +463,48 @@ class HipBackend final : public Backend {
   static void hipcheck(hipError_t e, const char* what) {
     if (e != hipSuccess) throw CascadeError(std::string(what) + ": " + hipGetErrorString(e));
   }
+  // Grow-only scratch through the size-class caching allocator: the old block goes back to the
+  // cache (reuse is stream-ordered: every user runs on this backend's one stream), no sync, no
+  // hipFree.
   void grow(void** p, size_t* cap, size_t bytes) {
     if (bytes <= *cap) return;
-    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-    if (*p) hipcheck(hipFree(*p), "hipFree");
+    if (*p) free(*p);
     *p = nullptr;
     *cap = 0;
     const size_t sz = std::max<size_t>(bytes, 4096) * 2;
-    hipcheck(hipMalloc(p, sz), "hipMalloc");
+    *p = alloc(int64_t(sz));
     *cap = sz;
   }
+  // Pinned host staging area (grow-only; waits for the copy still reading it before it is reused).
+  void grow_pinned(size_t bytes) {
+    wait_staged();
+    if (bytes <= pinned_cap_) return;
+    if (pinned_) {
+      hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");  // a kernel may still write it
+      hipcheck(hipHostFree(pinned_), "hipHostFree");
+    }
+    pinned_ = nullptr;
+    pinned_cap_ = 0;
+    const size_t sz = std::max<size_t>(bytes, 1 << 16) * 2;
+    hipcheck(hipHostMalloc(&pinned_, sz, hipHostMallocDefault), "hipHostMalloc");
+    pinned_cap_ = sz;
+  }
+  void wait_staged() {
+    if (staged_) {
+      hipcheck(hipEventSynchronize(stage_ev_), "hipEventSynchronize");
+      staged_ = false;
+    }
+  }
+  // Index list -> device through the pinned area with an asynchronous copy: the caller's vector may
+  // go away at once, and the next staging waits only for this copy (not for the whole stream).
   const int64_t* stage_idx(const std::vector<int64_t>& v) {
-    // one staging buffer per backend: the copy is stream-ordered after earlier users of it
     grow(&idx_, &idx_cap_, v.size() * 8);
-    hipcheck(hipMemcpyAsync(idx_, v.data(), v.size() * 8, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync idx");
-    // pageable source: make sure the host vector may be released by the caller
-    hipcheck(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    grow_pinned(v.size() * 8);
+    std::memcpy(pinned_, v.data(), v.size() * 8);
+    hipcheck(hipMemcpyAsync(idx_, pinned_, v.size() * 8, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync idx");
+    if (!stage_ev_) hipcheck(hipEventCreateWithFlags(&stage_ev_, hipEventDisableTiming), "hipEventCreate");
+    hipcheck(hipEventRecord(stage_ev_, stream_), "hipEventRecord");
+    staged_ = true;
     return static_cast<const int64_t*>(idx_);
   }
   void release_cache() {
@@ -415,8 +518,12 @@ class HipBackend final : public Backend {
   hipStream_t stream_ = nullptr;
   std::multimap<size_t, void*> cache_;
   std::map<void*, size_t> live_;
-  void *idx_ = nullptr, *ids_d_ = nullptr, *sqn_ = nullptr, *kkt_ = nullptr;
-  size_t idx_cap_ = 0, ids_cap_ = 0, sqn_cap_ = 0, kkt_cap_ = 0;
+  void *idx_ = nullptr, *ids_d_ = nullptr, *sqn_ = nullptr, *kkt_ = nullptr, *sel_d_ = nullptr;
+  size_t idx_cap_ = 0, ids_cap_ = 0, sqn_cap_ = 0, kkt_cap_ = 0, sel_cap_ = 0;
+  void* pinned_ = nullptr;  // host staging (index uploads, device SV selection results)
+  size_t pinned_cap_ = 0;
+  hipEvent_t stage_ev_ = nullptr;
+  bool staged_ = false;
   const bool serial_ = [] {
     const char* v = getenv("SVM355_CASCADE_SERIAL_SOLVES");
     return v && atoi(v) != 0;
