@@ -197,6 +197,9 @@ _HIP_SIGS = {
     "svmd_gather_rows": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P]),
     "svmd_train_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, _P, _P, c_int32, POINTER(SvmParams),
                                 POINTER(SvmResult), _P, c_int64, POINTER(SvmdTiming), POINTER(c_int32)]),
+    "svmd_train_decomp_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, _P, _P, POINTER(SvmParams), c_int32,
+                                       POINTER(SvmResult), POINTER(SvmdTiming), POINTER(c_int64),
+                                       POINTER(c_int32)]),
     "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
     "svmd_rbf_gram_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, c_double, _P, c_int64, POINTER(c_int32)]),
     "svmd_sv_rows_u8": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P]),

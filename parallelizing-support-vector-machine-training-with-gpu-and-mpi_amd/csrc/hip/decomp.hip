@@ -1,0 +1,623 @@
+// Working-set decomposition SMO (opt-in, SVC(solver="decomp")): the reference's first-order SMO
+// semantics per pair, but on a WORKING SET of up to q points at a time -- the SMO-type decomposition
+// of LIBSVM / ThunderSVM re-designed for MI355X.
+//
+// The reference (main3.cpp:162-294, gpu_svm_main3.cu:318-483) updates ONE pair per iteration over
+// all n points, so a GPU iteration is bound by a grid-wide exchange (~3.4 us at 60k even
+// persistent).  Here one outer iteration is:
+//   1. ws_select_kernel   per block of the points, its T most violating of I_high (smallest f) and
+//                         of I_low (largest f), lowest index on ties -- the union always holds the
+//                         globally maximal violating pair, so every outer iteration makes progress;
+//   2. ws_build_kernel    one workgroup: the stop test on the global extremes (b_low <= b_high + 2 tau,
+//                         main3.cpp:213), then the sorted, de-duplicated working set W (m <= q);
+//   3. K(W, W)            the working set's rows gathered, its m x m Gram on the exact-integer path
+//                         (the same kernel values as the full Gram, igram.hip);
+//   4. ws_inner_kernel    ONE workgroup runs first-order SMO on W with the reference's update
+//                         arithmetic (clip bounds, eta, stop reasons) -- an iteration is a workgroup
+//                         reduction and two L2-resident row reads, no grid exchange -- until W's own
+//                         gap is below max(tau, gap / 10);
+//   5. f update           f += K(:, W) (delta alpha * y): the exact-integer kernel values of all n
+//                         rows against W computed on int8 MFMA and reduced in the epilogue
+//                         (igram_tri_kernel GEMV mode), never stored -- no n x n Gram at all.
+// The stop test is the reference's, on all n points, so the model meets the same optimality bound
+// (tests: the same support-vector set as the pairwise solve, b within the stop tolerance); the
+// sequence of pair updates differs, so iteration counts and b differ in the last digits.
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "persist.h"
+#include "svm355_device.h"
+#include "trace.h"
+
+namespace svm355 {
+namespace {
+
+struct DecompHost {  // pinned: written by the kernels, read by the host once per outer iteration
+  double b_high, b_low;
+  int32_t m, stop;
+  int64_t inner_it;
+  int32_t inner_reason, changed;  // changed: points whose alpha the inner solve moved
+};
+
+constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
+constexpr int kMaxWS = 1024;             // working-set capacity (one 1024-thread inner workgroup)
+
+// Per block b of `per` points: the T most violating points of I_high (smallest f) and of I_low
+// (largest f) in wave_arg's order (value, then lowest index): T rounds of a block arg-reduction, the
+// winner masked out by its owner after each round.  -1 = fewer than T candidates.
+__global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restrict__ f,
+                                                           const double* __restrict__ alpha,
+                                                           const int32_t* __restrict__ y, int64_t n, int64_t per,
+                                                           int T, double C, double eps, int32_t* __restrict__ cand_h,
+                                                           int32_t* __restrict__ cand_l) {
+  constexpr int NW = kSelNT / 64;
+  __shared__ double sv[2][NW];
+  __shared__ uint32_t si[2][NW];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t lo = int64_t(blockIdx.x) * per, hi = std::min<int64_t>(n, lo + per);
+  const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
+  double fh[kSelE], fl[kSelE];
+#pragma unroll
+  for (int e = 0; e < kSelE; ++e) {
+    const int64_t i = lo + t + int64_t(kSelNT) * e;
+    fh[e] = inf;
+    fl[e] = -inf;
+    if (i < hi) {
+      const double a = alpha[i], fi = f[i];
+      const int32_t yi = y[i];
+      if ((yi == 1 && a < c_hi) || (yi == -1 && a > c_lo)) fh[e] = fi;
+      if ((yi == 1 && a > c_lo) || (yi == -1 && a < c_hi)) fl[e] = fi;
+    }
+  }
+  for (int k = 0; k < T; ++k) {
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+#pragma unroll
+    for (int e = 0; e < kSelE; ++e) {  // ascending index within a thread: strict compares keep the lowest
+      const uint32_t i = uint32_t(lo + t + int64_t(kSelNT) * e);
+      if (fh[e] < mn.v) mn = VI{fh[e], i};
+      if (fl[e] > mx.v) mx = VI{fl[e], i};
+    }
+    const VIL a = wave_arg<true>(mn), b = wave_arg<false>(mx);
+    if (lane == 0) {
+      sv[0][w] = a.v;
+      si[0][w] = a.i;
+      sv[1][w] = b.v;
+      si[1][w] = b.i;
+    }
+    __syncthreads();
+    VI gm{sv[0][0], si[0][0]}, gx{sv[1][0], si[1][0]};
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      const VI cm{sv[0][q], si[0][q]}, cx{sv[1][q], si[1][q]};
+      if (beats<true>(cm, gm)) gm = cm;
+      if (beats<false>(cx, gx)) gx = cx;
+    }
+    __syncthreads();  // the LDS slots are rewritten next round
+    if (t == 0) {
+      cand_h[int64_t(blockIdx.x) * T + k] = (gm.i == kSentinel || !(gm.v < inf)) ? -1 : int32_t(gm.i);
+      cand_l[int64_t(blockIdx.x) * T + k] = (gx.i == kSentinel || !(gx.v > -inf)) ? -1 : int32_t(gx.i);
+    }
+#pragma unroll
+    for (int e = 0; e < kSelE; ++e) {
+      const uint32_t i = uint32_t(lo + t + int64_t(kSelNT) * e);
+      if (i == gm.i) fh[e] = inf;
+      if (i == gx.i) fl[e] = -inf;
+    }
+  }
+}
+
+// One workgroup: b_high = min f over the I_high candidates, b_low = max f over the I_low ones (the
+// global extremes: every block's first pick is its own extreme), the stop test, and the working set
+// = the sorted union of the candidates without duplicates (a free SV may be in both lists).
+__global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const int32_t* __restrict__ cand, int L, int Lh,
+                                                          const double* __restrict__ f, double tau,
+                                                          int32_t* __restrict__ W, DecompHost* __restrict__ hs) {
+  __shared__ int32_t s[kMaxWS];
+  __shared__ int32_t wsum[kMaxWS / 64];
+  __shared__ double red[2][kMaxWS / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int32_t c = t < L ? cand[t] : -1;
+  double vh = __builtin_inf(), vl = -__builtin_inf();
+  if (c >= 0) {
+    if (t < Lh)
+      vh = f[c];
+    else
+      vl = f[c];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    vh = fmin(vh, __shfl_xor(vh, off, 64));
+    vl = fmax(vl, __shfl_xor(vl, off, 64));
+  }
+  if (lane == 0) {
+    red[0][w] = vh;
+    red[1][w] = vl;
+  }
+  s[t] = c >= 0 ? c : INT_MAX;
+  __syncthreads();
+  // bitonic sort of the 1024 candidate ids (ascending; INT_MAX = empty)
+  for (int k = 2; k <= kMaxWS; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int p = t ^ j;
+      if (p > t) {
+        const int32_t x = s[t], y = s[p];
+        const bool up = (t & k) == 0;
+        if ((x > y) == up) {
+          s[t] = y;
+          s[p] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int32_t v = s[t];
+  const bool keep = v != INT_MAX && (t == 0 || s[t - 1] != v);
+  const unsigned long long bal = __ballot(keep);
+  if (lane == 0) wsum[w] = __popcll(bal);
+  __syncthreads();
+  int off = 0;
+  for (int q = 0; q < w; ++q) off += wsum[q];
+  if (keep) W[off + __popcll(bal & ((1ull << lane) - 1ull))] = v;
+  if (t == 0) {
+    int m = 0;
+    double bh = __builtin_inf(), bl = -__builtin_inf();
+    for (int q = 0; q < kMaxWS / 64; ++q) {
+      m += wsum[q];
+      bh = fmin(bh, red[0][q]);
+      bl = fmax(bl, red[1][q]);
+    }
+    hs->m = m;
+    hs->b_high = bh;
+    hs->b_low = bl;
+    // no candidate on either side: the reference's "i_high or i_low not found" (main3.cpp:205-209)
+    hs->stop = !(bh < __builtin_inf()) || !(bl > -__builtin_inf()) ? SVM_STOP_NO_CANDIDATE
+               : (bl <= bh + 2.0 * tau)                             ? SVM_STOP_CONVERGED
+                                                                    : SVM_STOP_RUNNING;
+  }
+}
+
+// Qw[k] = Q[W[k]] (kq bytes), N0w[k], WNw[k]: one workgroup per working-set row.
+__global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict__ Q, const int32_t* __restrict__ N0,
+                                                       const double* __restrict__ WN, int kq,
+                                                       const int32_t* __restrict__ W, int m, int8_t* __restrict__ Qw,
+                                                       int32_t* __restrict__ N0w, double* __restrict__ WNw) {
+  const int k = blockIdx.x;
+  if (k >= m) return;
+  const int64_t src = W[k];
+  const int4* s = reinterpret_cast<const int4*>(Q + src * int64_t(kq));
+  int4* d = reinterpret_cast<int4*>(Qw + int64_t(k) * kq);
+  for (int c = threadIdx.x; c < kq / 16; c += 64) d[c] = s[c];
+  if (threadIdx.x == 0) {
+    N0w[k] = N0[src];
+    WNw[k] = WN[src];
+  }
+}
+
+// First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER points
+// W[t + NT e] (f, alpha, y in registers); per iteration each wave's arg-reduction carries the
+// winners' alpha and y, ONE barrier publishes the per-wave candidates (double-buffered by iteration
+// parity), and every wave merges them itself with the lowest-index rule -- so all waves hold the
+// identical (i_high, i_low, b_high, b_low, alpha, y) without a second barrier.  Every thread then
+// evaluates the reference's clip / eta / update arithmetic on the same inputs (persist_solve's
+// sequence, main3.cpp:235-275) and applies f += ch K(i, .) + cl K(j, .) from the L2-resident
+// K(W, W); the two row reads and K12 are the iteration's only memory round trip.  Stops at W's own
+// gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points whose alpha changed
+// are compacted in position order: cols[j] = their global ids, coef[j] = (alpha_new - alpha_old) y,
+// *mcount = how many -- the f update of all n points reads only those columns.
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
+                                                      const int32_t* __restrict__ W, int m,
+                                                      const int32_t* __restrict__ y, double* __restrict__ alpha,
+                                                      const double* __restrict__ f, double C, double eps,
+                                                      double tau_in, int64_t max_inner, int32_t* __restrict__ cols,
+                                                      double* __restrict__ coef, int32_t* __restrict__ mcount,
+                                                      DecompHost* __restrict__ hs) {
+  constexpr int NW = NT / 64;
+  __shared__ int32_t wcnt[PER][NW];
+  __shared__ double pv[2][2][NW], pa[2][2][NW];
+  __shared__ uint32_t pi[2][2][NW];
+  __shared__ int32_t py[2][2][NW];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double a[PER], a0[PER], ft[PER];
+  int32_t yt[PER];  // y = 0 (padding) is in neither set
+  int64_t gid[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int k = t + NT * e;
+    const bool valid = k < m;
+    gid[e] = valid ? W[k] : 0;
+    a[e] = valid ? alpha[gid[e]] : 0.0;
+    a0[e] = a[e];
+    yt[e] = valid ? y[gid[e]] : 0;
+    ft[e] = valid ? f[gid[e]] : 0.0;
+  }
+  const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
+  int64_t it = 0;
+  int32_t reason = SVM_STOP_CONVERGED;
+  for (int par = 0;; par ^= 1) {
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+    double mna = 0.0, mxa = 0.0;
+    int32_t mny = 0, mxy = 0;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {  // ascending position within a thread: strict compares keep the lowest
+      const bool in_high = (yt[e] == 1 && a[e] < c_hi) || (yt[e] == -1 && a[e] > c_lo);
+      const bool in_low = (yt[e] == 1 && a[e] > c_lo) || (yt[e] == -1 && a[e] < c_hi);
+      if (in_high && ft[e] < mn.v) {
+        mn = VI{ft[e], uint32_t(t + NT * e)};
+        mna = a[e];
+        mny = yt[e];
+      }
+      if (in_low && ft[e] > mx.v) {
+        mx = VI{ft[e], uint32_t(t + NT * e)};
+        mxa = a[e];
+        mxy = yt[e];
+      }
+    }
+    const VIL wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
+    const double awmn = read_lane64(mna, wmn.lane), awmx = read_lane64(mxa, wmx.lane);
+    const int32_t ywmn = __builtin_amdgcn_readlane(mny, wmn.lane), ywmx = __builtin_amdgcn_readlane(mxy, wmx.lane);
+    if (lane == 0) {
+      pv[par][0][w] = wmn.v;
+      pi[par][0][w] = wmn.i;
+      pa[par][0][w] = awmn;
+      py[par][0][w] = ywmn;
+      pv[par][1][w] = wmx.v;
+      pi[par][1][w] = wmx.i;
+      pa[par][1][w] = awmx;
+      py[par][1][w] = ywmx;
+    }
+    __syncthreads();
+    VI ca{inf, kSentinel}, cb{-inf, kSentinel};
+    double caa = 0.0, cba = 0.0;
+    int32_t cay = 0, cby = 0;
+    if (lane < NW) {
+      ca = VI{pv[par][0][lane], pi[par][0][lane]};
+      cb = VI{pv[par][1][lane], pi[par][1][lane]};
+      caa = pa[par][0][lane];
+      cba = pa[par][1][lane];
+      cay = py[par][0][lane];
+      cby = py[par][1][lane];
+    }
+    const VIL ra = wave_arg<true, NW>(ca), rb = wave_arg<false, NW>(cb);
+    const uint32_t uih = ra.i, uil = rb.i;
+    if (uih == kSentinel || uil == kSentinel) {
+      reason = SVM_STOP_NO_CANDIDATE;
+      break;
+    }
+    const double bh = ra.v, bl = rb.v;
+    if (bl <= bh + 2.0 * tau_in) break;  // W's own optimum (reason stays CONVERGED)
+    if (it >= max_inner) {
+      reason = SVM_STOP_MAX_ITER;
+      break;
+    }
+    const int ih = int(uih), il = int(uil);
+    // one memory round trip: K12 and this thread's entries of the two rows
+    const double K12 = Kw[int64_t(ih) * ldw + il];
+    double kh[PER], kl[PER];
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int k = t + NT * e;
+      kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+      kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+    }
+    const double ah = read_lane64(caa, ra.lane), al = read_lane64(cba, rb.lane);
+    const int32_t yh = __builtin_amdgcn_readlane(cay, ra.lane), yl = __builtin_amdgcn_readlane(cby, rb.lane);
+    const double K11 = 1.0, K22 = 1.0;  // the Gram's unit diagonal
+    const int s = yh * yl;
+    const double eta = K11 + K22 - 2.0 * K12;
+    double U, V;
+    if (s == -1) {
+      U = fmax(0.0, al - ah);
+      V = fmin(C, C + al - ah);
+    } else {
+      U = fmax(0.0, al + ah - C);
+      V = fmin(C, al + ah);
+    }
+    if (!(U <= V + 1e-12)) {
+      reason = SVM_STOP_INFEASIBLE;
+      break;
+    }
+    if (eta <= eps) {
+      reason = SVM_STOP_NONPOS_ETA;
+      break;
+    }
+    double al_new = al + double(yl) * (bh - bl) / eta;
+    if (al_new > V) al_new = V;
+    if (al_new < U) al_new = U;
+    const double ah_new = ah + double(s) * (al - al_new);
+    const double ch = (ah_new - ah) * double(yh);
+    const double cl = (al_new - al) * double(yl);
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int k = t + NT * e;
+      ft[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
+      if (k == ih) a[e] = ah_new;
+      if (k == il) a[e] = al_new;
+    }
+    ++it;
+  }
+  unsigned long long bal[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int k = t + NT * e;
+    const bool changed = k < m && a[e] != a0[e];
+    if (changed) alpha[gid[e]] = a[e];
+    bal[e] = __ballot(changed);
+    if (lane == 0) wcnt[e][w] = __popcll(bal[e]);
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {  // position order k = t + NT e: e-major, then wave, then lane
+    int off = base;
+    for (int q = 0; q < NW; ++q) {
+      if (q < w) off += wcnt[e][q];
+      base += wcnt[e][q];
+    }
+    if ((bal[e] >> lane) & 1ull) {
+      const int j = off + __popcll(bal[e] & ((1ull << lane) - 1ull));
+      cols[j] = int32_t(gid[e]);
+      coef[j] = (a[e] - a0[e]) * double(yt[e]);
+    }
+  }
+  if (t == 0) {
+    *mcount = base;
+    hs->changed = base;
+    hs->inner_it = it;
+    hs->inner_reason = reason;
+  }
+}
+
+// f[i] += the first ceil(*mcount / 64) column halves of part (the ones the GEMV wrote).
+__global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __restrict__ part, int64_t ldp,
+                                                            const int32_t* __restrict__ mcount,
+                                                            double* __restrict__ f, int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int npart = (*mcount + 63) / 64;
+  if (i >= n || npart == 0) return;
+  const double* p = part + i * ldp;
+  double s = 0.0;
+  for (int c = 0; c < npart; ++c) s += p[c];
+  f[i] += s;
+}
+
+__global__ void ws_init_kernel(const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f,
+                               int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) {
+    alpha[i] = 0.0;
+    f[i] = -static_cast<double>(y[i]);  // main3.cpp:165-172
+  }
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+// Decomposition solve on quantised rows (Q, N0, WN, the plan's step weights in stw on the device).
+// alpha: n doubles (cold start: zeroed here).  q: working-set size (<= 1024).  stats (6 int64):
+// outer iterations, inner iterations, working-set size, solve microseconds, columns of the f updates
+// (points moved, summed over the outer iterations), inner workgroup size.
+int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+               const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
+               svm_result* r, int64_t* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t s = ctx->stream;
+  if (n < 2 || n >= int64_t(kSentinel) || n > (int64_t(1) << 31) - 1) {
+    set_error("decomposition SMO: need 2 <= n < 2^31");
+    return SVM_ERR_ARG;
+  }
+  qws = std::max(4, std::min(qws, kMaxWS));
+  // blocks of <= 4096 points; T candidates per side per block with 2 * NB * T <= 1024
+  const int64_t NB = std::max<int64_t>((n + kSelNT * kSelE - 1) / (kSelNT * kSelE), std::min<int64_t>(64, (n + 63) / 64));
+  const int T = int(std::max<int64_t>(1, qws / (2 * NB)));
+  const int64_t L = 2 * NB * T;
+  if (L > kMaxWS) {
+    set_error("decomposition SMO: n = %lld needs %lld candidates per round (> %d)", (long long)n, (long long)L, kMaxWS);
+    return SVM_ERR_ARG;
+  }
+  const int64_t per = (n + NB - 1) / NB;
+  if (per > int64_t(kSelNT) * kSelE) {
+    set_error("decomposition SMO: selection blocks too large");
+    return SVM_ERR_INTERNAL;
+  }
+  // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 256 | 512 | 1024
+  int inner_nt = 512;
+  if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
+  // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
+  double tau_frac = 0.1;
+  if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
+  const int64_t ldw = kMaxWS;            // K(W, W) row stride
+  const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += al(bytes);
+    return o;
+  };
+  const size_t o_f = take(size_t(n) * 8), o_cand = take(size_t(L) * 4), o_W = take(kMaxWS * 4),
+               o_Qw = take(size_t(kMaxWS) * P.kq), o_N0w = take(kMaxWS * 4), o_WNw = take(kMaxWS * 8),
+               o_Kw = take(size_t(kMaxWS) * ldw * 8),
+               o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4), o_mcount = take(256), o_part = take(size_t(n) * ldp * 8);
+  int rc = ctx->ensure_ws(off);
+  if (rc) return rc;
+  rc = ctx->ensure_pinned(sizeof(DecompHost) * 2);
+  if (rc) return rc;
+  char* ws = static_cast<char*>(ctx->ws);
+  auto* f = reinterpret_cast<double*>(ws + o_f);
+  auto* cand = reinterpret_cast<int32_t*>(ws + o_cand);
+  auto* W = reinterpret_cast<int32_t*>(ws + o_W);
+  auto* Qw = reinterpret_cast<int8_t*>(ws + o_Qw);
+  auto* N0w = reinterpret_cast<int32_t*>(ws + o_N0w);
+  auto* WNw = reinterpret_cast<double*>(ws + o_WNw);
+  auto* Kw = reinterpret_cast<double*>(ws + o_Kw);
+  auto* coef = reinterpret_cast<double*>(ws + o_coef);
+  auto* cols = reinterpret_cast<int32_t*>(ws + o_cols);
+  auto* mcount = reinterpret_cast<int32_t*>(ws + o_mcount);
+  auto* part = reinterpret_cast<double*>(ws + o_part);
+  auto* hs = static_cast<DecompHost*>(ctx->pinned);
+  std::memset(hs, 0, sizeof(DecompHost));
+  hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, n);
+  SVMD_LAUNCH_CHECK();
+  int64_t outer = 0, inner_total = 0, changed_total = 0;
+  int32_t stop = SVM_STOP_RUNNING;
+  double bh = 0.0, bl = 0.0;
+  for (;;) {
+    hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NB)), dim3(kSelNT), 0, s, f, alpha, y, n, per, T, p.C, p.eps,
+                       cand, cand + NB * T);
+    hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, cand, int(L), int(NB * T), f, p.tau, W, hs);
+    SVMD_LAUNCH_CHECK();
+    SVMD_CHECK(hipStreamSynchronize(s));
+    if (outer > 0) {  // the previous outer iteration's inner solve
+      inner_total += hs->inner_it;
+      changed_total += hs->changed;
+      if (hs->inner_it == 0) {  // no progress on W (a reference stop reason inside W, or no candidate)
+        stop = hs->inner_reason == SVM_STOP_CONVERGED ? SVM_STOP_NO_CANDIDATE : hs->inner_reason;
+        bh = hs->b_high;
+        bl = hs->b_low;
+        break;
+      }
+    }
+    bh = hs->b_high;
+    bl = hs->b_low;
+    if (hs->stop != SVM_STOP_RUNNING) {
+      stop = hs->stop;
+      break;
+    }
+    if (inner_total + 1 > p.max_iter) {  // the reference counts num_iter from 1 (main3.cpp:283-287)
+      stop = SVM_STOP_MAX_ITER;
+      break;
+    }
+    const int m = hs->m;
+    if (m < 2 || m > kMaxWS) {
+      set_error("decomposition SMO: working set of %d points", m);
+      return SVM_ERR_INTERNAL;
+    }
+    hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(m)), dim3(64), 0, s, Q, N0, WN, P.kq, W, m, Qw, N0w, WNw);
+    SVMD_LAUNCH_CHECK();
+    rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), m, P, p.gamma, Kw, ldw, false);
+    if (rc) return rc;
+    const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
+    const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
+#define SVM_WS_INNER(NT, PER)                                                                                    \
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, f, p.C, p.eps, \
+                     tau_in, max_inner, cols, coef, mcount, hs)
+    if (inner_nt == 256)
+      SVM_WS_INNER(256, 4);
+    else if (inner_nt == 512)
+      SVM_WS_INNER(512, 2);
+    else
+      SVM_WS_INNER(1024, 1);
+#undef SVM_WS_INNER
+    SVMD_LAUNCH_CHECK();
+    rc = launch_igram_gemv(s, Q, N0, WN, stw, n, cols, coef, mcount, m, P, p.gamma, part, ldp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
+                       f, n);
+    SVMD_LAUNCH_CHECK();
+    ++outer;
+  }
+  if (stats) {
+    stats[0] = outer;
+    stats[1] = inner_total;
+    stats[2] = qws;
+    stats[3] = int64_t(ms_since(t0) * 1000.0);
+    stats[4] = changed_total;
+    stats[5] = inner_nt;
+  }
+  if (r) {
+    r->iterations = inner_total + 1;
+    r->b_high = bh;
+    r->b_low = bl;
+    r->b = (bh + bl) / 2;
+    r->stop_reason = stop;
+    r->reserved = 0;
+    r->n_sv = -1;
+    r->seconds = ms_since(t0) / 1e3;
+  }
+  return SVM_OK;
+}
+
+}  // namespace svm355
+
+using namespace svm355;
+
+extern "C" {
+
+// Decomposition SMO straight from uint8 pixel rows (exact-integer kernel values, no stored Gram).
+// *used = 0 and nothing done when the rows' statistics do not admit the integer plan.  stats
+// (optional, 6 int64): see run_decomp.
+SVM_API int svmd_train_decomp_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                                 const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params* pp,
+                                 int32_t q, svm_result* r, svmd_timing* timing, int64_t* stats, int32_t* used_out) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!Xu_d || n < 2 || d <= 0 || !mn_h || !mx_h || !y_d || !alpha_d) {
+    set_error("svmd_train_decomp_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ctx->begin();
+  if (rc) return rc;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return ctx->end();  // igram's LDS table bound
+  // quantised rows live in their own grow-only buffer (the solver's workspace is ctx->ws)
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t need = al(size_t(n) * P.kq) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
+                      al(quantize_u8_aux_bytes(P));
+  if (need > ctx->gram_bytes) {
+    if (ctx->gram) {
+      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+      SVMD_CHECK(hipFree(ctx->gram));
+      ctx->gram = nullptr;
+      ctx->gram_bytes = 0;
+    }
+    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
+    ctx->gram_bytes = need;
+  }
+  char* base = reinterpret_cast<char*>(ctx->gram);
+  auto* Q = reinterpret_cast<int8_t*>(base);
+  auto* N0 = reinterpret_cast<int32_t*>(base + al(size_t(n) * P.kq));
+  auto* WN = reinterpret_cast<double*>(reinterpret_cast<char*>(N0) + al(size_t(n) * 4));
+  auto* stw = reinterpret_cast<double*>(reinterpret_cast<char*>(WN) + al(size_t(n) * 8));
+  void* aux = reinterpret_cast<char*>(stw) + al(P.step_w.size() * 8);
+  bool ok = false;
+  {
+    TraceRange tr("svm355:quantise");
+    rc = quantize_u8_rows(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
+    if (rc) return rc;
+  }
+  if (!ok) return ctx->end();
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  const double t_prep = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  {
+    TraceRange ts("svm355:decomp");
+    rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats);
+  }
+  if (!rc && r) {
+    int64_t c = 0;
+    rc = count_sv(ctx, alpha_d, n, 1, p.sv_tol, &c);
+    if (!rc) r->n_sv = c;
+  }
+  if (rc) return rc;
+  if (timing) {
+    timing->gram_ms = t_prep;  // quantisation only: no Gram is stored
+    timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    timing->smo_ms = timing->total_ms - t_prep;
+  }
+  if (used_out) *used_out = 1;
+  return ctx->end();
+}
+
+}  // extern "C"

@@ -289,11 +289,21 @@ __global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict
 // symmetric Gram (every 128 x 128 tile of the tiles x ctiles grid, no mirror; column j of the block
 // at K[i * ldk + j]), e.g. the kernel values of a training set against its leading support vectors
 // (the cascade's warm-start check) or a distributed-SMO team's slab K(:, own) (dsmo.hip).
-template <bool EXTRA, int BK, bool RECT = false>
+//
+// GEMV (RECT only, decomposition solver, decomp.hip): block column j is row colid[j] of the same
+// quantised set, for j < *ncount (a device-side count: workgroups whose 64 columns all lie beyond it
+// exit at once), and instead of storing K the epilogue writes, per row, the sum over this
+// workgroup's 64 columns of coef[j] * K(row, colid[j]) to K[row * ldk + (column-half index)] (a
+// fixed-order butterfly: the caller adds the halves in index order, so the f update is
+// deterministic).
+template <bool EXTRA, int BK, bool RECT = false, bool GEMV = false>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
-    double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols, int64_t col0 = 0) {
+    double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols, int64_t col0 = 0,
+    const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
+    const int32_t* __restrict__ ncount = nullptr) {
+  static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
   constexpr int CPR = BK / 16;            // 16-byte chunks per staged row
@@ -310,7 +320,6 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   double* img = reinterpret_cast<double*>(smem + kTableBytes);  // epilogue: per-wave 32x33 images
 
   const int64_t ctiles = RECT ? (ncols + QBM - 1) / QBM : tiles;
-  const int64_t ncol = RECT ? ncols : n;  // column bound (block-local)
   const int64_t c0 = RECT ? col0 : 0;      // global row index of block column 0
   const int64_t ntile = RECT ? tiles * ctiles : tiles * (tiles + 1) / 2;
   const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
@@ -322,6 +331,11 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     tri_tile(wg >> 1, tiles, tm, tn);
   }
   const int64_t bm = tm * QBM, bn = tn * QBM + (wg & 1) * QBN;
+  // column bound (block-local); GEMV: the device-side count, whole workgroups beyond it exit
+  const int64_t ncol = GEMV ? int64_t(*ncount) : RECT ? ncols : n;
+  if (GEMV && bn >= ncol) return;
+  // global row of block column j: c0 + j, or colid[j] (GEMV)
+  auto crow = [&](int64_t j) -> int64_t { return GEMV ? int64_t(colid[j]) : c0 + j; };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int main_step0 = main0 / 32;
@@ -333,14 +347,20 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     if (EXTRA) wn_r[t] = gi < n ? WN[gi] : 0.0;
   } else if (t < QBM + QBN) {
     const int64_t gj = bn + (t - QBM);
-    n0_c[t - QBM] = gj < ncol ? N0[c0 + gj] : 0;
-    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[c0 + gj] : 0.0;
+    n0_c[t - QBM] = gj < ncol ? N0[crow(gj)] : 0;
+    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[crow(gj)] : 0.0;
   }
 
   // Staging per BK-column stage: thread t copies 16-byte chunk t % CPR of rows t / CPR + RPP * p.
   const int srow = t / CPR, scol = (t % CPR) * 16;
   const i32x4 zero4 = {0, 0, 0, 0};
   i32x4 ga[APASS], gb[BPASS];
+  int64_t brow[BPASS];  // global rows of this thread's staged B rows (-1: beyond the block)
+#pragma unroll
+  for (int p = 0; p < BPASS; ++p) {
+    const int64_t r = bn + srow + RPP * p;
+    brow[p] = r < (RECT ? ncol : n) ? crow(r) : -1;
+  }
   auto gload = [&](int k0) {
 #pragma unroll
     for (int p = 0; p < APASS; ++p) {
@@ -348,10 +368,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       ga[p] = r < n ? *reinterpret_cast<const i32x4*>(Q + r * kq + k0 + scol) : zero4;
     }
 #pragma unroll
-    for (int p = 0; p < BPASS; ++p) {
-      const int64_t r = bn + srow + RPP * p;
-      gb[p] = r < (RECT ? ncol : n) ? *reinterpret_cast<const i32x4*>(Q + (c0 + r) * kq + k0 + scol) : zero4;
-    }
+    for (int p = 0; p < BPASS; ++p)
+      gb[p] = brow[p] >= 0 ? *reinterpret_cast<const i32x4*>(Q + brow[p] * kq + k0 + scol) : zero4;
   };
   gload(0);
 
@@ -412,6 +430,59 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   }
 
   __syncthreads();  // staging tiles fully consumed: the union becomes the transpose images
+  if constexpr (GEMV) {
+    // ---- GEMV epilogue: rowsum[r] = sum over this workgroup's 64 columns of coef * K (the same kernel
+    // values as the stored path), lane-local over its two columns, then a 32-lane butterfly per row.
+    const int64_t row0 = bm + w * 32 + 4 * h;
+    double rs[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rs[r] = 0.0;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+      const int cl = bj * 32 + l32;
+      const int64_t gj = bn + cl;
+      const bool colok = gj < ncol;
+      const double cf = colok ? coef[gj] : 0.0;
+      const int64_t gid = colok ? int64_t(colid[gj]) : -1;
+      const int32_t nbj = n0_c[cl];
+      const double wbj = EXTRA ? wn_c[cl] : 0.0;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        double ex[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = 8 * half + q;
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int32_t D0 = n0_r[w * 32 + rl] + nbj - 2 * acc[bj][r];
+          double dist = w0 * double(D0);
+          if (EXTRA) dist += (wn_r[w * 32 + rl] + wbj) - 2.0 * xacc[bj][r];
+          dist = dist > 0.0 ? dist : 0.0;
+          ex[q] = neg_gamma * dist;
+        }
+        exp_batch<8>(ex);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = 8 * half + q;
+          const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
+          const double kv = gi == gid ? 1.0 : ex[q];
+          rs[r] += cf * kv;  // columns outside the block carry cf = 0
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) rs[r] += __shfl_xor(rs[r], off, 64);
+    if (l32 == 0) {
+      const int64_t part = (bn / QBN);  // this workgroup's 64-column half
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
+        if (gi < n) K[gi * ldk + part] = rs[r];
+      }
+    }
+    return;
+  }
   // ---- epilogue in the 32x32 accumulator layout: col = lane & 31,
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
   double* im = img + w * (32 * 33);
@@ -664,8 +735,8 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
 // The symmetric exact-integer Gram of quantised rows (Q, N0, WN); stw: device scratch for the step
 // weights.
 int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, double* stw, int64_t n,
-                     const QuantPlan& P, double gamma, double* K, int64_t ldk) {
-  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
+                     const QuantPlan& P, double gamma, double* K, int64_t ldk, bool copy_stw) {
+  if (copy_stw) SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
   const int64_t tiles = (n + QBM - 1) / QBM;
   const int64_t nwg = tiles * (tiles + 1);  // two 128x64 halves per upper-triangular 128x128 tile
   if (nwg > 0x7FFFFFFF) {
@@ -821,6 +892,34 @@ int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64
 #undef SVM_IGRAM_BLOCK
   SVMD_LAUNCH_CHECK();
   *used = true;
+  return SVM_OK;
+}
+
+// Decomposition solver f update (decomp.hip): part[i * ldp + c] = sum over the c-th 64-column half of
+// coef[k] * K(i, cols[k]) for every row i < n of (Q, N0, WN), k < *mcount (device; <= m, the grid's
+// bound).  ldp >= 2 * ceil(m / 128); halves at or beyond *mcount are not written: the caller sums
+// the first ceil(*mcount / 64) in index order.
+int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+                      int64_t n, const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m,
+                      const QuantPlan& P, double gamma, double* part, int64_t ldp) {
+  if (n <= 0 || m <= 0) return SVM_OK;
+  const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
+  const int64_t nwg = 2 * tiles * ctiles;
+  if (ldp < 2 * ctiles || nwg > 0x7FFFFFFF) {
+    set_error("igram gemv: bad partial stride or problem too large");
+    return SVM_ERR_ARG;
+  }
+  const int bk = P.kq % 128 == 0 ? 128 : 64;
+#define SVM_IGRAM_GEMV(EX, B)                                                                                       \
+  hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,        \
+                     P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, m, int64_t(0), cols, coef, mcount)
+  if (P.main0 > 0) {
+    if (bk == 128) SVM_IGRAM_GEMV(true, 128); else SVM_IGRAM_GEMV(true, 64);
+  } else {
+    if (bk == 128) SVM_IGRAM_GEMV(false, 128); else SVM_IGRAM_GEMV(false, 64);
+  }
+#undef SVM_IGRAM_GEMV
+  SVMD_LAUNCH_CHECK();
   return SVM_OK;
 }
 

@@ -53,6 +53,14 @@ SVM_API int svmd_train_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, 
                           const double* mx_h, const int32_t* y_d, double* alpha_d, int32_t warm,
                           const svm_params* p, svm_result* r, double* K_d, int64_t ldk, svmd_timing* timing,
                           int32_t* used);
+// Working-set decomposition SMO (decomp.hip, opt-in): working sets of up to q <= 1024 points solved
+// in one workgroup, f updated by the exact-integer kernel values against the working set; no stored
+// Gram.  *used = 0 when the rows are not integer pixels.  stats (optional, 6 int64): outer
+// iterations, inner iterations, working-set size, solve microseconds, f-update columns (points
+// moved, summed over the outer iterations), inner workgroup size.
+SVM_API int svmd_train_decomp_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                                 const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params* p,
+                                 int32_t q, svm_result* r, svmd_timing* timing, int64_t* stats, int32_t* used);
 SVM_API int svmd_minmax_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d);
 SVM_API int svmd_rbf_gram_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
                              const double* mx_h, double gamma, double* K_d, int64_t ldk, int32_t* used);

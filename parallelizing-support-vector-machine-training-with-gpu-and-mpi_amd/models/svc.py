@@ -44,9 +44,11 @@ class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto",
-                 wss: str = "first"):
+                 wss: str = "first", solver: str = "smo", working_set: int = 1024):
         if wss not in ("first", "second"):
             raise ValueError("wss must be 'first' (the reference's selection) or 'second'")
+        if solver not in ("smo", "decomp"):
+            raise ValueError("solver must be 'smo' (the reference's pairwise SMO over all n points) or 'decomp'")
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else default_threads(),
                                 wss=2 if wss == "second" else 1)
@@ -57,6 +59,12 @@ class SVC:
         self.gram = gram  # "auto" | "fp64" | "int" (device backend Gram path, see ops.device.train)
         self.kcache = kcache  # "auto" | "full" (resident Gram) | "rows" (on-demand HBM row cache)
         self._dev = None  # device-side model state (torch tensors)
+        # "smo": the reference's solver (one pair per iteration over all n points, resident Gram or row
+        # cache).  "decomp": working sets of up to `working_set` points solved in one workgroup with
+        # the same stop test on all n points (decomp.hip; GPU, uint8 pixel rows, cold start) -- the
+        # same support vectors, b within the stop tolerance, a different pair sequence.
+        self.solver = solver
+        self.working_set = int(working_set)
 
     # ------------------------------------------------------------------ fit
     def fit(self, X: np.ndarray, y: np.ndarray, alpha0: Optional[np.ndarray] = None) -> "SVC":
@@ -90,6 +98,8 @@ class SVC:
     def _fit_cpu(self, X, y, alpha0):
         from ..ops import cpu as C
 
+        if self.solver == "decomp":
+            raise ValueError("solver='decomp' runs on the GPU (device='cuda')")
         if self.scale:
             self.scaler_ = MinMaxScaler().fit(X)
             Xs = self.scaler_.transform(X)
@@ -107,6 +117,12 @@ class SVC:
         from ..ops import device as D
 
         device = torch.device(dev)
+        if self.solver == "decomp":
+            if X.dtype != np.uint8 or not self.scale or alpha0 is not None:
+                raise ValueError("solver='decomp' needs uint8 pixel rows, scale=True and a cold start")
+            if not self._fit_cuda_u8(X, y, None, device):
+                raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
+            return
         if (X.dtype == np.uint8 and self.scale and self.gram in ("auto", "int") and self.kcache in ("auto", "full")
                 and os.environ.get("SVM355_U8_TRAIN", "1") != "0" and self._fit_cuda_u8(X, y, alpha0, device)):
             return
@@ -122,7 +138,7 @@ class SVC:
         if alpha0 is not None:
             alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
         else:
-            alpha = torch.zeros(X.shape[0], dtype=torch.float64, device=device)
+            alpha = torch.empty(X.shape[0], dtype=torch.float64, device=device)  # the cold start zeroes it
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
         res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
@@ -156,21 +172,29 @@ class SVC:
         from ..ops import device as D
 
         n, d = X.shape
-        if self.kcache == "auto" and not D.gram_fits(n, device):
+        decomp = self.solver == "decomp"
+        if not decomp and self.kcache == "auto" and not D.gram_fits(n, device):
             return False
+        # No PyTorch kernel runs on this path (copies and the library's own kernels only): a process's
+        # first PyTorch kernel loads PyTorch's code objects, ~95 ms of a cold first fit
+        # (profiles/r3_cold_fit_probe.txt).
         t0 = time.perf_counter()
         Xu = D.upload_u8(X, device)
         yd = torch.from_numpy(y).to(device)
-        mn, mx = D.minmax_u8(Xu)
+        mmd = torch.empty(2 * d, dtype=torch.float64, device=device)
+        mn, mx = D.minmax_u8(Xu, out=mmd)
         if alpha0 is not None:
             alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
         else:
-            alpha = torch.zeros(n, dtype=torch.float64, device=device)
-        mm = torch.cat([mn, mx]).cpu().numpy()  # one D2H (synchronises) for the plan and the scaler
+            alpha = torch.empty(n, dtype=torch.float64, device=device)  # the cold start zeroes it
+        mm = mmd.cpu().numpy()  # one D2H (synchronises) for the plan and the scaler
         mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
         t1 = time.perf_counter()
-        out = D.train_u8(Xu, yd, alpha, self.params, mn_h, mx_h, warm=alpha0 is not None)
-        if out is None:
+        if decomp:
+            out = D.train_decomp_u8(Xu, yd, alpha, self.params, mn_h, mx_h, working_set=self.working_set)
+        else:
+            out = D.train_u8(Xu, yd, alpha, self.params, mn_h, mx_h, warm=alpha0 is not None)
+        if out is None:  # nothing ran (not an integer plan): the FP64-row path takes over
             return False
         res, tm = out
         self._finish(alpha.cpu().numpy(), y, res)

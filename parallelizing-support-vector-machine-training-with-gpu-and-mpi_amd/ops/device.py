@@ -365,11 +365,13 @@ def upload_u8(X: np.ndarray, device) -> torch.Tensor:
     return out
 
 
-def minmax_u8(Xu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Column min / max (FP64) of device uint8 rows: equal to those of the widened FP64 rows."""
+def minmax_u8(Xu: torch.Tensor, out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Column min / max (FP64) of device uint8 rows: equal to those of the widened FP64 rows.  With
+    ``out`` (2d float64) they are its two halves, so one read-back fetches both."""
     n, d = Xu.shape
-    mn = torch.empty(d, dtype=torch.float64, device=Xu.device)
-    mx = torch.empty(d, dtype=torch.float64, device=Xu.device)
+    if out is None:
+        out = torch.empty(2 * d, dtype=torch.float64, device=Xu.device)
+    mn, mx = out[:d], out[d:]
     ctx = _ctx_for(Xu)
     N.check(ctx.lib.svmd_minmax_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(mn), N.ptr(mx)), "svmd_minmax_u8")
     return mn, mx
@@ -398,6 +400,30 @@ def train_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVM
     return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
                                       "gram_alloc_ms": alloc_ms, "kcache": "full", "gram_path": "int8-exact",
                                       "rows": "uint8"}
+
+
+def train_decomp_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn: torch.Tensor,
+                    mx: torch.Tensor, working_set: int = 1024) -> Optional[Tuple[SMOResult, dict]]:
+    """Working-set decomposition SMO straight from the bytes (svmd_train_decomp_u8, decomp.hip): the
+    reference's stop test on all n points, reached by first-order SMO on working sets of up to
+    ``working_set`` points; no n x n Gram.  Cold start only.  None when the integer plan does not
+    apply."""
+    n, d = Xu.shape
+    ctx = _ctx_for(Xu)
+    a, b, _ = _host_stats(mn, mx)
+    r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
+    st = (ctypes.c_int64 * 6)()
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_train_decomp_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(a), N.ptr(b), N.ptr(y), N.ptr(alpha),
+                                         ctypes.byref(p), int(working_set), ctypes.byref(r), ctypes.byref(tm), st,
+                                         ctypes.byref(used)), "svmd_train_decomp_u8")
+    if not used.value:
+        return None
+    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
+                                      "kcache": "none", "gram_path": "int8-exact", "rows": "uint8",
+                                      "solver": "decomp", "outer_iterations": int(st[0]),
+                                      "inner_iterations": int(st[1]), "working_set": int(st[2]),
+                                      "update_columns": int(st[4]), "inner_threads": int(st[5])}
 
 
 def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:

@@ -1,0 +1,26 @@
+"""SVC's solver option on the CPU: the decomposition solver (decomp.hip) is GPU-only and says so; an
+unknown solver is refused at construction."""
+import numpy as np
+import pytest
+
+from svm355 import SVC
+from svm355.utils.data import synthetic_mnist
+
+
+def test_unknown_solver_is_refused():
+    with pytest.raises(ValueError, match="solver"):
+        SVC(solver="newton")
+
+
+def test_decomp_on_the_cpu_is_refused():
+    tr = synthetic_mnist(200, seed=1)
+    with pytest.raises(ValueError, match="GPU"):
+        SVC(device="cpu", solver="decomp").fit(tr.X, tr.y)
+
+
+def test_default_solver_is_the_reference_smo():
+    m = SVC(device="cpu")
+    assert m.solver == "smo" and m.working_set == 1024
+    tr = synthetic_mnist(300, seed=2)
+    m.fit(tr.X, tr.y)
+    assert m.stop_reason_ == "converged" and np.all(m.alpha_ >= 0)
