@@ -74,6 +74,12 @@ def main(argv=None):
                     help="N > 1: single-GPU fits timed after the run for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference; the headline) or the opt-in second-order")
+    ap.add_argument("--solver", choices=["smo", "decomp"], default="smo",
+                    help="N = 1: the reference's pairwise first-order SMO (the headline) or the opt-in working-set "
+                         "decomposition (SVC(solver='decomp'): same stop test on all n points, same SVs)")
+    ap.add_argument("--decomp-fits", type=int, default=3,
+                    help="N = 1, --solver smo: decomposition-solver fits timed after the run and reported next to the "
+                         "headline (0 = skip)")
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N > 1: seconds any rank waits on an exchange before every rank aborts its communicator "
                          "(a fit takes well under a second; a dead peer must not hang the run)")
@@ -98,6 +104,9 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
+    if a.solver == "decomp" and (a.gpus > 1 or a.cascade or a.parallel == "smo" or cpu or a.input != "u8"):
+        print("bench.py: --solver decomp is the one-GPU trainer on uint8 pixel rows", file=sys.stderr)
+        return 2
     ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
     if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
         print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, {ndev} visible "
@@ -117,6 +126,18 @@ def main(argv=None):
     dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
     sync = (lambda: torch.cuda.synchronize(dev)) if not cpu else (lambda: None)
     distributed = a.gpus > 1 or a.cascade or a.parallel == "smo"
+    # A fresh process's first GPU operation (any: a copy, a PyTorch kernel, a context) pays a one-off
+    # runtime/device initialisation (~85-115 ms, profiles/r3_first_op_probe.txt), whatever follows.
+    # It is paid and timed here, outside the fits, so cold_fit_ms is the first fit's own cost.
+    device_init_ms = None
+    if not cpu:
+        ti = time.perf_counter()
+        torch.zeros(1, dtype=torch.uint8).to(dev)
+        from svm355.ops import device as _D
+
+        _D.DeviceContext.get(dev)
+        sync()
+        device_init_ms = round((time.perf_counter() - ti) * 1e3, 3)
     dist = None
     if multiproc:
         import torch.distributed as dist
@@ -218,7 +239,7 @@ def main(argv=None):
     def step():
         nonlocal model
         if mode == "single":
-            model = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
+            model = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(full.X, full.y)
         elif mode == "smo":
             model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
         elif multiproc:
@@ -323,13 +344,32 @@ def main(argv=None):
                 f64_ms.append((time.perf_counter() - tf) * 1e3)
             extra["f64_input_fit_ms"] = round(float(np.median(f64_ms)), 3)
             extra["f64_input_same_model"] = bool(m64.b_ == model.b_ and m64.n_iter_ == model.n_iter_)
+        if a.decomp_fits > 0 and a.solver == "smo" and not cpu and a.input == "u8":
+            # the opt-in decomposition solver on the same rows (outside the timed region): same stop test
+            # on all n points by a different pair sequence; same SV set expected, b within a few tau
+            dm = SVC(device=str(dev), solver="decomp").fit(full.X, full.y)
+            d_ms = []
+            for _ in range(a.decomp_fits):
+                sync()
+                tf = time.perf_counter()
+                dm = SVC(device=str(dev), solver="decomp").fit(full.X, full.y)
+                sync()
+                d_ms.append((time.perf_counter() - tf) * 1e3)
+            extra["decomp_solver"] = {
+                "fit_ms": round(float(np.median(d_ms)), 3), "fit_ms_all": [round(x, 3) for x in d_ms],
+                "same_svs": bool(np.array_equal(dm.support_, model.support_)), "b": float(dm.b_),
+                "b_minus_headline_b": float(dm.b_ - model.b_), "iterations": int(dm.n_iter_),
+                "outer_iterations": dm.timings_["outer_iterations"], "working_set": dm.timings_["working_set"],
+                "accuracy": dm.score(te.X, te.y), "stop_reason": dm.stop_reason_}
         extra.update({
             "n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
             "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
             "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S,
             "cold_fit_ms": warm_ms[0] if warm_ms else None, "warmup_fit_ms": warm_ms,
+            "device_init_ms": device_init_ms, "solver": a.solver,
             "caveats": "timed fits reuse the library's grow-only Gram buffer and device context, allocated by the "
-                       "first (cold) fit, whose time is cold_fit_ms; host rows are uint8 pixels: min/max, the "
+                       "first (cold) fit, whose time is cold_fit_ms (measured after the process's one-off device "
+                       "initialisation, device_init_ms, which its first GPU operation of any kind pays); host rows are uint8 pixels: min/max, the "
                        "exact-integer quantisation and the Gram read the bytes on the device and only the support "
                        "vectors are widened to scaled fp64 (f64_input_fit_ms: the same fit from the reference's fp64 "
                        "host rows); the data are a synthetic MNIST-shaped draw, not MNIST"})
@@ -426,7 +466,8 @@ def main(argv=None):
             "dtype": "fp64",
             "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
             "config": {
-                "model": f"RBF SVM, {a.wss}-order SMO (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
+                "model": (f"RBF SVM, {a.wss}-order SMO" if a.solver == "smo" else "RBF SVM, working-set decomposition SMO")
+                         + " (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,
                 "parallelism": parallelism,

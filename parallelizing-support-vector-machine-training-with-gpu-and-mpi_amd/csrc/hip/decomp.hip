@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -41,6 +42,7 @@ struct DecompHost {  // pinned: written by the kernels, read by the host once pe
   int32_t m, stop;
   int64_t inner_it;
   int32_t inner_reason, changed;  // changed: points whose alpha the inner solve moved
+  int64_t prof[8];  // PROF builds: clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall ticks
 };
 
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
@@ -196,18 +198,58 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
   }
 }
 
+// Both of an iteration's wave arg-reductions in lockstep (minimum over I_high, maximum over I_low):
+// the two high-word butterflies are independent DPP chains and interleave; each side falls back to
+// wave_arg (low words, then the lowest index) only when its high word ties.  Same results as two
+// wave_arg calls.
+__device__ __forceinline__ void wave_arg_pair(VI mn, VI mx, VIL& rmn, VIL& rmx) {
+  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
+  uint32_t a = k1, b = k2;
+  a = min(a, dpp32<0xB1>(a));
+  b = max(b, dpp32<0xB1>(b));
+  a = min(a, dpp32<0x4E>(a));
+  b = max(b, dpp32<0x4E>(b));
+  a = min(a, dpp32<0x141>(a));
+  b = max(b, dpp32<0x141>(b));
+  a = min(a, dpp32<0x140>(a));
+  b = max(b, dpp32<0x140>(b));
+  a = swap_pick32<true, false>(a);
+  b = swap_pick32<false, false>(b);
+  a = swap_pick32<true, true>(a);
+  b = swap_pick32<false, true>(b);
+  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
+  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
+  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
+  if (__popcll(t1) == 1) {
+    const int src = __builtin_ctzll(t1);
+    rmn = VIL{read_lane64(mn.v, src), uint32_t(__builtin_amdgcn_readlane(int(mn.i), src)), src};
+  } else {
+    rmn = wave_arg<true>(mn);
+  }
+  if (__popcll(t2) == 1) {
+    const int src = __builtin_ctzll(t2);
+    rmx = VIL{read_lane64(mx.v, src), uint32_t(__builtin_amdgcn_readlane(int(mx.i), src)), src};
+  } else {
+    rmx = wave_arg<false>(mx);
+  }
+}
+
 // First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER points
-// W[t + NT e] (f, alpha, y in registers); per iteration each wave's arg-reduction carries the
-// winners' alpha and y, ONE barrier publishes the per-wave candidates (double-buffered by iteration
-// parity), and every wave merges them itself with the lowest-index rule -- so all waves hold the
-// identical (i_high, i_low, b_high, b_low, alpha, y) without a second barrier.  Every thread then
-// evaluates the reference's clip / eta / update arithmetic on the same inputs (persist_solve's
-// sequence, main3.cpp:235-275) and applies f += ch K(i, .) + cl K(j, .) from the L2-resident
-// K(W, W); the two row reads and K12 are the iteration's only memory round trip.  Stops at W's own
-// gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points whose alpha changed
-// are compacted in position order: cols[j] = their global ids, coef[j] = (alpha_new - alpha_old) y,
-// *mcount = how many -- the f update of all n points reads only those columns.
-template <int NT, int PER>
+// W[t + NT e] (f, alpha, y in registers).  Per iteration:
+//   select   branch-free thread-local (value, lowest position) minimum over I_high and maximum over
+//            I_low, carrying the winner's alpha, then the wave64 arg-reductions (wave_arg);
+//   publish  lane 0 of every wave writes its two candidates to LDS (double-buffered by iteration
+//            parity) -- the iteration's ONE barrier;
+//   merge    every lane folds the NW per-wave candidates itself (LDS broadcast reads, the same serial
+//            order and tie rule everywhere), so all waves hold the identical (i_high, i_low, b_high,
+//            b_low, alpha_h, alpha_l) with no second barrier; the pair's labels come from LDS;
+//   rows     K12 and this thread's entries of the two rows of the L2-resident K(W, W);
+//   update   the reference's clip / eta / update arithmetic on the same inputs in every thread
+//            (persist_solve's sequence, main3.cpp:235-275) and f += ch K(i, .) + cl K(j, .).
+// Stops at W's own gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points
+// whose alpha changed are compacted in position order: cols[j] = their global ids, coef[j] =
+// (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
+template <int NT, int PER, bool PROF = false, bool W2 = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, int m,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
@@ -216,13 +258,15 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
                                                       double* __restrict__ coef, int32_t* __restrict__ mcount,
                                                       DecompHost* __restrict__ hs) {
   constexpr int NW = NT / 64;
-  __shared__ int32_t wcnt[PER][NW];
   __shared__ double pv[2][2][NW], pa[2][2][NW];
   __shared__ uint32_t pi[2][2][NW];
-  __shared__ int32_t py[2][2][NW];
+  __shared__ double qv[2][NW], qa[2][NW], qf[2][NW], qk[2][NW];  // W2: the second index's candidates
+  __shared__ uint32_t qi[2][NW];
+  __shared__ int8_t sy[NT * PER];
+  __shared__ int32_t wcnt[PER][NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   double a[PER], a0[PER], ft[PER];
-  int32_t yt[PER];  // y = 0 (padding) is in neither set
+  bool yp[PER], yn[PER];  // y = +1 / y = -1 (padding: neither, so in neither set)
   int64_t gid[PER];
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
@@ -231,80 +275,163 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     gid[e] = valid ? W[k] : 0;
     a[e] = valid ? alpha[gid[e]] : 0.0;
     a0[e] = a[e];
-    yt[e] = valid ? y[gid[e]] : 0;
+    const int32_t yk = valid ? y[gid[e]] : 0;
+    yp[e] = yk == 1;
+    yn[e] = yk == -1;
+    sy[k] = int8_t(yk);
     ft[e] = valid ? f[gid[e]] : 0.0;
   }
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
   int64_t it = 0;
   int32_t reason = SVM_STOP_CONVERGED;
+  // PROF: wave 0's clock at the phase boundaries (select | publish+barrier | merge | row loads | update)
+  int64_t pacc[6] = {0, 0, 0, 0, 0, 0};
+  int64_t pt = PROF ? int64_t(clock64()) : 0;
+  const int64_t pc0 = pt, pw0 = PROF ? int64_t(wall_clock64()) : 0;
+  auto stamp = [&](int k) {
+    if constexpr (PROF) {
+      const int64_t now = int64_t(clock64());
+      pacc[k] += now - pt;
+      pt = now;
+    }
+  };
   for (int par = 0;; par ^= 1) {
-    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
-    double mna = 0.0, mxa = 0.0;
-    int32_t mny = 0, mxy = 0;
+    double hv = inf, lv = -inf, ha = 0.0, la = 0.0;
+    uint32_t hi = kSentinel, li = kSentinel;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {  // ascending position within a thread: strict compares keep the lowest
-      const bool in_high = (yt[e] == 1 && a[e] < c_hi) || (yt[e] == -1 && a[e] > c_lo);
-      const bool in_low = (yt[e] == 1 && a[e] > c_lo) || (yt[e] == -1 && a[e] < c_hi);
-      if (in_high && ft[e] < mn.v) {
-        mn = VI{ft[e], uint32_t(t + NT * e)};
-        mna = a[e];
-        mny = yt[e];
-      }
-      if (in_low && ft[e] > mx.v) {
-        mx = VI{ft[e], uint32_t(t + NT * e)};
-        mxa = a[e];
-        mxy = yt[e];
-      }
+      const bool below = a[e] < c_hi, above = a[e] > c_lo;
+      const bool in_high = (yp[e] && below) || (yn[e] && above);
+      const bool in_low = (yp[e] && above) || (yn[e] && below);
+      const bool ch = in_high && ft[e] < hv, cl = in_low && ft[e] > lv;
+      const uint32_t k = uint32_t(t + NT * e);
+      hv = ch ? ft[e] : hv;
+      ha = ch ? a[e] : ha;
+      hi = ch ? k : hi;
+      lv = cl ? ft[e] : lv;
+      la = cl ? a[e] : la;
+      li = cl ? k : li;
     }
-    const VIL wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
-    const double awmn = read_lane64(mna, wmn.lane), awmx = read_lane64(mxa, wmx.lane);
-    const int32_t ywmn = __builtin_amdgcn_readlane(mny, wmn.lane), ywmx = __builtin_amdgcn_readlane(mxy, wmx.lane);
+    VIL wmn, wmx;
+    wave_arg_pair(VI{hv, hi}, VI{lv, li}, wmn, wmx);
+    const double awmn = read_lane64(ha, wmn.lane), awmx = read_lane64(la, wmx.lane);
+    stamp(0);
     if (lane == 0) {
       pv[par][0][w] = wmn.v;
       pi[par][0][w] = wmn.i;
       pa[par][0][w] = awmn;
-      py[par][0][w] = ywmn;
       pv[par][1][w] = wmx.v;
       pi[par][1][w] = wmx.i;
       pa[par][1][w] = awmx;
-      py[par][1][w] = ywmx;
     }
     __syncthreads();
-    VI ca{inf, kSentinel}, cb{-inf, kSentinel};
-    double caa = 0.0, cba = 0.0;
-    int32_t cay = 0, cby = 0;
-    if (lane < NW) {
-      ca = VI{pv[par][0][lane], pi[par][0][lane]};
-      cb = VI{pv[par][1][lane], pi[par][1][lane]};
-      caa = pa[par][0][lane];
-      cba = pa[par][1][lane];
-      cay = py[par][0][lane];
-      cby = py[par][1][lane];
+    stamp(1);
+    double bh = pv[par][0][0], bl = pv[par][1][0], ah = pa[par][0][0], al = pa[par][1][0];
+    uint32_t uih = pi[par][0][0], uil = pi[par][1][0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {  // the same fold in every lane: value, then lowest position
+      const double vh = pv[par][0][q], vl = pv[par][1][q];
+      const uint32_t ih_q = pi[par][0][q], il_q = pi[par][1][q];
+      const bool th = vh < bh || (vh == bh && ih_q < uih);
+      const bool tl = vl > bl || (vl == bl && il_q < uil);
+      bh = th ? vh : bh;
+      ah = th ? pa[par][0][q] : ah;
+      uih = th ? ih_q : uih;
+      bl = tl ? vl : bl;
+      al = tl ? pa[par][1][q] : al;
+      uil = tl ? il_q : uil;
     }
-    const VIL ra = wave_arg<true, NW>(ca), rb = wave_arg<false, NW>(cb);
-    const uint32_t uih = ra.i, uil = rb.i;
+    stamp(2);
     if (uih == kSentinel || uil == kSentinel) {
       reason = SVM_STOP_NO_CANDIDATE;
       break;
     }
-    const double bh = ra.v, bl = rb.v;
     if (bl <= bh + 2.0 * tau_in) break;  // W's own optimum (reason stays CONVERGED)
     if (it >= max_inner) {
       reason = SVM_STOP_MAX_ITER;
       break;
     }
-    const int ih = int(uih), il = int(uil);
-    // one memory round trip: K12 and this thread's entries of the two rows
-    const double K12 = Kw[int64_t(ih) * ldw + il];
+    int ih = int(uih), il = int(uil);
+    double K12, bl_upd = bl;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
+    if constexpr (!W2) {
+      // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
+      K12 = Kw[int64_t(ih) * ldw + il];
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int k = t + NT * e;
-      kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
-      kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+      for (int e = 0; e < PER; ++e) {
+        const int k = t + NT * e;
+        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+      }
+    } else {
+      // second-order choice of the second index (smo_cpu.cpp / persist_solve WSS2): row i_high, then
+      // the maximum of (f_t - b_high)^2 / a_t over I_low points above b_high (a_t = 2 - 2 K(i, t),
+      // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
+      // and fold, then row j
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int k = t + NT * e;
+        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+      }
+      double gv = inf, ga = 0.0, gf = 0.0, gk = 0.0;
+      uint32_t gi = kSentinel;
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const bool below = a[e] < c_hi, above = a[e] > c_lo;
+        const bool in_low = (yp[e] && above) || (yn[e] && below);
+        const double bb = ft[e] - bh;
+        double at = 2.0 - 2.0 * kh[e];
+        at = at <= 0.0 ? eps : at;
+        const double gain = -(bb * bb) * __builtin_amdgcn_rcp(at);
+        const bool c = in_low && ft[e] > bh && gain < gv;
+        gv = c ? gain : gv;
+        ga = c ? a[e] : ga;
+        gf = c ? ft[e] : gf;
+        gk = c ? kh[e] : gk;
+        gi = c ? uint32_t(t + NT * e) : gi;
+      }
+      const VIL wc = wave_arg<true>(VI{gv, gi});
+      const double wa = read_lane64(ga, wc.lane), wf = read_lane64(gf, wc.lane), wk = read_lane64(gk, wc.lane);
+      if (lane == 0) {
+        qv[par][w] = wc.v;
+        qi[par][w] = wc.i;
+        qa[par][w] = wa;
+        qf[par][w] = wf;
+        qk[par][w] = wk;
+      }
+      __syncthreads();
+      double cv = qv[par][0];
+      uint32_t ci = qi[par][0];
+      al = qa[par][0];
+      bl_upd = qf[par][0];
+      K12 = qk[par][0];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) {
+        const double v = qv[par][q];
+        const uint32_t i2 = qi[par][q];
+        const bool tk = v < cv || (v == cv && i2 < ci);
+        cv = tk ? v : cv;
+        ci = tk ? i2 : ci;
+        al = tk ? qa[par][q] : al;
+        bl_upd = tk ? qf[par][q] : bl_upd;
+        K12 = tk ? qk[par][q] : K12;
+      }
+      if (ci == kSentinel) {  // no I_low point above b_high (cannot happen while the gap is open)
+        reason = SVM_STOP_NO_CANDIDATE;
+        break;
+      }
+      il = int(ci);
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int k = t + NT * e;
+        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+      }
     }
-    const double ah = read_lane64(caa, ra.lane), al = read_lane64(cba, rb.lane);
-    const int32_t yh = __builtin_amdgcn_readlane(cay, ra.lane), yl = __builtin_amdgcn_readlane(cby, rb.lane);
+    const int32_t yh = sy[ih], yl = sy[il];
+    if constexpr (PROF) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      stamp(3);
+    }
     const double K11 = 1.0, K22 = 1.0;  // the Gram's unit diagonal
     const int s = yh * yl;
     const double eta = K11 + K22 - 2.0 * K12;
@@ -324,7 +451,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       reason = SVM_STOP_NONPOS_ETA;
       break;
     }
-    double al_new = al + double(yl) * (bh - bl) / eta;
+    double al_new = al + double(yl) * (bh - bl_upd) / eta;
     if (al_new > V) al_new = V;
     if (al_new < U) al_new = U;
     const double ah_new = ah + double(s) * (al - al_new);
@@ -334,10 +461,10 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     for (int e = 0; e < PER; ++e) {
       const int k = t + NT * e;
       ft[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
-      if (k == ih) a[e] = ah_new;
-      if (k == il) a[e] = al_new;
+      a[e] = k == ih ? ah_new : k == il ? al_new : a[e];
     }
     ++it;
+    stamp(4);
   }
   unsigned long long bal[PER];
 #pragma unroll
@@ -360,8 +487,13 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     if ((bal[e] >> lane) & 1ull) {
       const int j = off + __popcll(bal[e] & ((1ull << lane) - 1ull));
       cols[j] = int32_t(gid[e]);
-      coef[j] = (a[e] - a0[e]) * double(yt[e]);
+      coef[j] = (a[e] - a0[e]) * (yp[e] ? 1.0 : -1.0);
     }
+  }
+  if (PROF && t == 0) {
+    for (int k = 0; k < 5; ++k) hs->prof[k] += pacc[k];
+    hs->prof[6] += int64_t(clock64()) - pc0;
+    hs->prof[7] += int64_t(wall_clock64()) - pw0;
   }
   if (t == 0) {
     *mcount = base;
@@ -427,11 +559,15 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     return SVM_ERR_INTERNAL;
   }
   // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 256 | 512 | 1024
-  int inner_nt = 512;
+  int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
   // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
   double tau_frac = 0.1;
   if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
+  // SVM355_DECOMP_PROF=1: clock64 phase totals of the inner solves on stderr (diagnostic build)
+  const bool prof = getenv("SVM355_DECOMP_PROF") && atoi(getenv("SVM355_DECOMP_PROF")) == 1;
+  // inner pair selection: first order (default) or second order for j (SVM355_DECOMP_WSS=2)
+  const bool inner_wss2 = getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 2;
   const int64_t ldw = kMaxWS;            // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -505,9 +641,18 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     if (rc) return rc;
     const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
     const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
-#define SVM_WS_INNER(NT, PER)                                                                                    \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, f, p.C, p.eps, \
-                     tau_in, max_inner, cols, coef, mcount, hs)
+#define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, f, p.C,  \
+                     p.eps, tau_in, max_inner, cols, coef, mcount, hs)
+#define SVM_WS_INNER(NT, PER)                \
+  if (prof && inner_wss2)                    \
+    SVM_WS_INNER_(NT, PER, true, true);      \
+  else if (prof)                             \
+    SVM_WS_INNER_(NT, PER, true, false);     \
+  else if (inner_wss2)                       \
+    SVM_WS_INNER_(NT, PER, false, true);     \
+  else                                       \
+    SVM_WS_INNER_(NT, PER, false, false)
     if (inner_nt == 256)
       SVM_WS_INNER(256, 4);
     else if (inner_nt == 512)
@@ -515,6 +660,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     else
       SVM_WS_INNER(1024, 1);
 #undef SVM_WS_INNER
+#undef SVM_WS_INNER_
     SVMD_LAUNCH_CHECK();
     rc = launch_igram_gemv(s, Q, N0, WN, stw, n, cols, coef, mcount, m, P, p.gamma, part, ldp);
     if (rc) return rc;
@@ -522,6 +668,13 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
                        f, n);
     SVMD_LAUNCH_CHECK();
     ++outer;
+  }
+  if (prof && inner_total > 0) {
+    const double it = double(inner_total);
+    fprintf(stderr, "decomp prof (clock64 ticks / inner iteration): select %.0f  publish+barrier %.0f  merge %.0f  "
+            "row loads %.0f  update %.0f  (%lld iterations; inner kernels %.3f ms wall = %lld clock64 ticks)\n",
+            hs->prof[0] / it, hs->prof[1] / it, hs->prof[2] / it, hs->prof[3] / it, hs->prof[4] / it,
+            (long long)inner_total, hs->prof[7] / 1e5, (long long)hs->prof[6]);
   }
   if (stats) {
     stats[0] = outer;
