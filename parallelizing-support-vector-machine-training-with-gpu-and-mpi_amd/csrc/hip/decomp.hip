@@ -326,21 +326,32 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     }
     __syncthreads();
     stamp(1);
-    double bh = pv[par][0][0], bl = pv[par][1][0], ah = pa[par][0][0], al = pa[par][1][0];
-    uint32_t uih = pi[par][0][0], uil = pi[par][1][0];
+    // the same pairwise tree fold in every lane (value, then lowest position): log2(NW) dependent steps
+    double fv[2][NW], fa[2][NW];
+    uint32_t fi[2][NW];
 #pragma unroll
-    for (int q = 1; q < NW; ++q) {  // the same fold in every lane: value, then lowest position
-      const double vh = pv[par][0][q], vl = pv[par][1][q];
-      const uint32_t ih_q = pi[par][0][q], il_q = pi[par][1][q];
-      const bool th = vh < bh || (vh == bh && ih_q < uih);
-      const bool tl = vl > bl || (vl == bl && il_q < uil);
-      bh = th ? vh : bh;
-      ah = th ? pa[par][0][q] : ah;
-      uih = th ? ih_q : uih;
-      bl = tl ? vl : bl;
-      al = tl ? pa[par][1][q] : al;
-      uil = tl ? il_q : uil;
-    }
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        fv[sd][q] = pv[par][sd][q];
+        fa[sd][q] = pa[par][sd][q];
+        fi[sd][q] = pi[par][sd][q];
+      }
+#pragma unroll
+    for (int st = 1; st < NW; st <<= 1)
+#pragma unroll
+      for (int q = 0; q + st < NW; q += 2 * st) {
+        const bool th = fv[0][q + st] < fv[0][q] || (fv[0][q + st] == fv[0][q] && fi[0][q + st] < fi[0][q]);
+        const bool tl = fv[1][q + st] > fv[1][q] || (fv[1][q + st] == fv[1][q] && fi[1][q + st] < fi[1][q]);
+        fv[0][q] = th ? fv[0][q + st] : fv[0][q];
+        fa[0][q] = th ? fa[0][q + st] : fa[0][q];
+        fi[0][q] = th ? fi[0][q + st] : fi[0][q];
+        fv[1][q] = tl ? fv[1][q + st] : fv[1][q];
+        fa[1][q] = tl ? fa[1][q + st] : fa[1][q];
+        fi[1][q] = tl ? fi[1][q + st] : fi[1][q];
+      }
+    double bh = fv[0][0], bl = fv[1][0], ah = fa[0][0], al = fa[1][0];
+    uint32_t uih = fi[0][0], uil = fi[1][0];
     stamp(2);
     if (uih == kSentinel || uil == kSentinel) {
       reason = SVM_STOP_NO_CANDIDATE;
@@ -558,7 +569,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     set_error("decomposition SMO: selection blocks too large");
     return SVM_ERR_INTERNAL;
   }
-  // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 256 | 512 | 1024
+  // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512 | 1024
   int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
   // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
@@ -566,8 +577,9 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
   // SVM355_DECOMP_PROF=1: clock64 phase totals of the inner solves on stderr (diagnostic build)
   const bool prof = getenv("SVM355_DECOMP_PROF") && atoi(getenv("SVM355_DECOMP_PROF")) == 1;
-  // inner pair selection: first order (default) or second order for j (SVM355_DECOMP_WSS=2)
-  const bool inner_wss2 = getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 2;
+  // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
+  // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
+  const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
   const int64_t ldw = kMaxWS;            // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -653,7 +665,11 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     SVM_WS_INNER_(NT, PER, false, true);     \
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
-    if (inner_nt == 256)
+    if (inner_nt == 64)
+      SVM_WS_INNER(64, 16);
+    else if (inner_nt == 128)
+      SVM_WS_INNER(128, 8);
+    else if (inner_nt == 256)
       SVM_WS_INNER(256, 4);
     else if (inner_nt == 512)
       SVM_WS_INNER(512, 2);
