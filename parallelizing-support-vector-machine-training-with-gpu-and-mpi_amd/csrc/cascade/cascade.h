@@ -221,6 +221,12 @@ class Transport {
   virtual void bcast(void* buf, int64_t bytes, int root) = 0;
   // Every rank sends `bytes` from send; root receives world * bytes into recv (rank order).
   virtual void gather(const void* send, int64_t bytes, void* recv, int root) = 0;
+  // All-gather of `bytes` from every rank into recv (world * bytes, rank-major), e.g. the distributed
+  // decomposition SMO's candidate records.  Default: a gather to rank 0, then a broadcast of it.
+  virtual void allgather(const void* send, int64_t bytes, void* recv) {
+    gather(send, bytes, recv, 0);
+    bcast(recv, bytes * world(), 0);
+  }
   virtual void send_i64(int64_t v, int peer) = 0;
   virtual int64_t recv_i64(int peer) = 0;
   virtual void send(const void* buf, int64_t bytes, int peer) = 0;

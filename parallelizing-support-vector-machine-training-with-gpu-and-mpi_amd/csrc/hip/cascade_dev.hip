@@ -27,6 +27,7 @@
 #include "cascade.h"
 #include "cascade_capi.h"
 #include "ctx.h"
+#include "decomp.h"
 #include "svm355_device.h"
 
 namespace svm355 {
@@ -208,6 +209,7 @@ class HipBackend final : public Backend {
   HipBackend& operator=(const HipBackend&) = delete;
 
   hipStream_t stream() const { return stream_; }
+  DeviceCtx* device_ctx() const { return static_cast<DeviceCtx*>(ctx_); }
   int device() const { return device_; }
   const char* name() const override { return "hip"; }
   int64_t ld(int64_t d) const override { return svmd_padded_dim(d); }
@@ -617,6 +619,11 @@ class RcclTransport final : public Transport {
     NCCLT(ncclGather(send, recv, size_t(bytes), ncclUint8, root, comm_, stream_));
     wait("ncclGather");
   }
+  void allgather(const void* send, int64_t bytes, void* recv) override {
+    if (bytes <= 0) return;
+    NCCLT(ncclAllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
+    wait("ncclAllGather");
+  }
   void send_i64(int64_t v, int peer) override {
     pinned_[2] = v;
     HIPT(hipMemcpyAsync(scratch_ + 2, pinned_ + 2, 8, hipMemcpyHostToDevice, stream_));
@@ -775,6 +782,50 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
     return e.what();
   }
   return "";
+}
+
+// One rank of the distributed decomposition SMO (decomp.hip): the rank's GPU gets all n uint8 rows
+// and labels, quantises them, and runs the solve over its block range with the candidate records
+// all-gathered through `tr` (null: one GPU).  alpha_out (host, n doubles) may be null.
+void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                    const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
+                    double* mm_out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  auto check = [](int rc, const char* what) {
+    if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
+  };
+  DeviceCtx* ctx = be.device_ctx();
+  auto* Xd = static_cast<uint8_t*>(be.alloc(n * d));
+  auto* yd = static_cast<int32_t*>(be.alloc(n * 4));
+  auto* ad = static_cast<double*>(be.alloc(n * 8));
+  auto* mm = static_cast<double*>(be.alloc(2 * d * 8));
+  struct Free {
+    HipBackend& b;
+    std::vector<void*> ptrs;
+    ~Free() {
+      for (void* q : ptrs) b.free(q);
+    }
+  } fr{be, {Xd, yd, ad, mm}};
+  be.h2d(Xd, X, n * d);
+  be.h2d(yd, y, n * 4);
+  check(svmd_minmax_u8(ctx, Xd, n, d, mm, mm + d), "svmd_minmax_u8");
+  std::vector<double> mmh(size_t(2 * d));
+  be.d2h(mmh.data(), mm, 2 * d * 8);
+  if (mm_out) std::memcpy(mm_out, mmh.data(), size_t(2 * d) * 8);
+  const int world = tr ? tr->world() : 1, rank = tr ? tr->rank() : 0;
+  DecompAllGather ag;
+  if (tr) ag = [tr](const void* send, int64_t bytes, void* recv) { tr->allgather(send, bytes, recv); };
+  bool used = false;
+  double prep = 0.0;
+  svm_result res{};
+  check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, world, rank,
+                      ag),
+        "decomposition SMO");
+  if (!used) throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan)");
+  if (alpha_out) be.d2h(alpha_out, ad, n * 8);
+  be.sync();
+  if (r) *r = res;
+  if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace
@@ -957,6 +1008,104 @@ SVM_API svm_cascade_out* svmd_cascade_group_fit(void* h, const void* X, int32_t 
   } catch (const std::exception& e) {
     set_error("cascade: %s", e.what());
     return nullptr;
+  }
+}
+
+// Distributed decomposition SMO over the group's ranks: every rank's GPU holds all n uint8 rows (host
+// X, n x d) and owns a block range of f; one candidate all-gather per outer iteration.  alpha_out
+// (host, n doubles) and r come from rank 0 (every rank's alpha is the same replica); stats: 6 int64
+// (decomp.h) from rank 0; rank_ms (world doubles, may be null): each rank's wall time; mm_out (2 d
+// doubles, may be null): the column min / max the model's scaling uses.
+SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                      const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                      int64_t* stats, double* rank_ms, double* mm_out) {
+  auto* g = static_cast<Group*>(h);
+  if (!g || !X || !y || n < 2 || d <= 0) {
+    set_error("svmd_cascade_group_decomp: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->broken) {
+    set_error("svmd_cascade_group_decomp: the group's communicators were aborted by an earlier failure");
+    return SVM_ERR_ARG;
+  }
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  const int P = g->world;
+  auto token = std::make_shared<AbortToken>();
+  const WaitPolicy wp{token, g->timeout_s};
+  std::vector<Transport*> tr(static_cast<size_t>(P));
+  std::vector<std::unique_ptr<LoopbackTransport>> ltr;
+  std::shared_ptr<LoopbackGroup> lg = g->rccl ? nullptr : std::make_shared<LoopbackGroup>(P, wp);
+  for (int rr = 0; rr < P; ++rr) {
+    if (g->rccl) {
+      g->rtr[size_t(rr)]->set_policy(wp);
+      tr[size_t(rr)] = g->rtr[size_t(rr)].get();
+    } else {
+      ltr.push_back(std::make_unique<LoopbackTransport>(lg, rr, g->be[size_t(rr)].get()));
+      tr[size_t(rr)] = ltr.back().get();
+    }
+  }
+  std::vector<double> ms(static_cast<size_t>(P), 0.0);
+  try {
+    g->pool->run(
+        token,
+        [&](int rr) {
+          if (hipSetDevice(g->devices[size_t(rr)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
+          decomp_on_rank(*g->be[size_t(rr)], P > 1 ? tr[size_t(rr)] : nullptr, X, y, n, d, p, q,
+                         rr == 0 ? alpha_out : nullptr, rr == 0 ? r : nullptr, rr == 0 ? stats : nullptr,
+                         &ms[size_t(rr)], rr == 0 ? mm_out : nullptr);
+        },
+        [&](int rr) {
+          (void)hipSetDevice(g->devices[size_t(rr)]);
+          tr[size_t(rr)]->abort();
+        });
+  } catch (const std::exception& e) {
+    if (g->rccl) g->broken = true;
+    set_error("decomposition SMO: %s", e.what());
+    return SVM_ERR_DEVICE;
+  }
+  if (rank_ms)
+    for (int rr = 0; rr < P; ++rr) rank_ms[rr] = ms[size_t(rr)];
+  return SVM_OK;
+}
+
+// One process rank of the distributed decomposition SMO (every rank passes all n rows and labels).
+SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                     const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                     int64_t* stats, double* ms_out, double* mm_out) {
+  auto* pr = static_cast<ProcRank*>(h);
+  if (!pr || !X || !y || n < 2 || d <= 0) {
+    set_error("svmd_cascade_rank_decomp: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  if (pr->broken) {
+    set_error("svmd_cascade_rank_decomp: the communicator was aborted by an earlier failure");
+    return SVM_ERR_ARG;
+  }
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  try {
+    (void)hipSetDevice(pr->device);
+    pr->tr->set_policy(WaitPolicy{nullptr, pr->timeout_s});
+    try {
+      decomp_on_rank(*pr->be, pr->tr->world() > 1 ? pr->tr.get() : nullptr, X, y, n, d, p, q, alpha_out, r, stats,
+                     ms_out, mm_out);
+    } catch (...) {
+      pr->tr->abort();  // the peers' waits fail too
+      pr->broken = true;
+      throw;
+    }
+    return SVM_OK;
+  } catch (const std::exception& e) {
+    set_error("decomposition SMO: %s", e.what());
+    return SVM_ERR_DEVICE;
   }
 }
 

@@ -1,0 +1,36 @@
+// Working-set decomposition SMO (decomp.hip): shapes and the host driver, shared by the one-GPU C ABI
+// (svmd_train_decomp_u8) and the distributed solve over a cascade group or process rank
+// (cascade_dev.hip: svmd_cascade_group_decomp / svmd_cascade_rank_decomp).
+#pragma once
+#include <cstdint>
+#include <functional>
+
+#include "ctx.h"
+
+namespace svm355 {
+
+// Selection shape for n points: NB blocks of `per` points, T candidates per side per block, L = 2 NB T
+// gathered candidates (<= 1024), q the working-set capacity.
+struct DecompShape {
+  bool ok = false;
+  int q = 0, T = 0;
+  int64_t NB = 0, per = 0, L = 0;
+};
+DecompShape decomp_shape(int64_t n, int qws, int world);
+
+// All-gather of `bytes` from every GPU into recv (world * bytes, GPU-major), ordered on the solver's
+// stream (the distributed solve's one exchange per outer iteration).
+using DecompAllGather = std::function<void(const void* send, int64_t bytes, void* recv)>;
+
+int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+               const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
+               svm_result* r, int64_t* stats, int world = 1, int rank = 0, const DecompAllGather& allgather = {});
+
+// Quantise the device uint8 rows (all n) into the context's grow-only buffer and run the solve.
+// *used = false (nothing done) when the rows' statistics do not admit the exact-integer plan.
+// prep_ms: the quantisation's host-side time.
+int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                  const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
+                  bool* used, double* prep_ms, int world = 1, int rank = 0, const DecompAllGather& allgather = {});
+
+}  // namespace svm355

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <vector>
 
+#include "decomp.h"
 #include "persist.h"
 #include "svm355_device.h"
 #include "trace.h"
@@ -47,156 +48,6 @@ struct DecompHost {  // pinned: written by the kernels, read by the host once pe
 
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
 constexpr int kMaxWS = 1024;             // working-set capacity (one 1024-thread inner workgroup)
-
-// Per block b of `per` points: the T most violating points of I_high (smallest f) and of I_low
-// (largest f) in wave_arg's order (value, then lowest index): T rounds of a block arg-reduction, the
-// winner masked out by its owner after each round.  -1 = fewer than T candidates.
-__global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restrict__ f,
-                                                           const double* __restrict__ alpha,
-                                                           const int32_t* __restrict__ y, int64_t n, int64_t per,
-                                                           int T, double C, double eps, int32_t* __restrict__ cand_h,
-                                                           int32_t* __restrict__ cand_l) {
-  constexpr int NW = kSelNT / 64;
-  __shared__ double sv[2][NW];
-  __shared__ uint32_t si[2][NW];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t lo = int64_t(blockIdx.x) * per, hi = std::min<int64_t>(n, lo + per);
-  const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
-  double fh[kSelE], fl[kSelE];
-#pragma unroll
-  for (int e = 0; e < kSelE; ++e) {
-    const int64_t i = lo + t + int64_t(kSelNT) * e;
-    fh[e] = inf;
-    fl[e] = -inf;
-    if (i < hi) {
-      const double a = alpha[i], fi = f[i];
-      const int32_t yi = y[i];
-      if ((yi == 1 && a < c_hi) || (yi == -1 && a > c_lo)) fh[e] = fi;
-      if ((yi == 1 && a > c_lo) || (yi == -1 && a < c_hi)) fl[e] = fi;
-    }
-  }
-  for (int k = 0; k < T; ++k) {
-    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
-#pragma unroll
-    for (int e = 0; e < kSelE; ++e) {  // ascending index within a thread: strict compares keep the lowest
-      const uint32_t i = uint32_t(lo + t + int64_t(kSelNT) * e);
-      if (fh[e] < mn.v) mn = VI{fh[e], i};
-      if (fl[e] > mx.v) mx = VI{fl[e], i};
-    }
-    const VIL a = wave_arg<true>(mn), b = wave_arg<false>(mx);
-    if (lane == 0) {
-      sv[0][w] = a.v;
-      si[0][w] = a.i;
-      sv[1][w] = b.v;
-      si[1][w] = b.i;
-    }
-    __syncthreads();
-    VI gm{sv[0][0], si[0][0]}, gx{sv[1][0], si[1][0]};
-#pragma unroll
-    for (int q = 1; q < NW; ++q) {
-      const VI cm{sv[0][q], si[0][q]}, cx{sv[1][q], si[1][q]};
-      if (beats<true>(cm, gm)) gm = cm;
-      if (beats<false>(cx, gx)) gx = cx;
-    }
-    __syncthreads();  // the LDS slots are rewritten next round
-    if (t == 0) {
-      cand_h[int64_t(blockIdx.x) * T + k] = (gm.i == kSentinel || !(gm.v < inf)) ? -1 : int32_t(gm.i);
-      cand_l[int64_t(blockIdx.x) * T + k] = (gx.i == kSentinel || !(gx.v > -inf)) ? -1 : int32_t(gx.i);
-    }
-#pragma unroll
-    for (int e = 0; e < kSelE; ++e) {
-      const uint32_t i = uint32_t(lo + t + int64_t(kSelNT) * e);
-      if (i == gm.i) fh[e] = inf;
-      if (i == gx.i) fl[e] = -inf;
-    }
-  }
-}
-
-// One workgroup: b_high = min f over the I_high candidates, b_low = max f over the I_low ones (the
-// global extremes: every block's first pick is its own extreme), the stop test, and the working set
-// = the sorted union of the candidates without duplicates (a free SV may be in both lists).
-__global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const int32_t* __restrict__ cand, int L, int Lh,
-                                                          const double* __restrict__ f, double tau,
-                                                          int32_t* __restrict__ W, DecompHost* __restrict__ hs) {
-  __shared__ int32_t s[kMaxWS];
-  __shared__ int32_t wsum[kMaxWS / 64];
-  __shared__ double red[2][kMaxWS / 64];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int32_t c = t < L ? cand[t] : -1;
-  double vh = __builtin_inf(), vl = -__builtin_inf();
-  if (c >= 0) {
-    if (t < Lh)
-      vh = f[c];
-    else
-      vl = f[c];
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    vh = fmin(vh, __shfl_xor(vh, off, 64));
-    vl = fmax(vl, __shfl_xor(vl, off, 64));
-  }
-  if (lane == 0) {
-    red[0][w] = vh;
-    red[1][w] = vl;
-  }
-  s[t] = c >= 0 ? c : INT_MAX;
-  __syncthreads();
-  // bitonic sort of the 1024 candidate ids (ascending; INT_MAX = empty)
-  for (int k = 2; k <= kMaxWS; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int p = t ^ j;
-      if (p > t) {
-        const int32_t x = s[t], y = s[p];
-        const bool up = (t & k) == 0;
-        if ((x > y) == up) {
-          s[t] = y;
-          s[p] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  const int32_t v = s[t];
-  const bool keep = v != INT_MAX && (t == 0 || s[t - 1] != v);
-  const unsigned long long bal = __ballot(keep);
-  if (lane == 0) wsum[w] = __popcll(bal);
-  __syncthreads();
-  int off = 0;
-  for (int q = 0; q < w; ++q) off += wsum[q];
-  if (keep) W[off + __popcll(bal & ((1ull << lane) - 1ull))] = v;
-  if (t == 0) {
-    int m = 0;
-    double bh = __builtin_inf(), bl = -__builtin_inf();
-    for (int q = 0; q < kMaxWS / 64; ++q) {
-      m += wsum[q];
-      bh = fmin(bh, red[0][q]);
-      bl = fmax(bl, red[1][q]);
-    }
-    hs->m = m;
-    hs->b_high = bh;
-    hs->b_low = bl;
-    // no candidate on either side: the reference's "i_high or i_low not found" (main3.cpp:205-209)
-    hs->stop = !(bh < __builtin_inf()) || !(bl > -__builtin_inf()) ? SVM_STOP_NO_CANDIDATE
-               : (bl <= bh + 2.0 * tau)                             ? SVM_STOP_CONVERGED
-                                                                    : SVM_STOP_RUNNING;
-  }
-}
-
-// Qw[k] = Q[W[k]] (kq bytes), N0w[k], WNw[k]: one workgroup per working-set row.
-__global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict__ Q, const int32_t* __restrict__ N0,
-                                                       const double* __restrict__ WN, int kq,
-                                                       const int32_t* __restrict__ W, int m, int8_t* __restrict__ Qw,
-                                                       int32_t* __restrict__ N0w, double* __restrict__ WNw) {
-  const int k = blockIdx.x;
-  if (k >= m) return;
-  const int64_t src = W[k];
-  const int4* s = reinterpret_cast<const int4*>(Q + src * int64_t(kq));
-  int4* d = reinterpret_cast<int4*>(Qw + int64_t(k) * kq);
-  for (int c = threadIdx.x; c < kq / 16; c += 64) d[c] = s[c];
-  if (threadIdx.x == 0) {
-    N0w[k] = N0[src];
-    WNw[k] = WN[src];
-  }
-}
 
 // Both of an iteration's wave arg-reductions in lockstep (minimum over I_high, maximum over I_low):
 // the two high-word butterflies are independent DPP chains and interleave; each side falls back to
@@ -234,6 +85,178 @@ __device__ __forceinline__ void wave_arg_pair(VI mn, VI mx, VIL& rmn, VIL& rmx) 
   }
 }
 
+// A working-set candidate: global point id (-1 = none) and its f.  Candidates carry f because in the
+// distributed solve a GPU holds f only for its own points (every GPU holds alpha and y for all).
+struct CandRec {
+  double f;
+  int32_t id, pad;
+};
+
+// Per block b of `per` points of this GPU's slice (local rows [b per, (b + 1) per), global ids lo +
+// local): the T most violating points of I_high (smallest f) and of I_low (largest f) in wave_arg's
+// order (value, then lowest index): T rounds of a block arg-reduction, the winner masked out by its
+// owner after each round.  f is the slice's (local index); alpha and y are global.
+__global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restrict__ f,
+                                                           const double* __restrict__ alpha,
+                                                           const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
+                                                           int64_t per, int T, double C, double eps,
+                                                           CandRec* __restrict__ cand_h, CandRec* __restrict__ cand_l) {
+  constexpr int NW = kSelNT / 64;
+  __shared__ double sv[2][NW];
+  __shared__ uint32_t si[2][NW];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t b0 = int64_t(blockIdx.x) * per, b1 = std::min<int64_t>(nloc, b0 + per);
+  const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
+  double fh[kSelE], fl[kSelE];
+#pragma unroll
+  for (int e = 0; e < kSelE; ++e) {
+    const int64_t i = b0 + t + int64_t(kSelNT) * e;
+    fh[e] = inf;
+    fl[e] = -inf;
+    if (i < b1) {
+      const double a = alpha[lo + i], fi = f[i];
+      const int32_t yi = y[lo + i];
+      if ((yi == 1 && a < c_hi) || (yi == -1 && a > c_lo)) fh[e] = fi;
+      if ((yi == 1 && a > c_lo) || (yi == -1 && a < c_hi)) fl[e] = fi;
+    }
+  }
+  for (int k = 0; k < T; ++k) {
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+#pragma unroll
+    for (int e = 0; e < kSelE; ++e) {  // ascending index within a thread: strict compares keep the lowest
+      const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
+      const bool ch = fh[e] < mn.v, cl = fl[e] > mx.v;
+      mn = ch ? VI{fh[e], i} : mn;
+      mx = cl ? VI{fl[e], i} : mx;
+    }
+    VIL a, b;
+    wave_arg_pair(mn, mx, a, b);
+    if (lane == 0) {
+      sv[0][w] = a.v;
+      si[0][w] = a.i;
+      sv[1][w] = b.v;
+      si[1][w] = b.i;
+    }
+    __syncthreads();
+    VI gm{sv[0][0], si[0][0]}, gx{sv[1][0], si[1][0]};
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      const VI cm{sv[0][q], si[0][q]}, cx{sv[1][q], si[1][q]};
+      if (beats<true>(cm, gm)) gm = cm;
+      if (beats<false>(cx, gx)) gx = cx;
+    }
+    __syncthreads();  // the LDS slots are rewritten next round
+    if (t == 0) {
+      const bool hok = gm.i != kSentinel && gm.v < inf, lok = gx.i != kSentinel && gx.v > -inf;
+      cand_h[int64_t(blockIdx.x) * T + k] = CandRec{hok ? gm.v : 0.0, hok ? int32_t(gm.i) : -1, 0};
+      cand_l[int64_t(blockIdx.x) * T + k] = CandRec{lok ? gx.v : 0.0, lok ? int32_t(gx.i) : -1, 0};
+    }
+#pragma unroll
+    for (int e = 0; e < kSelE; ++e) {
+      const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
+      if (i == gm.i) fh[e] = inf;
+      if (i == gx.i) fl[e] = -inf;
+    }
+  }
+}
+
+// One workgroup over the L gathered candidates (Lr per GPU, GPU-major; the first Lh of each GPU's
+// are I_high picks, the rest I_low): b_high = min f over the I_high candidates, b_low = max f over
+// the I_low ones (the global extremes: every block's first pick is its own extreme), the stop test,
+// and the working set = the candidates' ids sorted, without duplicates (a free SV may be in both
+// lists), with their f (Wf).  Independent of the order the candidates arrive in.
+__global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restrict__ cand, int L, int Lr, int Lh,
+                                                          double tau, int32_t* __restrict__ W,
+                                                          double* __restrict__ Wf, DecompHost* __restrict__ hs) {
+  __shared__ int32_t s[kMaxWS];
+  __shared__ double sf[kMaxWS];
+  __shared__ int32_t wsum[kMaxWS / 64];
+  __shared__ double red[2][kMaxWS / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const CandRec c = t < L ? cand[t] : CandRec{0.0, -1, 0};
+  double vh = __builtin_inf(), vl = -__builtin_inf();
+  if (c.id >= 0) {
+    if (t % Lr < Lh)
+      vh = c.f;
+    else
+      vl = c.f;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    vh = fmin(vh, __shfl_xor(vh, off, 64));
+    vl = fmax(vl, __shfl_xor(vl, off, 64));
+  }
+  if (lane == 0) {
+    red[0][w] = vh;
+    red[1][w] = vl;
+  }
+  s[t] = c.id >= 0 ? c.id : INT_MAX;
+  sf[t] = c.f;
+  __syncthreads();
+  // bitonic sort of the 1024 candidate ids (ascending; INT_MAX = empty), f riding along
+  for (int k = 2; k <= kMaxWS; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int p = t ^ j;
+      if (p > t) {
+        const int32_t x = s[t], y = s[p];
+        const bool up = (t & k) == 0;
+        if ((x > y) == up) {
+          const double fx = sf[t];
+          s[t] = y;
+          s[p] = x;
+          sf[t] = sf[p];
+          sf[p] = fx;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int32_t v = s[t];
+  const bool keep = v != INT_MAX && (t == 0 || s[t - 1] != v);
+  const unsigned long long bal = __ballot(keep);
+  if (lane == 0) wsum[w] = __popcll(bal);
+  __syncthreads();
+  int off = 0;
+  for (int q = 0; q < w; ++q) off += wsum[q];
+  if (keep) {
+    const int j = off + __popcll(bal & ((1ull << lane) - 1ull));
+    W[j] = v;
+    Wf[j] = sf[t];  // duplicates of an id carry the same f
+  }
+  if (t == 0) {
+    int m = 0;
+    double bh = __builtin_inf(), bl = -__builtin_inf();
+    for (int q = 0; q < kMaxWS / 64; ++q) {
+      m += wsum[q];
+      bh = fmin(bh, red[0][q]);
+      bl = fmax(bl, red[1][q]);
+    }
+    hs->m = m;
+    hs->b_high = bh;
+    hs->b_low = bl;
+    // no candidate on either side: the reference's "i_high or i_low not found" (main3.cpp:205-209)
+    hs->stop = !(bh < __builtin_inf()) || !(bl > -__builtin_inf()) ? SVM_STOP_NO_CANDIDATE
+               : (bl <= bh + 2.0 * tau)                             ? SVM_STOP_CONVERGED
+                                                                    : SVM_STOP_RUNNING;
+  }
+}
+
+// Qw[k] = Q[W[k]] (kq bytes), N0w[k], WNw[k]: one workgroup per working-set row.
+__global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict__ Q, const int32_t* __restrict__ N0,
+                                                       const double* __restrict__ WN, int kq,
+                                                       const int32_t* __restrict__ W, int m, int8_t* __restrict__ Qw,
+                                                       int32_t* __restrict__ N0w, double* __restrict__ WNw) {
+  const int k = blockIdx.x;
+  if (k >= m) return;
+  const int64_t src = W[k];
+  const int4* s = reinterpret_cast<const int4*>(Q + src * int64_t(kq));
+  int4* d = reinterpret_cast<int4*>(Qw + int64_t(k) * kq);
+  for (int c = threadIdx.x; c < kq / 16; c += 64) d[c] = s[c];
+  if (threadIdx.x == 0) {
+    N0w[k] = N0[src];
+    WNw[k] = WN[src];
+  }
+}
+
 // First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER points
 // W[t + NT e] (f, alpha, y in registers).  Per iteration:
 //   select   branch-free thread-local (value, lowest position) minimum over I_high and maximum over
@@ -253,7 +276,7 @@ template <int NT, int PER, bool PROF = false, bool W2 = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, int m,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
-                                                      const double* __restrict__ f, double C, double eps,
+                                                      const double* __restrict__ Wf, double C, double eps,
                                                       double tau_in, int64_t max_inner, int32_t* __restrict__ cols,
                                                       double* __restrict__ coef, int32_t* __restrict__ mcount,
                                                       DecompHost* __restrict__ hs) {
@@ -279,7 +302,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     yp[e] = yk == 1;
     yn[e] = yk == -1;
     sy[k] = int8_t(yk);
-    ft[e] = valid ? f[gid[e]] : 0.0;
+    ft[e] = valid ? Wf[k] : 0.0;
   }
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
   int64_t it = 0;
@@ -528,12 +551,10 @@ __global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __rest
 }
 
 __global__ void ws_init_kernel(const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f,
-                               int64_t n) {
+                               int64_t lo, int64_t nloc, int64_t n) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) {
-    alpha[i] = 0.0;
-    f[i] = -static_cast<double>(y[i]);  // main3.cpp:165-172
-  }
+  if (i < n) alpha[i] = 0.0;
+  if (i < nloc) f[i] = -static_cast<double>(y[lo + i]);  // main3.cpp:165-172
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -542,33 +563,51 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 }  // namespace
 
-// Decomposition solve on quantised rows (Q, N0, WN, the plan's step weights in stw on the device).
-// alpha: n doubles (cold start: zeroed here).  q: working-set size (<= 1024).  stats (6 int64):
-// outer iterations, inner iterations, working-set size, solve microseconds, columns of the f updates
-// (points moved, summed over the outer iterations), inner workgroup size.
+DecompShape decomp_shape(int64_t n, int qws, int world) {
+  DecompShape d;
+  d.q = std::max(4, std::min(qws, kMaxWS));
+  // blocks of <= 4096 points, at least 64 blocks (each gives its own top-T picks), a multiple of 8 so
+  // 1, 2, 4 or 8 GPUs own whole blocks and the distributed trajectory is the one-GPU one (another
+  // world rounds to a multiple of it)
+  const int64_t nb0 = std::max<int64_t>((n + kSelNT * kSelE - 1) / (kSelNT * kSelE), std::min<int64_t>(64, (n + 63) / 64));
+  const int64_t mult = (8 % world == 0) ? 8 : int64_t(8) * world;
+  d.NB = (nb0 + mult - 1) / mult * mult;
+  d.per = (n + d.NB - 1) / d.NB;
+  d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
+  d.L = 2 * d.NB * d.T;
+  d.ok = n >= 2 && n < int64_t(kSentinel) && d.L <= kMaxWS && d.per <= int64_t(kSelNT) * kSelE && world >= 1;
+  return d;
+}
+
+// Decomposition solve on quantised rows (Q, N0, WN: all n rows; the plan's step weights in stw on the
+// device).  alpha: n doubles (cold start: zeroed here).  q: working-set size (<= 1024).
+// Distributed (world > 1): this GPU owns the blocks [rank NB / world, (rank + 1) NB / world) of the
+// selection's global block partition, keeps f for their points only, and exchanges its candidate
+// records once per outer iteration through `allgather`; every GPU then builds the same working set and
+// runs the same inner solve on the same inputs (alpha is replicated and updated identically), and
+// updates f for its own points.  With world dividing 8 the trajectory is the one-GPU trajectory.
+// stats (6 int64): outer iterations, inner iterations, working-set size, solve microseconds, columns
+// of the f updates (points moved, summed over the outer iterations), inner workgroup size.
 int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
-               svm_result* r, int64_t* stats) {
+               svm_result* r, int64_t* stats, int world, int rank, const DecompAllGather& allgather) {
   const auto t0 = std::chrono::steady_clock::now();
   hipStream_t s = ctx->stream;
-  if (n < 2 || n >= int64_t(kSentinel) || n > (int64_t(1) << 31) - 1) {
-    set_error("decomposition SMO: need 2 <= n < 2^31");
+  if (world < 1 || rank < 0 || rank >= world || (world > 1 && !allgather)) {
+    set_error("decomposition SMO: bad world / rank / exchange");
     return SVM_ERR_ARG;
   }
-  qws = std::max(4, std::min(qws, kMaxWS));
-  // blocks of <= 4096 points; T candidates per side per block with 2 * NB * T <= 1024
-  const int64_t NB = std::max<int64_t>((n + kSelNT * kSelE - 1) / (kSelNT * kSelE), std::min<int64_t>(64, (n + 63) / 64));
-  const int T = int(std::max<int64_t>(1, qws / (2 * NB)));
-  const int64_t L = 2 * NB * T;
-  if (L > kMaxWS) {
-    set_error("decomposition SMO: n = %lld needs %lld candidates per round (> %d)", (long long)n, (long long)L, kMaxWS);
+  const DecompShape sh = decomp_shape(n, qws, world);
+  if (!sh.ok) {
+    set_error("decomposition SMO: n = %lld is outside the solver's shapes (2 <= n, %lld candidates <= %d, blocks "
+              "of <= %d points)", (long long)n, (long long)sh.L, kMaxWS, kSelNT * kSelE);
     return SVM_ERR_ARG;
   }
-  const int64_t per = (n + NB - 1) / NB;
-  if (per > int64_t(kSelNT) * kSelE) {
-    set_error("decomposition SMO: selection blocks too large");
-    return SVM_ERR_INTERNAL;
-  }
+  const int64_t NBr = sh.NB / world, b0 = rank * NBr;
+  const int64_t lo = std::min<int64_t>(n, b0 * sh.per), hi = std::min<int64_t>(n, (b0 + NBr) * sh.per);
+  const int64_t nloc = hi - lo;
+  const int T = sh.T;
+  const int64_t Lr = 2 * NBr * T;  // this GPU's candidate records (I_high picks, then I_low)
   // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512 | 1024
   int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
@@ -580,7 +619,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
   // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
   const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
-  const int64_t ldw = kMaxWS;            // K(W, W) row stride
+  const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   size_t off = 0;
@@ -589,18 +628,21 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     off += al(bytes);
     return o;
   };
-  const size_t o_f = take(size_t(n) * 8), o_cand = take(size_t(L) * 4), o_W = take(kMaxWS * 4),
+  const size_t o_f = take(size_t(std::max<int64_t>(nloc, 1)) * 8), o_own = take(size_t(Lr) * sizeof(CandRec)),
+               o_all = take(size_t(sh.L) * sizeof(CandRec)), o_W = take(kMaxWS * 4), o_Wf = take(kMaxWS * 8),
                o_Qw = take(size_t(kMaxWS) * P.kq), o_N0w = take(kMaxWS * 4), o_WNw = take(kMaxWS * 8),
-               o_Kw = take(size_t(kMaxWS) * ldw * 8),
-               o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4), o_mcount = take(256), o_part = take(size_t(n) * ldp * 8);
+               o_Kw = take(size_t(kMaxWS) * ldw * 8), o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4),
+               o_mcount = take(256), o_part = take(size_t(std::max<int64_t>(nloc, 1)) * ldp * 8);
   int rc = ctx->ensure_ws(off);
   if (rc) return rc;
   rc = ctx->ensure_pinned(sizeof(DecompHost) * 2);
   if (rc) return rc;
   char* ws = static_cast<char*>(ctx->ws);
   auto* f = reinterpret_cast<double*>(ws + o_f);
-  auto* cand = reinterpret_cast<int32_t*>(ws + o_cand);
+  auto* cown = reinterpret_cast<CandRec*>(ws + o_own);
+  auto* call = world > 1 ? reinterpret_cast<CandRec*>(ws + o_all) : cown;
   auto* W = reinterpret_cast<int32_t*>(ws + o_W);
+  auto* Wf = reinterpret_cast<double*>(ws + o_Wf);
   auto* Qw = reinterpret_cast<int8_t*>(ws + o_Qw);
   auto* N0w = reinterpret_cast<int32_t*>(ws + o_N0w);
   auto* WNw = reinterpret_cast<double*>(ws + o_WNw);
@@ -611,15 +653,19 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   auto* part = reinterpret_cast<double*>(ws + o_part);
   auto* hs = static_cast<DecompHost*>(ctx->pinned);
   std::memset(hs, 0, sizeof(DecompHost));
-  hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, n);
+  hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n);
   SVMD_LAUNCH_CHECK();
   int64_t outer = 0, inner_total = 0, changed_total = 0;
   int32_t stop = SVM_STOP_RUNNING;
   double bh = 0.0, bl = 0.0;
   for (;;) {
-    hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NB)), dim3(kSelNT), 0, s, f, alpha, y, n, per, T, p.C, p.eps,
-                       cand, cand + NB * T);
-    hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, cand, int(L), int(NB * T), f, p.tau, W, hs);
+    if (NBr > 0)
+      hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per, T,
+                         p.C, p.eps, cown, cown + NBr * T);
+    SVMD_LAUNCH_CHECK();
+    if (world > 1) allgather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
+    hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
+                       W, Wf, hs);
     SVMD_LAUNCH_CHECK();
     SVMD_CHECK(hipStreamSynchronize(s));
     if (outer > 0) {  // the previous outer iteration's inner solve
@@ -654,7 +700,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
     const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, f, p.C,  \
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, p.C, \
                      p.eps, tau_in, max_inner, cols, coef, mcount, hs)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
@@ -678,11 +724,14 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
     SVMD_LAUNCH_CHECK();
-    rc = launch_igram_gemv(s, Q, N0, WN, stw, n, cols, coef, mcount, m, P, p.gamma, part, ldp);
-    if (rc) return rc;
-    hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
-                       f, n);
-    SVMD_LAUNCH_CHECK();
+    if (nloc > 0) {
+      rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
+                             m, P, p.gamma, part, ldp);
+      if (rc) return rc;
+      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
+                         f, nloc);
+      SVMD_LAUNCH_CHECK();
+    }
     ++outer;
   }
   if (prof && inner_total > 0) {
@@ -695,7 +744,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   if (stats) {
     stats[0] = outer;
     stats[1] = inner_total;
-    stats[2] = qws;
+    stats[2] = sh.q;
     stats[3] = int64_t(ms_since(t0) * 1000.0);
     stats[4] = changed_total;
     stats[5] = inner_nt;
@@ -710,6 +759,58 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     r->n_sv = -1;
     r->seconds = ms_since(t0) / 1e3;
   }
+  return SVM_OK;
+}
+
+int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                  const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
+                  bool* used, double* prep_ms, int world, int rank, const DecompAllGather& allgather) {
+  const auto t0 = std::chrono::steady_clock::now();
+  *used = false;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;  // igram's LDS table bound
+  // quantised rows live in the context's grow-only buffer (the solver's workspace is ctx->ws)
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t need = al(size_t(n) * P.kq) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
+                      al(quantize_u8_aux_bytes(P));
+  if (need > ctx->gram_bytes) {
+    if (ctx->gram) {
+      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+      SVMD_CHECK(hipFree(ctx->gram));
+      ctx->gram = nullptr;
+      ctx->gram_bytes = 0;
+    }
+    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
+    ctx->gram_bytes = need;
+  }
+  char* base = reinterpret_cast<char*>(ctx->gram);
+  auto* Q = reinterpret_cast<int8_t*>(base);
+  auto* N0 = reinterpret_cast<int32_t*>(base + al(size_t(n) * P.kq));
+  auto* WN = reinterpret_cast<double*>(reinterpret_cast<char*>(N0) + al(size_t(n) * 4));
+  auto* stw = reinterpret_cast<double*>(reinterpret_cast<char*>(WN) + al(size_t(n) * 8));
+  void* aux = reinterpret_cast<char*>(stw) + al(P.step_w.size() * 8);
+  bool ok = false;
+  {
+    TraceRange tr("svm355:quantise");
+    const int rc = quantize_u8_rows(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
+    if (rc) return rc;
+  }
+  if (!ok) return SVM_OK;
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  if (prep_ms) *prep_ms = ms_since(t0);
+  {
+    TraceRange ts("svm355:decomp");
+    const int rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, world, rank,
+                              allgather);
+    if (rc) return rc;
+  }
+  if (r) {
+    int64_t c = 0;
+    const int rc = count_sv(ctx, alpha_d, n, 1, p.sv_tol, &c);
+    if (rc) return rc;
+    r->n_sv = c;
+  }
+  *used = true;
   return SVM_OK;
 }
 
@@ -739,53 +840,16 @@ SVM_API int svmd_train_decomp_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_
   const auto t0 = std::chrono::steady_clock::now();
   int rc = ctx->begin();
   if (rc) return rc;
-  QuantPlan P;
-  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return ctx->end();  // igram's LDS table bound
-  // quantised rows live in their own grow-only buffer (the solver's workspace is ctx->ws)
-  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  const size_t need = al(size_t(n) * P.kq) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
-                      al(quantize_u8_aux_bytes(P));
-  if (need > ctx->gram_bytes) {
-    if (ctx->gram) {
-      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
-      SVMD_CHECK(hipFree(ctx->gram));
-      ctx->gram = nullptr;
-      ctx->gram_bytes = 0;
-    }
-    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
-    ctx->gram_bytes = need;
-  }
-  char* base = reinterpret_cast<char*>(ctx->gram);
-  auto* Q = reinterpret_cast<int8_t*>(base);
-  auto* N0 = reinterpret_cast<int32_t*>(base + al(size_t(n) * P.kq));
-  auto* WN = reinterpret_cast<double*>(reinterpret_cast<char*>(N0) + al(size_t(n) * 4));
-  auto* stw = reinterpret_cast<double*>(reinterpret_cast<char*>(WN) + al(size_t(n) * 8));
-  void* aux = reinterpret_cast<char*>(stw) + al(P.step_w.size() * 8);
-  bool ok = false;
-  {
-    TraceRange tr("svm355:quantise");
-    rc = quantize_u8_rows(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
-    if (rc) return rc;
-  }
-  if (!ok) return ctx->end();
-  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-  const double t_prep = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  {
-    TraceRange ts("svm355:decomp");
-    rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats);
-  }
-  if (!rc && r) {
-    int64_t c = 0;
-    rc = count_sv(ctx, alpha_d, n, 1, p.sv_tol, &c);
-    if (!rc) r->n_sv = c;
-  }
+  bool used = false;
+  double prep = 0.0;
+  rc = decomp_fit_u8(ctx, Xu_d, n, d, mn_h, mx_h, y_d, alpha_d, p, q, r, stats, &used, &prep);
   if (rc) return rc;
-  if (timing) {
-    timing->gram_ms = t_prep;  // quantisation only: no Gram is stored
+  if (used && timing) {
+    timing->gram_ms = prep;  // quantisation only: no Gram is stored
     timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    timing->smo_ms = timing->total_ms - t_prep;
+    timing->smo_ms = timing->total_ms - prep;
   }
-  if (used_out) *used_out = 1;
+  if (used_out) *used_out = used ? 1 : 0;
   return ctx->end();
 }
 

@@ -302,7 +302,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
     double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols, int64_t col0 = 0,
     const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
-    const int32_t* __restrict__ ncount = nullptr) {
+    const int32_t* __restrict__ ncount = nullptr, const int8_t* __restrict__ Qc = nullptr,
+    const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0) {
   static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
@@ -321,6 +322,11 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 
   const int64_t ctiles = RECT ? (ncols + QBM - 1) / QBM : tiles;
   const int64_t c0 = RECT ? col0 : 0;      // global row index of block column 0
+  // column operand: the same rows, or for GEMV the full set the ids colid index (the row operand may
+  // be a slice of it starting at global row row_off)
+  const int8_t* __restrict__ Qb = GEMV ? Qc : Q;
+  const int32_t* __restrict__ N0b = GEMV ? N0c : N0;
+  const double* __restrict__ WNb = GEMV ? WNc : WN;
   const int64_t ntile = RECT ? tiles * ctiles : tiles * (tiles + 1) / 2;
   const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
   int64_t tm, tn;
@@ -347,8 +353,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     if (EXTRA) wn_r[t] = gi < n ? WN[gi] : 0.0;
   } else if (t < QBM + QBN) {
     const int64_t gj = bn + (t - QBM);
-    n0_c[t - QBM] = gj < ncol ? N0[crow(gj)] : 0;
-    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WN[crow(gj)] : 0.0;
+    n0_c[t - QBM] = gj < ncol ? N0b[crow(gj)] : 0;
+    if (EXTRA) wn_c[t - QBM] = gj < ncol ? WNb[crow(gj)] : 0.0;
   }
 
   // Staging per BK-column stage: thread t copies 16-byte chunk t % CPR of rows t / CPR + RPP * p.
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     }
 #pragma unroll
     for (int p = 0; p < BPASS; ++p)
-      gb[p] = brow[p] >= 0 ? *reinterpret_cast<const i32x4*>(Q + brow[p] * kq + k0 + scol) : zero4;
+      gb[p] = brow[p] >= 0 ? *reinterpret_cast<const i32x4*>(Qb + brow[p] * kq + k0 + scol) : zero4;
   };
   gload(0);
 
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
         for (int q = 0; q < 8; ++q) {
           const int r = 8 * half + q;
           const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
-          const double kv = gi == gid ? 1.0 : ex[q];
+          const double kv = gi + row_off == gid ? 1.0 : ex[q];
           rs[r] += cf * kv;  // columns outside the block carry cf = 0
         }
       }
@@ -896,12 +902,14 @@ int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64
 }
 
 // Decomposition solver f update (decomp.hip): part[i * ldp + c] = sum over the c-th 64-column half of
-// coef[k] * K(i, cols[k]) for every row i < n of (Q, N0, WN), k < *mcount (device; <= m, the grid's
+// coef[k] * K(i, cols[k]) for every row i < n of (Q, N0, WN) -- global row row_off + i of the full
+// quantised set (Qc, N0c, WNc) the column ids index -- and k < *mcount (device; <= m, the grid's
 // bound).  ldp >= 2 * ceil(m / 128); halves at or beyond *mcount are not written: the caller sums
 // the first ceil(*mcount / 64) in index order.
 int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
-                      int64_t n, const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m,
-                      const QuantPlan& P, double gamma, double* part, int64_t ldp) {
+                      int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
+                      const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m, const QuantPlan& P,
+                      double gamma, double* part, int64_t ldp) {
   if (n <= 0 || m <= 0) return SVM_OK;
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
   const int64_t nwg = 2 * tiles * ctiles;
@@ -912,7 +920,8 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
   const int bk = P.kq % 128 == 0 ? 128 : 64;
 #define SVM_IGRAM_GEMV(EX, B)                                                                                       \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,        \
-                     P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, m, int64_t(0), cols, coef, mcount)
+                     P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, m, int64_t(0), cols, coef, mcount, Qc, N0c, WNc, \
+                     row_off)
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM_GEMV(true, 128); else SVM_IGRAM_GEMV(true, 64);
   } else {

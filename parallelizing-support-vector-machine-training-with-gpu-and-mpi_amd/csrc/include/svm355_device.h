@@ -190,6 +190,17 @@ SVM_API int svmd_cascade_rank_barrier(void* rank);
 // driver's op set (svm_preflight_script) on RCCL communicators (SVM355_RCCL_PREFLIGHT=0 skips it).
 // A failure aborts the communicators (the group / rank is then unusable).
 SVM_API int svmd_cascade_group_exercise(void* group, const char* script, double timeout_s);
+// Distributed working-set decomposition SMO (decomp.hip) over a group's ranks or one process rank:
+// every rank's GPU holds all n uint8 rows (host X, n x d) and labels, owns a block range of f, and
+// all-gathers its candidate records once per outer iteration; the working set, inner solve and alpha
+// are replicated.  With 1, 2, 4 or 8 ranks the trajectory equals svmd_train_decomp_u8's.  alpha_out
+// (n), r, stats (6 int64, see svmd_train_decomp_u8) and mm_out (2 d: column min / max) may be null.
+SVM_API int svmd_cascade_group_decomp(void* group, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                      const svm_params* p, int32_t q, double* alpha_out, svm_result* r,
+                                      int64_t* stats, double* rank_ms, double* mm_out);
+SVM_API int svmd_cascade_rank_decomp(void* rank, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                     const svm_params* p, int32_t q, double* alpha_out, svm_result* r,
+                                     int64_t* stats, double* ms_out, double* mm_out);
 SVM_API int svmd_cascade_rank_exercise(void* rank, const char* script, double timeout_s);
 SVM_API int svmd_cascade_group_broken(void* group);  // 1 once a failure aborted its communicators
 // RCCL the library was compiled against (NCCL_VERSION_CODE) and the one it runs on (ncclGetVersion),

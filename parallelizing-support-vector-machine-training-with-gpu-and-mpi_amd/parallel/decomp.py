@@ -1,0 +1,130 @@
+"""Distributed working-set decomposition SMO over the GPUs of one node (``--parallel decomp``;
+csrc/hip/decomp.hip + the group / rank entry points of csrc/hip/cascade_dev.hip).
+
+The one-GPU decomposition solver (``SVC(solver="decomp")``) spends its outer iterations on three
+kinds of work: choosing the working set (top violators per block of points), solving it (one
+workgroup, latency-bound), and updating f for all n points (an int8-MFMA GEMV over the points whose
+alpha moved).  The first and last scale with n; the middle does not.  Here every GPU:
+
+- holds all n rows (uint8, quantised on its own device), the labels and a replica of alpha;
+- owns a contiguous range of the selection's blocks and keeps f for those points only;
+- selects its blocks' candidates, and ONE all-gather per outer iteration (RCCL ``ncclAllGather``
+  over xGMI, 16-byte records: id and f) gives every GPU the same candidate list;
+- builds the same working set, runs the same inner solve on the same inputs (so the alpha replicas
+  stay identical without any exchange), and updates f for its own points.
+
+The selection's block partition is global and a multiple of 8 blocks, so with 1, 2, 4 or 8 GPUs the
+trajectory -- every working set, every alpha, b and the iteration counts -- equals the one-GPU
+decomposition solver's (tests/test_gpu_decomp.py).  It pays where the GEMV and the selection
+dominate: large n (see README "Distributed decomposition").
+
+Launch forms: a ``DeviceGroup`` of this process (thread ranks, ``ncclCommInitAll``; or
+``transport="loopback"``: P ranks rehearsed on the visible GPU), or one ``RcclRank`` per process
+under torchrun (``ncclCommInitRank``).
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from typing import Optional
+
+import numpy as np
+
+from .. import _native as N
+from ..utils.config import SVMParams
+
+
+def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: int, world: int) -> dict:
+    X = np.ascontiguousarray(X)
+    if X.dtype != np.uint8 or X.ndim != 2:
+        raise ValueError("the distributed decomposition solver needs uint8 pixel rows (n, d)")
+    y = np.ascontiguousarray(y, dtype=np.int32)
+    n, d = X.shape
+    if y.shape != (n,):
+        raise ValueError("y must be (n,)")
+    alpha = np.empty(n, dtype=np.float64)
+    mm = np.empty(2 * d, dtype=np.float64)
+    r = N.SvmResult()
+    st = (ctypes.c_int64 * 6)()
+    ms = np.zeros(max(world, 1), dtype=np.float64)
+    p = params.to_struct()
+    t0 = time.perf_counter()
+    N.check(fn(handle, N.ptr(X), N.ptr(y), n, d, ctypes.byref(p), int(q), N.ptr(alpha), ctypes.byref(r), st,
+               N.ptr(ms), N.ptr(mm)), fn.__name__)
+    wall = (time.perf_counter() - t0) * 1e3
+    return {"alpha": alpha, "b": float(r.b), "b_high": float(r.b_high), "b_low": float(r.b_low),
+            "iterations": int(r.iterations), "stop_reason": N.STOP_NAMES.get(int(r.stop_reason), str(r.stop_reason)),
+            "n_sv": int(r.n_sv), "mn": mm[:d].copy(), "mx": mm[d:].copy(),
+            "stats": {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
+                      "solve_us": int(st[3]), "update_columns": int(st[4]), "inner_threads": int(st[5])},
+            "rank_ms": [float(x) for x in ms[:world]], "wall_ms": wall}
+
+
+def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
+    """One distributed decomposition solve over a ``DeviceGroup`` (its ranks are this process's
+    threads; RCCL or the loopback rehearsal)."""
+    lib = N.hip()
+    return _fit_native(lib.svmd_cascade_group_decomp, group.handle, X, y, params or SVMParams(), q, group.world)
+
+
+def rank_fit(rank, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
+    """This process's rank of a distributed decomposition solve (every rank passes all rows)."""
+    lib = N.hip()
+    return _fit_native(lib.svmd_cascade_rank_decomp, rank.handle, X, y, params or SVMParams(), q, 1)
+
+
+class DistributedDecompSVC:
+    """Estimator over a ``DeviceGroup`` or an ``RcclRank``: ``fit`` / ``decision_function`` /
+    ``predict`` / ``score``; the fitted model is an ``SVC`` on this process's GPU."""
+
+    def __init__(self, world: int = 1, transport: str = "auto", C: float = 10.0, gamma: float = 0.00125,
+                 tol: float = 1e-5, eps: float = 1e-12, sv_tol: float = 1e-8, max_iter: int = 100000,
+                 working_set: int = 1024, group=None, rank=None):
+        self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter)
+        self.world, self.transport, self.group, self.rank = world, transport, group, rank
+        self.working_set = int(working_set)
+
+    def fit(self, X: np.ndarray, y: np.ndarray) -> "DistributedDecompSVC":
+        from ..models.svc import SVC
+        from ..utils.data import MinMaxScaler
+        from .rccl import DeviceGroup
+
+        t0 = time.perf_counter()
+        if self.rank is not None:
+            out = rank_fit(self.rank, X, y, self.params, self.working_set)
+            dev = f"cuda:{self.rank.device}"
+        else:
+            g = self.group or DeviceGroup.shared(self.world, self.transport)
+            out = group_fit(g, X, y, self.params, self.working_set)
+            dev = "cuda:0"
+        a = out["alpha"]
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        sup = np.flatnonzero(a > self.params.sv_tol).astype(np.int64)
+        p = self.params
+        m = SVC(C=p.C, gamma=p.gamma, tol=p.tau, eps=p.eps, sv_tol=p.sv_tol, max_iter=p.max_iter, device=dev)
+        m.scaler_ = MinMaxScaler(out["mn"], out["mx"])
+        m.alpha_, m.support_ = a, sup
+        m.support_labels_ = y[sup].astype(np.int32)
+        m.dual_coef_ = a[sup] * y[sup]
+        m.b_, m.intercept_ = out["b"], -out["b"]
+        m.n_iter_, m.stop_reason_ = out["iterations"], out["stop_reason"]
+        m.support_vectors_ = m.scaler_.transform(np.asarray(X)[sup])
+        m._upload_model(dev)
+        self.model_ = m
+        self.alpha_, self.support_, self.b_ = a, sup, out["b"]
+        self.n_iter_, self.stop_reason_ = out["iterations"], out["stop_reason"]
+        self.stats_ = out["stats"]
+        self.rank_ms_ = out["rank_ms"]
+        self.timings_ = {"solve_ms": out["stats"]["solve_us"] / 1e3, "native_ms": out["wall_ms"],
+                         **out["stats"]}
+        self.fit_time_ = time.perf_counter() - t0
+        return self
+
+    def decision_function(self, X) -> np.ndarray:
+        return self.model_.decision_function(X)
+
+    def predict(self, X) -> np.ndarray:
+        return self.model_.predict(X)
+
+    def score(self, X, y) -> float:
+        return self.model_.score(X, y)

@@ -71,3 +71,41 @@ def test_decomp_refuses_what_it_does_not_cover():
         SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64) / 255.0, tr.y)
     with pytest.raises(ValueError, match="cold start"):
         SVC(device="cuda:0", solver="decomp").fit(tr.compact().X, tr.y, alpha0=np.zeros(tr.n))
+
+
+@pytest.mark.parametrize("n,world", [(6000, 2), (6000, 8), (20000, 4)])
+def test_distributed_rehearsal_equals_one_gpu(n, world):
+    """P ranks rehearsed on the one GPU (loopback transport, thread ranks): the global block partition
+    makes every working set, alpha, b and iteration count the one-GPU decomposition solver's."""
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.rccl import DeviceGroup
+
+    tr = synthetic_mnist(n, seed=91).compact()
+    one = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    g = DeviceGroup(world, "loopback")
+    try:
+        m = DistributedDecompSVC(world, group=g).fit(tr.X, tr.y)
+    finally:
+        g.close()
+    assert m.stop_reason_ == "converged"
+    assert m.n_iter_ == one.n_iter_ and m.b_ == one.b_
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
+    assert m.stats_["outer_iterations"] == one.timings_["outer_iterations"]
+    te = synthetic_mnist(500, seed=92).compact()
+    np.testing.assert_array_equal(m.predict(te.X), one.predict(te.X))
+
+
+def test_distributed_process_rank_world1_equals_one_gpu():
+    """The per-process entry (torchrun form, RCCL communicator of one rank) on the one GPU."""
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.rccl import RcclRank
+
+    tr = synthetic_mnist(4000, seed=93).compact()
+    one = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    rk = RcclRank(0, RcclRank.unique_id(), 1, 0)
+    try:
+        m = DistributedDecompSVC(rank=rk).fit(tr.X, tr.y)
+    finally:
+        rk.close()
+    assert m.n_iter_ == one.n_iter_ and m.b_ == one.b_
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
