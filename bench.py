@@ -60,9 +60,10 @@ def main(argv=None):
     ap.add_argument("--n", "--rows", dest="n", type=int, default=60000, help="training rows (MNIST-60k config)")
     ap.add_argument("--m", "--test-rows", dest="m", type=int, default=10000, help="test rows for the parity fields")
     ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--parallel", choices=["auto", "smo", "cascade"], default="auto",
+    ap.add_argument("--parallel", choices=["auto", "smo", "cascade", "decomp"], default="auto",
                     help="N > 1: one distributed SMO over the GPUs (smo), the reference's Cascade SVM (cascade), "
-                         "or smo with a fallback to the cascade when it does not apply (auto)")
+                         "smo or the cascade, whichever fit is measured faster (auto), or the opt-in distributed "
+                         "working-set decomposition solver (decomp; compared with the one-GPU decomposition solver)")
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
                     help="direct launch, N > 1: one GPU per rank (auto / rccl), or loopback = a rehearsal of N ranks "
@@ -99,12 +100,13 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per process under torchrun; with one process (--cascade) the same per-process path runs
     # on a single GPU, so a one-GPU box rehearses the launch the N-GPU run takes
-    multiproc = world_env > 1 or ("LOCAL_RANK" in os.environ and (a.cascade or a.parallel == "smo"))
+    multiproc = world_env > 1 or ("LOCAL_RANK" in os.environ and (a.cascade or a.parallel in ("smo", "decomp")))
     if multiproc and world_env != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
-    if a.solver == "decomp" and (a.gpus > 1 or a.cascade or a.parallel == "smo" or cpu or a.input != "u8"):
+    if a.solver == "decomp" and (a.gpus > 1 or a.cascade or a.parallel in ("smo", "decomp") or cpu
+                                 or a.input != "u8"):
         print("bench.py: --solver decomp is the one-GPU trainer on uint8 pixel rows", file=sys.stderr)
         return 2
     ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
@@ -125,7 +127,7 @@ def main(argv=None):
         torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
     sync = (lambda: torch.cuda.synchronize(dev)) if not cpu else (lambda: None)
-    distributed = a.gpus > 1 or a.cascade or a.parallel == "smo"
+    distributed = a.gpus > 1 or a.cascade or a.parallel in ("smo", "decomp")
     # A fresh process's first GPU operation (any: a copy, a PyTorch kernel, a context) pays a one-off
     # runtime/device initialisation (~85-115 ms, profiles/r3_first_op_probe.txt), whatever follows.
     # It is paid and timed here, outside the fits, so cold_fit_ms is the first fit's own cost.
@@ -162,8 +164,8 @@ def main(argv=None):
         if mode == "cascade":
             fallback_reason = ("not pixel rows" if not pixel else "cpu device" if cpu else "second-order selection"
                                if a.wss != "first" else "cascade requested" if a.cascade else "more than 8 GPUs")
-    elif mode == "smo" and (cpu or not pixel):
-        print("bench.py: --parallel smo needs uint8 pixel rows on GPUs", file=sys.stderr)
+    elif mode in ("smo", "decomp") and (cpu or not pixel):
+        print(f"bench.py: --parallel {mode} needs uint8 pixel rows on GPUs", file=sys.stderr)
         return 2
 
     def agree(ok: bool) -> bool:
@@ -211,6 +213,18 @@ def main(argv=None):
                     h.close()
             dgroup = drank = None
 
+    if mode == "decomp":
+        from svm355.parallel.decomp import DistributedDecompSVC
+
+        if multiproc:
+            from svm355.parallel.rccl import RcclRank
+
+            crank = RcclRank.from_torch_dist(dev_index, a.comm_timeout)
+        else:
+            from svm355.parallel.rccl import DeviceGroup
+
+            group = DeviceGroup(a.gpus, a.transport, a.comm_timeout)
+
     # auto with both applicable: the cascade is set up too and the faster measured fit runs (below)
     if mode == "cascade" or (auto and mode == "smo"):
         if multiproc and cpu:
@@ -242,6 +256,8 @@ def main(argv=None):
             model = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(full.X, full.y)
         elif mode == "smo":
             model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
+        elif mode == "decomp":
+            model = DistributedDecompSVC(a.gpus, group=group, rank=crank).fit(full.X, full.y)
         elif multiproc:
             model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit_rank(
                 crank, part.X, part.y, np.arange(lo, hi), a.n)
@@ -373,6 +389,19 @@ def main(argv=None):
                        "exact-integer quantisation and the Gram read the bytes on the device and only the support "
                        "vectors are widened to scaled fp64 (f64_input_fit_ms: the same fit from the reference's fp64 "
                        "host rows); the data are a synthetic MNIST-shaped draw, not MNIST"})
+    elif mode == "decomp":
+        extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
+                 "stop_reason": model.stop_reason_, "decomp_stats": model.stats_, "rank_ms": model.rank_ms_,
+                 "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
+                 "launch_form": ("one rank per process" if multiproc else "thread ranks, one GPU each")
+                 if a.transport != "loopback" else f"rehearsal: {a.gpus} ranks on one GPU",
+                 "note": "opt-in working-set decomposition solver over all GPUs: every GPU holds all rows and an "
+                         "alpha replica, owns 1/N of the selection blocks and of f, and all-gathers its candidate "
+                         "records once per outer iteration; the working-set solve is replicated.  Compared with "
+                         "the ONE-GPU DECOMPOSITION solver (single_gpu_s, bit_identical_to_1gpu), not the "
+                         "pairwise headline trainer"}
+        if rank == 0:
+            extra["accuracy"] = model.score(te.X, te.y)
     elif mode == "smo":
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
                  "stop_reason": model.stop_reason_, "timings_ms": model.timings_, "team_shape": model.shape_,
@@ -416,22 +445,23 @@ def main(argv=None):
             extra["speedup_vs_ref_cascade_same_P"] = round(ref / value, 2)
         if fallback_reason:
             extra["fallback_reason"] = fallback_reason
-    if mode in ("smo", "cascade") and a.baseline_1gpu > 0:  # the single-GPU trainer, same data, rank 0's GPU
+    if mode in ("smo", "cascade", "decomp") and a.baseline_1gpu > 0:  # the single-GPU trainer, rank 0's GPU
         if dist is not None:
             dist.barrier()
         if rank == 0:
-            one = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)  # warm
+            one_solver = "decomp" if mode == "decomp" else "smo"
+            one = SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)  # warm
             ts = []
             for _ in range(a.baseline_1gpu):
                 sync()
                 tb = time.perf_counter()
-                one = SVC(device=str(dev), wss=a.wss).fit(full.X, full.y)
+                one = SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)
                 sync()
                 ts.append(time.perf_counter() - tb)
             t1 = float(np.median(ts))
             extra["single_gpu_s"] = round(t1, 6)
             extra["speedup_vs_1gpu"] = round(t1 / value, 4)
-            if mode == "smo":
+            if mode in ("smo", "decomp"):
                 extra["bit_identical_to_1gpu"] = bool(one.n_iter_ == model.n_iter_ and one.b_ == model.b_ and
                                                       np.array_equal(one.alpha_, model.alpha_))
         if dist is not None:
@@ -450,6 +480,8 @@ def main(argv=None):
             parallelism = "single-gpu"
         elif mode == "smo":
             parallelism = f"distributed-smo-dp{a.gpus}"
+        elif mode == "decomp":
+            parallelism = f"distributed-decomp-dp{a.gpus}"
         else:
             parallelism = f"cascade-{a.topology}-dp{a.gpus}"
         line = {
@@ -466,7 +498,8 @@ def main(argv=None):
             "dtype": "fp64",
             "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
             "config": {
-                "model": (f"RBF SVM, {a.wss}-order SMO" if a.solver == "smo" else "RBF SVM, working-set decomposition SMO")
+                "model": (f"RBF SVM, {a.wss}-order SMO" if a.solver == "smo" and mode != "decomp"
+                          else "RBF SVM, working-set decomposition SMO")
                          + " (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,

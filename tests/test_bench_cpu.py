@@ -98,3 +98,8 @@ def test_bench_decomp_solver_is_one_gpu_only(capsys):
     assert bench.main(["--solver", "decomp", "--device", "cpu", "--rows", "600", "--steps", "1"]) == 2
     assert "one-GPU trainer" in capsys.readouterr().err
     assert bench.main(["--solver", "decomp", "--gpus", "2", "--transport", "loopback", "--rows", "600"]) == 2
+
+
+def test_bench_parallel_decomp_refuses_cpu(capsys):
+    assert bench.main(["--gpus", "2", "--device", "cpu", "--parallel", "decomp", "--rows", "600", "--steps", "1"]) == 2
+    assert "--parallel decomp needs uint8 pixel rows on GPUs" in capsys.readouterr().err
