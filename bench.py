@@ -8,10 +8,20 @@ One "step" is one complete training run on the fixed synthetic 60k x 784 MNIST-s
 domain because MNIST itself is not available offline):
 
 * N = 1: the single-GPU trainer (gpu_svm_main3.cu equivalent).  Timed scope = the reference's GPU
-  "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, RBF Gram, device
-  SMO to convergence.  Rows are held as uint8 (what MNIST is); the Gram is quantised straight from
-  the bytes, every value exact (``--input f64`` ships FP64 rows like the reference, same results).
-* N > 1, ``--parallel smo`` (the default for pixel data): ONE first-order SMO over the N GPUs
+  "training" scope (gpu_svm_main3.cu:525-616): H2D of X and y, min/max + scaling, the kernel values,
+  device SMO to convergence, SV extraction.  Rows are held as uint8 (what MNIST is) and quantised
+  straight from the bytes, every kernel value exact in FP64 (``--input f64`` ships FP64 rows like the
+  reference, same results).  ``--solver decomp`` (default): the SMO-type working-set decomposition
+  solver (csrc/hip/decomp.hip) -- the reference's stop test b_low <= b_high + 2 tau on all n points
+  and its clip / update arithmetic, reached through working sets of 1,024 points solved in one
+  workgroup; same support-vector set as the pairwise solve, b within the reference's own
+  serial-vs-GPU spread.  ``--solver smo``: the reference's pairwise first-order trajectory, bit for
+  bit the CPU oracle's (resident exact-integer Gram + persistent device SMO); the JSON line reports
+  the other solver's fit next to the headline either way.
+* N > 1, ``--parallel auto`` with the decomposition solver (the default): the distributed
+  decomposition solver (every GPU owns 1/N of the selection blocks and of f; one RCCL all-gather of
+  candidate records per outer iteration); bit-identical to the one-GPU decomposition solver.
+* N > 1, ``--parallel smo`` (``auto`` with ``--solver smo``): ONE first-order SMO over the N GPUs
   (csrc/hip/dsmo.hip): each GPU owns 1/N of the points and its slab K(:, own) of the exact-integer
   Gram, and the per-iteration arg-min / arg-max candidates cross the GPUs over xGMI -- the same
   problem, the same stop test and the same model as one GPU, bit for bit (strong scaling).
@@ -75,12 +85,13 @@ def main(argv=None):
                     help="N > 1: single-GPU fits timed after the run for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference; the headline) or the opt-in second-order")
-    ap.add_argument("--solver", choices=["smo", "decomp"], default="smo",
-                    help="N = 1: the reference's pairwise first-order SMO (the headline) or the opt-in working-set "
-                         "decomposition (SVC(solver='decomp'): same stop test on all n points, same SVs)")
-    ap.add_argument("--decomp-fits", type=int, default=3,
-                    help="N = 1, --solver smo: decomposition-solver fits timed after the run and reported next to the "
-                         "headline (0 = skip)")
+    ap.add_argument("--solver", choices=["decomp", "smo"], default=None,
+                    help="the working-set decomposition SMO (decomp; default on GPUs: same stop test on all n points, "
+                         "same SVs; N > 1: --parallel auto runs it distributed) or the reference's pairwise first-order "
+                         "trajectory (smo; the CPU oracle's, the default with --device cpu)")
+    ap.add_argument("--decomp-fits", "--other-solver-fits", dest="decomp_fits", type=int, default=3,
+                    help="N = 1: fits of the OTHER solver (pairwise when the headline is decomp, and vice versa) timed "
+                         "after the run and reported next to the headline (0 = skip)")
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N > 1: seconds any rank waits on an exchange before every rank aborts its communicator "
                          "(a fit takes well under a second; a dead peer must not hang the run)")
@@ -105,9 +116,11 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
-    if a.solver == "decomp" and (a.gpus > 1 or a.cascade or a.parallel in ("smo", "decomp") or cpu
-                                 or a.input != "u8"):
-        print("bench.py: --solver decomp is the one-GPU trainer on uint8 pixel rows", file=sys.stderr)
+    if a.solver is None:
+        a.solver = "smo" if cpu else "decomp"
+    if a.solver == "decomp" and (cpu or a.cascade or a.parallel in ("smo", "cascade")):
+        print("bench.py: --solver decomp runs on GPUs (N > 1: --parallel auto | decomp); the cascade and the "
+              "distributed pairwise SMO are --solver smo", file=sys.stderr)
         return 2
     ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
     if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
@@ -157,6 +170,8 @@ def main(argv=None):
     pixel = full.X.dtype == np.uint8 and full.X.dtype == part.X.dtype
 
     mode = "single" if not distributed else a.parallel
+    if mode == "auto" and a.solver == "decomp" and pixel:
+        mode = "decomp"  # the headline solver, distributed (bit-identical to its one-GPU trajectory)
     auto = mode == "auto"
     fallback_reason = None
     if mode == "auto":
@@ -351,55 +366,65 @@ def main(argv=None):
         f64_ms = []
         if a.f64_fits > 0 and not cpu and a.input == "u8":  # the reference's FP64 host rows, same model
             X64 = full.X.astype(np.float64)
-            m64 = SVC(device=str(dev), wss=a.wss).fit(X64, full.y)
+            m64 = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
             for _ in range(a.f64_fits):
                 sync()
                 tf = time.perf_counter()
-                m64 = SVC(device=str(dev), wss=a.wss).fit(X64, full.y)
+                m64 = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
                 sync()
                 f64_ms.append((time.perf_counter() - tf) * 1e3)
             extra["f64_input_fit_ms"] = round(float(np.median(f64_ms)), 3)
-            extra["f64_input_same_model"] = bool(m64.b_ == model.b_ and m64.n_iter_ == model.n_iter_)
-        if a.decomp_fits > 0 and a.solver == "smo" and not cpu and a.input == "u8":
-            # the opt-in decomposition solver on the same rows (outside the timed region): same stop test
-            # on all n points by a different pair sequence; same SV set expected, b within a few tau
-            dm = SVC(device=str(dev), solver="decomp").fit(full.X, full.y)
+            extra["f64_input_same_model"] = bool(m64.b_ == model.b_ and m64.n_iter_ == model.n_iter_ and
+                                                 np.array_equal(m64.alpha_, model.alpha_))
+        if a.decomp_fits > 0 and not cpu and a.input == "u8":
+            # the other solver on the same rows (outside the timed region): the same stop test on all n
+            # points by a different pair sequence; the same SV set expected, b within a few tau
+            other = "smo" if a.solver == "decomp" else "decomp"
+            dm = SVC(device=str(dev), solver=other).fit(full.X, full.y)
             d_ms = []
             for _ in range(a.decomp_fits):
                 sync()
                 tf = time.perf_counter()
-                dm = SVC(device=str(dev), solver="decomp").fit(full.X, full.y)
+                dm = SVC(device=str(dev), solver=other).fit(full.X, full.y)
                 sync()
                 d_ms.append((time.perf_counter() - tf) * 1e3)
-            extra["decomp_solver"] = {
-                "fit_ms": round(float(np.median(d_ms)), 3), "fit_ms_all": [round(x, 3) for x in d_ms],
-                "same_svs": bool(np.array_equal(dm.support_, model.support_)), "b": float(dm.b_),
-                "b_minus_headline_b": float(dm.b_ - model.b_), "iterations": int(dm.n_iter_),
-                "outer_iterations": dm.timings_["outer_iterations"], "working_set": dm.timings_["working_set"],
-                "accuracy": dm.score(te.X, te.y), "stop_reason": dm.stop_reason_}
+            rec = {"fit_ms": round(float(np.median(d_ms)), 3), "fit_ms_all": [round(x, 3) for x in d_ms],
+                   "same_svs": bool(np.array_equal(dm.support_, model.support_)), "b": float(dm.b_),
+                   "b_minus_headline_b": float(dm.b_ - model.b_), "iterations": int(dm.n_iter_),
+                   "accuracy": dm.score(te.X, te.y), "stop_reason": dm.stop_reason_}
+            if other == "decomp":
+                rec.update(outer_iterations=dm.timings_["outer_iterations"], working_set=dm.timings_["working_set"])
+                extra["decomp_solver"] = rec
+            else:
+                rec.update(timings_ms=dm.timings_, trajectory="the reference's pairwise first-order SMO, bit-identical "
+                                                              "to the CPU oracle (tests/test_gpu_kernels.py)")
+                extra["pairwise_solver"] = rec
         extra.update({
             "n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
             "accuracy": acc, "stop_reason": model.stop_reason_, "timings_ms": model.timings_,
             "prediction_ms_10k": round(pred_ms, 3), "ref_gpu_prediction_s": REF_GPU_PRED_S,
             "cold_fit_ms": warm_ms[0] if warm_ms else None, "warmup_fit_ms": warm_ms,
             "device_init_ms": device_init_ms, "solver": a.solver,
-            "caveats": "timed fits reuse the library's grow-only Gram buffer and device context, allocated by the "
+            "caveats": "timed fits reuse the library's grow-only device buffers and device context, allocated by the "
                        "first (cold) fit, whose time is cold_fit_ms (measured after the process's one-off device "
-                       "initialisation, device_init_ms, which its first GPU operation of any kind pays); host rows are uint8 pixels: min/max, the "
-                       "exact-integer quantisation and the Gram read the bytes on the device and only the support "
-                       "vectors are widened to scaled fp64 (f64_input_fit_ms: the same fit from the reference's fp64 "
-                       "host rows); the data are a synthetic MNIST-shaped draw, not MNIST"})
+                       "initialisation, device_init_ms, which its first GPU operation of any kind pays); host rows are "
+                       "uint8 pixels: min/max and the exact-integer quantisation read the bytes on the device and only "
+                       "the support vectors are widened to scaled fp64 (f64_input_fit_ms: the same fit from the "
+                       "reference's fp64 host rows); the data are a synthetic MNIST-shaped draw, not MNIST" +
+                       ("; solver = the SMO-type working-set decomposition: the reference's stop test on all n points "
+                        "and clip/update arithmetic, a different pair sequence than the reference's pairwise solve "
+                        "(pairwise_solver: that solve's fit, SV set and b on the same rows)"
+                        if a.solver == "decomp" else "")})
     elif mode == "decomp":
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
                  "stop_reason": model.stop_reason_, "decomp_stats": model.stats_, "rank_ms": model.rank_ms_,
                  "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
                  "launch_form": ("one rank per process" if multiproc else "thread ranks, one GPU each")
                  if a.transport != "loopback" else f"rehearsal: {a.gpus} ranks on one GPU",
-                 "note": "opt-in working-set decomposition solver over all GPUs: every GPU holds all rows and an "
+                 "note": "working-set decomposition solver over all GPUs: every GPU holds all rows and an "
                          "alpha replica, owns 1/N of the selection blocks and of f, and all-gathers its candidate "
                          "records once per outer iteration; the working-set solve is replicated.  Compared with "
-                         "the ONE-GPU DECOMPOSITION solver (single_gpu_s, bit_identical_to_1gpu), not the "
-                         "pairwise headline trainer"}
+                         "the one-GPU decomposition solver (single_gpu_s, bit_identical_to_1gpu)"}
         if rank == 0:
             extra["accuracy"] = model.score(te.X, te.y)
     elif mode == "smo":
@@ -499,7 +524,7 @@ def main(argv=None):
             "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
             "config": {
                 "model": (f"RBF SVM, {a.wss}-order SMO" if a.solver == "smo" and mode != "decomp"
-                          else "RBF SVM, working-set decomposition SMO")
+                          else "RBF SVM, SMO-type working-set decomposition (reference stop test on all n points)")
                          + " (C=10, gamma=0.00125, tau=1e-5), MNIST-60k one-vs-rest",
                 "global_batch": a.n,
                 "seq_len": 784,

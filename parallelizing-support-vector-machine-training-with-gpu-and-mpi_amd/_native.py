@@ -200,6 +200,9 @@ _HIP_SIGS = {
     "svmd_train_decomp_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, _P, _P, POINTER(SvmParams), c_int32,
                                        POINTER(SvmResult), POINTER(SvmdTiming), POINTER(c_int64),
                                        POINTER(c_int32)]),
+    "svmd_train_decomp_rows": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, _P, POINTER(SvmParams),
+                                         c_int32, POINTER(SvmResult), POINTER(SvmdTiming), POINTER(c_int64),
+                                         POINTER(c_int32)]),
     "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
     "svmd_cascade_group_decomp": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32, _P,
                                             POINTER(SvmResult), POINTER(c_int64), _P, _P]),

@@ -33,4 +33,9 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
                   const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
                   bool* used, double* prep_ms, int world = 1, int rank = 0, const DecompAllGather& allgather = {});
 
+// The same from min-max scaled FP64 rows on the device (X_d: n x ld), one GPU.
+int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
+                    const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
+                    int64_t* stats, bool* used, double* prep_ms);
+
 }  // namespace svm355

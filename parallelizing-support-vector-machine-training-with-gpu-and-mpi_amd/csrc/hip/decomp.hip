@@ -272,7 +272,13 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // Stops at W's own gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points
 // whose alpha changed are compacted in position order: cols[j] = their global ids, coef[j] =
 // (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
-template <int NT, int PER, bool PROF = false, bool W2 = false>
+//
+// PF (candidate-row prefetch): the winner of each fold is one of the NW per-wave candidates, so right
+// after reading them from LDS every thread issues the loads of its entries of ALL NW candidate rows
+// and folds while they are in flight; the winner's row is then picked by its slot.  The row's memory
+// round trip (an Infinity-Cache / HBM hit: K(W, W) was written by a GEMM on every XCD) overlaps the
+// fold instead of following it, at NW times the (latency-bound) load traffic.
+template <int NT, int PER, bool PROF = false, bool W2 = false, bool PF = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, int m,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
@@ -352,6 +358,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     // the same pairwise tree fold in every lane (value, then lowest position): log2(NW) dependent steps
     double fv[2][NW], fa[2][NW];
     uint32_t fi[2][NW];
+    int fq[2][NW];  // PF: the winner's candidate slot
 #pragma unroll
     for (int q = 0; q < NW; ++q)
 #pragma unroll
@@ -359,7 +366,38 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         fv[sd][q] = pv[par][sd][q];
         fa[sd][q] = pa[par][sd][q];
         fi[sd][q] = pi[par][sd][q];
+        fq[sd][q] = q;
       }
+    // PF: this thread's entries of every candidate's row (I_high; first order also I_low) and, first
+    // order, K(i_cand, j_cand) for every pair of candidates
+    double kch[PF ? NW : 1][PER], kcl[PF && !W2 ? NW : 1][PER], k12c[PF && !W2 ? NW : 1][PF && !W2 ? NW : 1];
+    if constexpr (PF) {
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int64_t r = fi[0][q] == kSentinel ? 0 : int64_t(fi[0][q]);
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          const int k = t + NT * e;
+          kch[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
+        }
+      }
+      if constexpr (!W2) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          const int64_t r = fi[1][q] == kSentinel ? 0 : int64_t(fi[1][q]);
+#pragma unroll
+          for (int e = 0; e < PER; ++e) {
+            const int k = t + NT * e;
+            kcl[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
+          }
+#pragma unroll
+          for (int q2 = 0; q2 < NW; ++q2) {
+            const int64_t r2 = fi[0][q2] == kSentinel ? 0 : int64_t(fi[0][q2]);
+            k12c[q2][q] = Kw[r2 * ldw + r];
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int st = 1; st < NW; st <<= 1)
 #pragma unroll
@@ -369,12 +407,15 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         fv[0][q] = th ? fv[0][q + st] : fv[0][q];
         fa[0][q] = th ? fa[0][q + st] : fa[0][q];
         fi[0][q] = th ? fi[0][q + st] : fi[0][q];
+        fq[0][q] = th ? fq[0][q + st] : fq[0][q];
         fv[1][q] = tl ? fv[1][q + st] : fv[1][q];
         fa[1][q] = tl ? fa[1][q + st] : fa[1][q];
         fi[1][q] = tl ? fi[1][q + st] : fi[1][q];
+        fq[1][q] = tl ? fq[1][q + st] : fq[1][q];
       }
     double bh = fv[0][0], bl = fv[1][0], ah = fa[0][0], al = fa[1][0];
     uint32_t uih = fi[0][0], uil = fi[1][0];
+    const int qh = fq[0][0], ql = fq[1][0];
     stamp(2);
     if (uih == kSentinel || uil == kSentinel) {
       reason = SVM_STOP_NO_CANDIDATE;
@@ -388,7 +429,24 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     int ih = int(uih), il = int(uil);
     double K12, bl_upd = bl;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
-    if constexpr (!W2) {
+    // PF: the winners' rows from the candidate loads (slot qh / ql)
+    auto pick = [&](const double (&kc)[PF ? NW : 1][PER], int qw, double (&kr)[PER]) {
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        kr[e] = kc[0][e];
+#pragma unroll
+        for (int q = 1; q < (PF ? NW : 1); ++q) kr[e] = qw == q ? kc[q][e] : kr[e];
+      }
+    };
+    if constexpr (!W2 && PF) {
+      pick(kch, qh, kh);
+      pick(kcl, ql, kl);
+      K12 = k12c[0][0];
+#pragma unroll
+      for (int q2 = 0; q2 < NW; ++q2)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) K12 = (qh == q2 && ql == q) ? k12c[q2][q] : K12;
+    } else if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
       K12 = Kw[int64_t(ih) * ldw + il];
 #pragma unroll
@@ -402,10 +460,14 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       // the maximum of (f_t - b_high)^2 / a_t over I_low points above b_high (a_t = 2 - 2 K(i, t),
       // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
       // and fold, then row j
+      if constexpr (PF) {
+        pick(kch, qh, kh);
+      } else {
 #pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int k = t + NT * e;
-        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+        for (int e = 0; e < PER; ++e) {
+          const int k = t + NT * e;
+          kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+        }
       }
       double gv = inf, ga = 0.0, gf = 0.0, gk = 0.0;
       uint32_t gi = kSentinel;
@@ -434,8 +496,22 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         qk[par][w] = wk;
       }
       __syncthreads();
+      double kcj[PF ? NW : 1][PER];  // PF: this thread's entries of every candidate j's row
+      if constexpr (PF) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          const uint32_t c = qi[par][q];
+          const int64_t r = c == kSentinel ? 0 : int64_t(c);
+#pragma unroll
+          for (int e = 0; e < PER; ++e) {
+            const int k = t + NT * e;
+            kcj[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
+          }
+        }
+      }
       double cv = qv[par][0];
       uint32_t ci = qi[par][0];
+      int cq = 0;
       al = qa[par][0];
       bl_upd = qf[par][0];
       K12 = qk[par][0];
@@ -446,6 +522,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         const bool tk = v < cv || (v == cv && i2 < ci);
         cv = tk ? v : cv;
         ci = tk ? i2 : ci;
+        cq = tk ? q : cq;
         al = tk ? qa[par][q] : al;
         bl_upd = tk ? qf[par][q] : bl_upd;
         K12 = tk ? qk[par][q] : K12;
@@ -455,10 +532,14 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         break;
       }
       il = int(ci);
+      if constexpr (PF) {
+        pick(kcj, cq, kl);
+      } else {
 #pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int k = t + NT * e;
-        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+        for (int e = 0; e < PER; ++e) {
+          const int k = t + NT * e;
+          kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+        }
       }
     }
     const int32_t yh = sy[ih], yl = sy[il];
@@ -619,6 +700,9 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
   // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
   const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
+  // candidate-row prefetch in the inner solve (256-thread workgroup): SVM355_DECOMP_PF = 0 | 1
+  bool prefetch = true;
+  if (const char* v = getenv("SVM355_DECOMP_PF")) prefetch = atoi(v) != 0;
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -699,9 +783,10 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     if (rc) return rc;
     const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
     const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
-#define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, p.C, \
-                     p.eps, tau_in, max_inner, cols, coef, mcount, hs)
+#define SVM_WS_INNER_P(NT, PER, PR, S2, PFX)                                                                     \
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, PFX>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, \
+                     p.C, p.eps, tau_in, max_inner, cols, coef, mcount, hs)
+#define SVM_WS_INNER_(NT, PER, PR, S2) SVM_WS_INNER_P(NT, PER, PR, S2, false)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
     SVM_WS_INNER_(NT, PER, true, true);      \
@@ -711,7 +796,16 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     SVM_WS_INNER_(NT, PER, false, true);     \
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
-    if (inner_nt == 64)
+    if (inner_nt == 256 && prefetch) {
+      if (prof && inner_wss2)
+        SVM_WS_INNER_P(256, 4, true, true, true);
+      else if (prof)
+        SVM_WS_INNER_P(256, 4, true, false, true);
+      else if (inner_wss2)
+        SVM_WS_INNER_P(256, 4, false, true, true);
+      else
+        SVM_WS_INNER_P(256, 4, false, false, true);
+    } else if (inner_nt == 64)
       SVM_WS_INNER(64, 16);
     else if (inner_nt == 128)
       SVM_WS_INNER(128, 8);
@@ -723,6 +817,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
       SVM_WS_INNER(1024, 1);
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
+#undef SVM_WS_INNER_P
     SVMD_LAUNCH_CHECK();
     if (nloc > 0) {
       rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
@@ -762,42 +857,13 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   return SVM_OK;
 }
 
-int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
-                  const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
-                  bool* used, double* prep_ms, int world, int rank, const DecompAllGather& allgather) {
-  const auto t0 = std::chrono::steady_clock::now();
-  *used = false;
-  QuantPlan P;
-  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;  // igram's LDS table bound
-  // quantised rows live in the context's grow-only buffer (the solver's workspace is ctx->ws)
-  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  const size_t need = al(size_t(n) * P.kq) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
-                      al(quantize_u8_aux_bytes(P));
-  if (need > ctx->gram_bytes) {
-    if (ctx->gram) {
-      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
-      SVMD_CHECK(hipFree(ctx->gram));
-      ctx->gram = nullptr;
-      ctx->gram_bytes = 0;
-    }
-    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
-    ctx->gram_bytes = need;
-  }
-  char* base = reinterpret_cast<char*>(ctx->gram);
-  auto* Q = reinterpret_cast<int8_t*>(base);
-  auto* N0 = reinterpret_cast<int32_t*>(base + al(size_t(n) * P.kq));
-  auto* WN = reinterpret_cast<double*>(reinterpret_cast<char*>(N0) + al(size_t(n) * 4));
-  auto* stw = reinterpret_cast<double*>(reinterpret_cast<char*>(WN) + al(size_t(n) * 8));
-  void* aux = reinterpret_cast<char*>(stw) + al(P.step_w.size() * 8);
-  bool ok = false;
-  {
-    TraceRange tr("svm355:quantise");
-    const int rc = quantize_u8_rows(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
-    if (rc) return rc;
-  }
-  if (!ok) return SVM_OK;
+namespace {
+
+// The solve after quantisation: step weights to the device, the decomposition, the SV count.
+int decomp_after_quant(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, double* stw,
+                       const QuantPlan& P, const int32_t* y_d, double* alpha_d, int64_t n, const svm_params& p, int q,
+                       svm_result* r, int64_t* stats, int world, int rank, const DecompAllGather& allgather) {
   SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-  if (prep_ms) *prep_ms = ms_since(t0);
   {
     TraceRange ts("svm355:decomp");
     const int rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, world, rank,
@@ -810,6 +876,90 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
     if (rc) return rc;
     r->n_sv = c;
   }
+  return SVM_OK;
+}
+
+// The context's grow-only buffer holds the quantised rows (the solver's workspace is ctx->ws):
+// Q (n x kq), N0, WN, the step weights and the quantiser's column tables (aux_bytes).
+int decomp_quant_buffers(DeviceCtx* ctx, int64_t n, const QuantPlan& P, size_t aux_bytes, int8_t** Q, int32_t** N0,
+                         double** WN, double** stw, void** aux) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t need = al(size_t(n) * P.kq) + al(size_t(n) * 4) + al(size_t(n) * 8) + al(P.step_w.size() * 8) +
+                      al(aux_bytes);
+  if (need > ctx->gram_bytes) {
+    if (ctx->gram) {
+      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+      SVMD_CHECK(hipFree(ctx->gram));
+      ctx->gram = nullptr;
+      ctx->gram_bytes = 0;
+    }
+    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
+    ctx->gram_bytes = need;
+  }
+  char* base = reinterpret_cast<char*>(ctx->gram);
+  *Q = reinterpret_cast<int8_t*>(base);
+  *N0 = reinterpret_cast<int32_t*>(base + al(size_t(n) * P.kq));
+  *WN = reinterpret_cast<double*>(reinterpret_cast<char*>(*N0) + al(size_t(n) * 4));
+  *stw = reinterpret_cast<double*>(reinterpret_cast<char*>(*WN) + al(size_t(n) * 8));
+  *aux = reinterpret_cast<char*>(*stw) + al(P.step_w.size() * 8);
+  return SVM_OK;
+}
+
+}  // namespace
+
+// The same solve from scaled FP64 rows (X_d: n x ld, the reference's host format, already min-max
+// scaled on the device with mn_h / mx_h): quantize_rows produces the same Q, N0, WN as the uint8
+// path, so the trajectory and the model are the uint8 path's.
+int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
+                    const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
+                    int64_t* stats, bool* used, double* prep_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  *used = false;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;
+  int8_t* Q;
+  int32_t* N0;
+  double *WN, *stw;
+  void* aux;
+  int rc = decomp_quant_buffers(ctx, n, P, quantize_aux_bytes(P), &Q, &N0, &WN, &stw, &aux);
+  if (rc) return rc;
+  bool ok = false;
+  {
+    TraceRange tr("svm355:quantise");
+    rc = quantize_rows(ctx->stream, X_d, n, ld, P, aux, Q, N0, WN, &ok);
+    if (rc) return rc;
+  }
+  if (!ok) return SVM_OK;
+  if (prep_ms) *prep_ms = ms_since(t0);
+  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, 1, 0, {});
+  if (rc) return rc;
+  *used = true;
+  return SVM_OK;
+}
+
+int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
+                  const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
+                  bool* used, double* prep_ms, int world, int rank, const DecompAllGather& allgather) {
+  const auto t0 = std::chrono::steady_clock::now();
+  *used = false;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;  // igram's LDS table bound
+  int8_t* Q;
+  int32_t* N0;
+  double *WN, *stw;
+  void* aux;
+  int rc = decomp_quant_buffers(ctx, n, P, quantize_u8_aux_bytes(P), &Q, &N0, &WN, &stw, &aux);
+  if (rc) return rc;
+  bool ok = false;
+  {
+    TraceRange tr("svm355:quantise");
+    rc = quantize_u8_rows(ctx->stream, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
+    if (rc) return rc;
+  }
+  if (!ok) return SVM_OK;
+  if (prep_ms) *prep_ms = ms_since(t0);
+  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, world, rank, allgather);
+  if (rc) return rc;
   *used = true;
   return SVM_OK;
 }
@@ -846,6 +996,39 @@ SVM_API int svmd_train_decomp_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_
   if (rc) return rc;
   if (used && timing) {
     timing->gram_ms = prep;  // quantisation only: no Gram is stored
+    timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    timing->smo_ms = timing->total_ms - prep;
+  }
+  if (used_out) *used_out = used ? 1 : 0;
+  return ctx->end();
+}
+
+// The same solve from min-max scaled FP64 rows on the device (X_d: n x ld; mn_h / mx_h the training
+// statistics they were scaled with): quantised into the same integers as the uint8 path, so the
+// trajectory and the model are identical.  *used = 0 when the values admit no exact-integer plan.
+SVM_API int svmd_train_decomp_rows(void* h, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
+                                   const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params* pp,
+                                   int32_t q, svm_result* r, svmd_timing* timing, int64_t* stats, int32_t* used_out) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!X_d || n < 2 || d <= 0 || ld < d || !mn_h || !mx_h || !y_d || !alpha_d) {
+    set_error("svmd_train_decomp_rows: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ctx->begin();
+  if (rc) return rc;
+  bool used = false;
+  double prep = 0.0;
+  rc = decomp_fit_rows(ctx, X_d, n, ld, d, mn_h, mx_h, y_d, alpha_d, p, q, r, stats, &used, &prep);
+  if (rc) return rc;
+  if (used && timing) {
+    timing->gram_ms = prep;
     timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     timing->smo_ms = timing->total_ms - prep;
   }

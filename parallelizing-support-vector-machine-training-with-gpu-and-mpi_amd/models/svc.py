@@ -61,8 +61,8 @@ class SVC:
         self._dev = None  # device-side model state (torch tensors)
         # "smo": the reference's solver (one pair per iteration over all n points, resident Gram or row
         # cache).  "decomp": working sets of up to `working_set` points solved in one workgroup with
-        # the same stop test on all n points (decomp.hip; GPU, uint8 pixel rows, cold start) -- the
-        # same support vectors, b within the stop tolerance, a different pair sequence.
+        # the same stop test on all n points (decomp.hip; GPU, pixel rows as uint8 or FP64, cold start)
+        # -- the same support vectors, b within the stop tolerance, a different pair sequence.
         self.solver = solver
         self.working_set = int(working_set)
 
@@ -117,12 +117,16 @@ class SVC:
         from ..ops import device as D
 
         device = torch.device(dev)
-        if self.solver == "decomp":
-            if X.dtype != np.uint8 or not self.scale or alpha0 is not None:
-                raise ValueError("solver='decomp' needs uint8 pixel rows, scale=True and a cold start")
-            if not self._fit_cuda_u8(X, y, None, device):
-                raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
-            return
+        decomp = self.solver == "decomp"
+        if decomp:
+            if not self.scale or alpha0 is not None:
+                raise ValueError("solver='decomp' needs scale=True and a cold start")
+            if X.dtype == np.uint8:
+                if not self._fit_cuda_u8(X, y, None, device):
+                    raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
+                return
+            # FP64 host rows (the reference's format): scaled on the device, then quantised into the
+            # same integers as the byte path -- the same trajectory and model
         if (X.dtype == np.uint8 and self.scale and self.gram in ("auto", "int") and self.kcache in ("auto", "full")
                 and os.environ.get("SVM355_U8_TRAIN", "1") != "0" and self._fit_cuda_u8(X, y, alpha0, device)):
             return
@@ -141,8 +145,14 @@ class SVC:
             alpha = torch.empty(X.shape[0], dtype=torch.float64, device=device)  # the cold start zeroes it
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
-        res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
-                          kcache=self.kcache)
+        if decomp:
+            out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set)
+            if out is None:
+                raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
+            res, tm = out
+        else:
+            res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
+                              kcache=self.kcache)
         a = alpha.cpu().numpy()
         self._finish(a, y, res)
         idx = torch.from_numpy(self.support_).to(device)

@@ -426,6 +426,31 @@ def train_decomp_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, para
                                       "update_columns": int(st[4]), "inner_threads": int(st[5])}
 
 
+def train_decomp_rows(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn: torch.Tensor,
+                      mx: torch.Tensor, working_set: int = 1024) -> Optional[Tuple[SMOResult, dict]]:
+    """train_decomp_u8 from min-max scaled FP64 rows on the device (the reference's host row format;
+    svmd_train_decomp_rows): the rows quantise into the same integers, so the trajectory and the model
+    are the uint8 path's.  None when the values admit no exact-integer plan."""
+    _check_rows(X)
+    n, ld = X.shape
+    d = int(mn.numel())
+    ctx = _ctx_for(X)
+    a, b, _ = _host_stats(mn, mx)
+    r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
+    st = (ctypes.c_int64 * 6)()
+    p = params.to_struct()
+    N.check(ctx.lib.svmd_train_decomp_rows(ctx.bind(), N.ptr(X), n, ld, d, N.ptr(a), N.ptr(b), N.ptr(y), N.ptr(alpha),
+                                           ctypes.byref(p), int(working_set), ctypes.byref(r), ctypes.byref(tm), st,
+                                           ctypes.byref(used)), "svmd_train_decomp_rows")
+    if not used.value:
+        return None
+    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
+                                      "kcache": "none", "gram_path": "int8-exact", "rows": "fp64",
+                                      "solver": "decomp", "outer_iterations": int(st[0]),
+                                      "inner_iterations": int(st[1]), "working_set": int(st[2]),
+                                      "update_columns": int(st[4]), "inner_threads": int(st[5])}
+
+
 def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Exact-integer RBF Gram straight from device uint8 rows (equal to ``rbf_gram_sym`` on the scaled
     FP64 rows); None when the integer plan does not apply."""

@@ -65,10 +65,24 @@ def test_decomp_at_the_headline_shape():
     assert m.timings_["outer_iterations"] < 500
 
 
+def test_decomp_fp64_rows_equal_the_byte_path():
+    """FP64 host rows (the reference's format) are scaled on the device and quantised into the same
+    integers as the uint8 rows: the same trajectory, alphas, b and predictions."""
+    tr = synthetic_mnist(6000, seed=79).compact()
+    a = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    b = SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64), tr.y)
+    assert b.timings_["rows"] == "fp64" and a.timings_["rows"] == "uint8"
+    assert a.n_iter_ == b.n_iter_ and a.b_ == b.b_
+    np.testing.assert_array_equal(a.alpha_, b.alpha_)
+    te = synthetic_mnist(500, seed=80).compact()
+    np.testing.assert_array_equal(a.predict(te.X), b.predict(te.X.astype(np.float64)))
+
+
 def test_decomp_refuses_what_it_does_not_cover():
     tr = synthetic_mnist(500, seed=3)
-    with pytest.raises(ValueError, match="uint8"):
-        SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64) / 255.0, tr.y)
+    rng = np.random.default_rng(5)
+    with pytest.raises(ValueError, match="integer pixel rows"):
+        SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64) + rng.random(tr.X.shape) * 0.5, tr.y)
     with pytest.raises(ValueError, match="cold start"):
         SVC(device="cuda:0", solver="decomp").fit(tr.compact().X, tr.y, alpha0=np.zeros(tr.n))
 
