@@ -227,6 +227,15 @@ class Transport {
     gather(send, bytes, recv, 0);
     bcast(recv, bytes * world(), 0);
   }
+  // The all-gather enqueued on the rank's stream without waiting for it; the caller then waits
+  // with stream_wait.  Transports that exchange through the host complete it here.
+  virtual void allgather_async(const void* send, int64_t bytes, void* recv) { allgather(send, bytes, recv); }
+  // Wait for the rank's stream under the transport's deadline / abort policy.  false: this transport
+  // has no stream of its own to poll (the caller synchronises its stream itself).
+  virtual bool stream_wait(const char* what) {
+    (void)what;
+    return false;
+  }
   virtual void send_i64(int64_t v, int peer) = 0;
   virtual int64_t recv_i64(int peer) = 0;
   virtual void send(const void* buf, int64_t bytes, int peer) = 0;

@@ -624,6 +624,13 @@ class RcclTransport final : public Transport {
     NCCLT(ncclAllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
     wait("ncclAllGather");
   }
+  void allgather_async(const void* send, int64_t bytes, void* recv) override {
+    if (bytes > 0) NCCLT(ncclAllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
+  }
+  bool stream_wait(const char* what) override {
+    wait(what);
+    return true;
+  }
   void send_i64(int64_t v, int peer) override {
     pinned_[2] = v;
     HIPT(hipMemcpyAsync(scratch_ + 2, pinned_ + 2, 8, hipMemcpyHostToDevice, stream_));
@@ -813,8 +820,12 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   be.d2h(mmh.data(), mm, 2 * d * 8);
   if (mm_out) std::memcpy(mm_out, mmh.data(), size_t(2 * d) * 8);
   const int world = tr ? tr->world() : 1, rank = tr ? tr->rank() : 0;
+  // RCCL: the all-gather is only enqueued; the solver's one host wait per outer iteration (after the
+  // working-set build that reads the gathered candidates) polls under the transport's deadline
   DecompAllGather ag;
-  if (tr) ag = [tr](const void* send, int64_t bytes, void* recv) { tr->allgather(send, bytes, recv); };
+  if (tr)
+    ag = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
+          [tr]() { return tr->stream_wait("decomposition SMO: candidate all-gather + working-set build"); }};
   bool used = false;
   double prep = 0.0;
   svm_result res{};

@@ -19,8 +19,13 @@ struct DecompShape {
 DecompShape decomp_shape(int64_t n, int qws, int world);
 
 // All-gather of `bytes` from every GPU into recv (world * bytes, GPU-major), ordered on the solver's
-// stream (the distributed solve's one exchange per outer iteration).
-using DecompAllGather = std::function<void(const void* send, int64_t bytes, void* recv)>;
+// stream (the distributed solve's one exchange per outer iteration), and optionally the wait for that
+// stream (true: waited; false / empty: the solver synchronises the stream itself).
+struct DecompAllGather {
+  std::function<void(const void* send, int64_t bytes, void* recv)> gather;
+  std::function<bool()> wait;
+  explicit operator bool() const { return bool(gather); }
+};
 
 int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,

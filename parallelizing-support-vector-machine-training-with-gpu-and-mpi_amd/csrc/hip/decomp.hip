@@ -747,11 +747,11 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
       hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per, T,
                          p.C, p.eps, cown, cown + NBr * T);
     SVMD_LAUNCH_CHECK();
-    if (world > 1) allgather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
+    if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
     hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
                        W, Wf, hs);
     SVMD_LAUNCH_CHECK();
-    SVMD_CHECK(hipStreamSynchronize(s));
+    if (!(world > 1 && allgather.wait && allgather.wait())) SVMD_CHECK(hipStreamSynchronize(s));
     if (outer > 0) {  // the previous outer iteration's inner solve
       inner_total += hs->inner_it;
       changed_total += hs->changed;
