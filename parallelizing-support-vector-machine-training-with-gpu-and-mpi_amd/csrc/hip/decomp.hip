@@ -43,7 +43,9 @@ struct DecompHost {  // pinned: written by the kernels, read by the host once pe
   int32_t m, stop;
   int64_t inner_it;
   int32_t inner_reason, changed;  // changed: points whose alpha the inner solve moved
-  int64_t prof[8];  // PROF builds: clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall ticks
+  int64_t prof[12];  // PROF builds: clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall
+                     // ticks; [8..11] the second-order j phase split (row i, gains + wave reduction, publish +
+                     // barrier, fold)
 };
 
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
@@ -272,13 +274,7 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // Stops at W's own gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points
 // whose alpha changed are compacted in position order: cols[j] = their global ids, coef[j] =
 // (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
-//
-// PF (candidate-row prefetch): the winner of each fold is one of the NW per-wave candidates, so right
-// after reading them from LDS every thread issues the loads of its entries of ALL NW candidate rows
-// and folds while they are in flight; the winner's row is then picked by its slot.  The row's memory
-// round trip (an Infinity-Cache / HBM hit: K(W, W) was written by a GEMM on every XCD) overlaps the
-// fold instead of following it, at NW times the (latency-bound) load traffic.
-template <int NT, int PER, bool PROF = false, bool W2 = false, bool PF = false>
+template <int NT, int PER, bool PROF = false, bool W2 = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, int m,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
@@ -314,7 +310,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   int64_t it = 0;
   int32_t reason = SVM_STOP_CONVERGED;
   // PROF: wave 0's clock at the phase boundaries (select | publish+barrier | merge | row loads | update)
-  int64_t pacc[6] = {0, 0, 0, 0, 0, 0};
+  int64_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t pt = PROF ? int64_t(clock64()) : 0;
   const int64_t pc0 = pt, pw0 = PROF ? int64_t(wall_clock64()) : 0;
   auto stamp = [&](int k) {
@@ -358,7 +354,6 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     // the same pairwise tree fold in every lane (value, then lowest position): log2(NW) dependent steps
     double fv[2][NW], fa[2][NW];
     uint32_t fi[2][NW];
-    int fq[2][NW];  // PF: the winner's candidate slot
 #pragma unroll
     for (int q = 0; q < NW; ++q)
 #pragma unroll
@@ -366,38 +361,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         fv[sd][q] = pv[par][sd][q];
         fa[sd][q] = pa[par][sd][q];
         fi[sd][q] = pi[par][sd][q];
-        fq[sd][q] = q;
       }
-    // PF: this thread's entries of every candidate's row (I_high; first order also I_low) and, first
-    // order, K(i_cand, j_cand) for every pair of candidates
-    double kch[PF ? NW : 1][PER], kcl[PF && !W2 ? NW : 1][PER], k12c[PF && !W2 ? NW : 1][PF && !W2 ? NW : 1];
-    if constexpr (PF) {
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int64_t r = fi[0][q] == kSentinel ? 0 : int64_t(fi[0][q]);
-#pragma unroll
-        for (int e = 0; e < PER; ++e) {
-          const int k = t + NT * e;
-          kch[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
-        }
-      }
-      if constexpr (!W2) {
-#pragma unroll
-        for (int q = 0; q < NW; ++q) {
-          const int64_t r = fi[1][q] == kSentinel ? 0 : int64_t(fi[1][q]);
-#pragma unroll
-          for (int e = 0; e < PER; ++e) {
-            const int k = t + NT * e;
-            kcl[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
-          }
-#pragma unroll
-          for (int q2 = 0; q2 < NW; ++q2) {
-            const int64_t r2 = fi[0][q2] == kSentinel ? 0 : int64_t(fi[0][q2]);
-            k12c[q2][q] = Kw[r2 * ldw + r];
-          }
-        }
-      }
-    }
 #pragma unroll
     for (int st = 1; st < NW; st <<= 1)
 #pragma unroll
@@ -407,15 +371,12 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         fv[0][q] = th ? fv[0][q + st] : fv[0][q];
         fa[0][q] = th ? fa[0][q + st] : fa[0][q];
         fi[0][q] = th ? fi[0][q + st] : fi[0][q];
-        fq[0][q] = th ? fq[0][q + st] : fq[0][q];
         fv[1][q] = tl ? fv[1][q + st] : fv[1][q];
         fa[1][q] = tl ? fa[1][q + st] : fa[1][q];
         fi[1][q] = tl ? fi[1][q + st] : fi[1][q];
-        fq[1][q] = tl ? fq[1][q + st] : fq[1][q];
       }
     double bh = fv[0][0], bl = fv[1][0], ah = fa[0][0], al = fa[1][0];
     uint32_t uih = fi[0][0], uil = fi[1][0];
-    const int qh = fq[0][0], ql = fq[1][0];
     stamp(2);
     if (uih == kSentinel || uil == kSentinel) {
       reason = SVM_STOP_NO_CANDIDATE;
@@ -429,24 +390,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     int ih = int(uih), il = int(uil);
     double K12, bl_upd = bl;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
-    // PF: the winners' rows from the candidate loads (slot qh / ql)
-    auto pick = [&](const double (&kc)[PF ? NW : 1][PER], int qw, double (&kr)[PER]) {
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        kr[e] = kc[0][e];
-#pragma unroll
-        for (int q = 1; q < (PF ? NW : 1); ++q) kr[e] = qw == q ? kc[q][e] : kr[e];
-      }
-    };
-    if constexpr (!W2 && PF) {
-      pick(kch, qh, kh);
-      pick(kcl, ql, kl);
-      K12 = k12c[0][0];
-#pragma unroll
-      for (int q2 = 0; q2 < NW; ++q2)
-#pragma unroll
-        for (int q = 0; q < NW; ++q) K12 = (qh == q2 && ql == q) ? k12c[q2][q] : K12;
-    } else if constexpr (!W2) {
+    if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
       K12 = Kw[int64_t(ih) * ldw + il];
 #pragma unroll
@@ -460,14 +404,14 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       // the maximum of (f_t - b_high)^2 / a_t over I_low points above b_high (a_t = 2 - 2 K(i, t),
       // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
       // and fold, then row j
-      if constexpr (PF) {
-        pick(kch, qh, kh);
-      } else {
 #pragma unroll
-        for (int e = 0; e < PER; ++e) {
-          const int k = t + NT * e;
-          kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
-        }
+      for (int e = 0; e < PER; ++e) {
+        const int k = t + NT * e;
+        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+      }
+      if constexpr (PROF) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(8);
       }
       double gv = inf, ga = 0.0, gf = 0.0, gk = 0.0;
       uint32_t gi = kSentinel;
@@ -488,6 +432,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       }
       const VIL wc = wave_arg<true>(VI{gv, gi});
       const double wa = read_lane64(ga, wc.lane), wf = read_lane64(gf, wc.lane), wk = read_lane64(gk, wc.lane);
+      stamp(9);
       if (lane == 0) {
         qv[par][w] = wc.v;
         qi[par][w] = wc.i;
@@ -496,22 +441,9 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         qk[par][w] = wk;
       }
       __syncthreads();
-      double kcj[PF ? NW : 1][PER];  // PF: this thread's entries of every candidate j's row
-      if constexpr (PF) {
-#pragma unroll
-        for (int q = 0; q < NW; ++q) {
-          const uint32_t c = qi[par][q];
-          const int64_t r = c == kSentinel ? 0 : int64_t(c);
-#pragma unroll
-          for (int e = 0; e < PER; ++e) {
-            const int k = t + NT * e;
-            kcj[q][e] = k < m ? Kw[r * ldw + k] : 0.0;
-          }
-        }
-      }
+      stamp(10);
       double cv = qv[par][0];
       uint32_t ci = qi[par][0];
-      int cq = 0;
       al = qa[par][0];
       bl_upd = qf[par][0];
       K12 = qk[par][0];
@@ -522,7 +454,6 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         const bool tk = v < cv || (v == cv && i2 < ci);
         cv = tk ? v : cv;
         ci = tk ? i2 : ci;
-        cq = tk ? q : cq;
         al = tk ? qa[par][q] : al;
         bl_upd = tk ? qf[par][q] : bl_upd;
         K12 = tk ? qk[par][q] : K12;
@@ -532,14 +463,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         break;
       }
       il = int(ci);
-      if constexpr (PF) {
-        pick(kcj, cq, kl);
-      } else {
+      stamp(11);
 #pragma unroll
-        for (int e = 0; e < PER; ++e) {
-          const int k = t + NT * e;
-          kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
-        }
+      for (int e = 0; e < PER; ++e) {
+        const int k = t + NT * e;
+        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
       }
     }
     const int32_t yh = sy[ih], yl = sy[il];
@@ -607,6 +535,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   }
   if (PROF && t == 0) {
     for (int k = 0; k < 5; ++k) hs->prof[k] += pacc[k];
+    for (int k = 8; k < 12; ++k) hs->prof[k] += pacc[k];
     hs->prof[6] += int64_t(clock64()) - pc0;
     hs->prof[7] += int64_t(wall_clock64()) - pw0;
   }
@@ -700,9 +629,6 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
   // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
   const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
-  // candidate-row prefetch in the inner solve (256-thread workgroup): SVM355_DECOMP_PF = 0 | 1
-  bool prefetch = true;
-  if (const char* v = getenv("SVM355_DECOMP_PF")) prefetch = atoi(v) != 0;
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -783,10 +709,9 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     if (rc) return rc;
     const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
     const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
-#define SVM_WS_INNER_P(NT, PER, PR, S2, PFX)                                                                     \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, PFX>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, \
-                     p.C, p.eps, tau_in, max_inner, cols, coef, mcount, hs)
-#define SVM_WS_INNER_(NT, PER, PR, S2) SVM_WS_INNER_P(NT, PER, PR, S2, false)
+#define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, p.C, \
+                     p.eps, tau_in, max_inner, cols, coef, mcount, hs)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
     SVM_WS_INNER_(NT, PER, true, true);      \
@@ -796,16 +721,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     SVM_WS_INNER_(NT, PER, false, true);     \
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
-    if (inner_nt == 256 && prefetch) {
-      if (prof && inner_wss2)
-        SVM_WS_INNER_P(256, 4, true, true, true);
-      else if (prof)
-        SVM_WS_INNER_P(256, 4, true, false, true);
-      else if (inner_wss2)
-        SVM_WS_INNER_P(256, 4, false, true, true);
-      else
-        SVM_WS_INNER_P(256, 4, false, false, true);
-    } else if (inner_nt == 64)
+    if (inner_nt == 64)
       SVM_WS_INNER(64, 16);
     else if (inner_nt == 128)
       SVM_WS_INNER(128, 8);
@@ -817,7 +733,6 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
       SVM_WS_INNER(1024, 1);
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
-#undef SVM_WS_INNER_P
     SVMD_LAUNCH_CHECK();
     if (nloc > 0) {
       rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
@@ -833,8 +748,13 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     const double it = double(inner_total);
     fprintf(stderr, "decomp prof (clock64 ticks / inner iteration): select %.0f  publish+barrier %.0f  merge %.0f  "
             "row loads %.0f  update %.0f  (%lld iterations; inner kernels %.3f ms wall = %lld clock64 ticks)\n",
-            hs->prof[0] / it, hs->prof[1] / it, hs->prof[2] / it, hs->prof[3] / it, hs->prof[4] / it,
+            hs->prof[0] / it, hs->prof[1] / it, hs->prof[2] / it,
+            (hs->prof[3] + hs->prof[8] + hs->prof[9] + hs->prof[10] + hs->prof[11]) / it, hs->prof[4] / it,
             (long long)inner_total, hs->prof[7] / 1e5, (long long)hs->prof[6]);
+    if (inner_wss2)
+      fprintf(stderr, "decomp prof second-order j (inside row loads): row i %.0f  gains + wave reduction %.0f  "
+              "publish + barrier %.0f  fold %.0f  row j %.0f\n", hs->prof[8] / it, hs->prof[9] / it,
+              hs->prof[10] / it, hs->prof[11] / it, hs->prof[3] / it);
   }
   if (stats) {
     stats[0] = outer;
