@@ -116,8 +116,8 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
-    if a.solver is None:
-        a.solver = "smo" if cpu else "decomp"
+    if a.solver is None:  # the pairwise solver family for the CPU oracle, the cascade and the distributed SMO
+        a.solver = "smo" if (cpu or a.cascade or a.parallel in ("smo", "cascade")) else "decomp"
     if a.solver == "decomp" and (cpu or a.cascade or a.parallel in ("smo", "cascade")):
         print("bench.py: --solver decomp runs on GPUs (N > 1: --parallel auto | decomp); the cascade and the "
               "distributed pairwise SMO are --solver smo", file=sys.stderr)
