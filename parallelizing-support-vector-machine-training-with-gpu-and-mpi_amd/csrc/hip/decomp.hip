@@ -87,6 +87,30 @@ __device__ __forceinline__ void wave_arg_pair(VI mn, VI mx, VIL& rmn, VIL& rmx) 
   }
 }
 
+// The lanes holding wave_arg_pair's two winners (wave-uniform), without reading their values: the
+// winning lanes publish their own registers.
+__device__ __forceinline__ void wave_arg_pair_lanes(VI mn, VI mx, int& lmn, int& lmx) {
+  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
+  uint32_t a = k1, b = k2;
+  a = min(a, dpp32<0xB1>(a));
+  b = max(b, dpp32<0xB1>(b));
+  a = min(a, dpp32<0x4E>(a));
+  b = max(b, dpp32<0x4E>(b));
+  a = min(a, dpp32<0x141>(a));
+  b = max(b, dpp32<0x141>(b));
+  a = min(a, dpp32<0x140>(a));
+  b = max(b, dpp32<0x140>(b));
+  a = swap_pick32<true, false>(a);
+  b = swap_pick32<false, false>(b);
+  a = swap_pick32<true, true>(a);
+  b = swap_pick32<false, true>(b);
+  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
+  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
+  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
+  lmn = __popcll(t1) == 1 ? __builtin_ctzll(t1) : wave_arg<true>(mn).lane;
+  lmx = __popcll(t2) == 1 ? __builtin_ctzll(t2) : wave_arg<false>(mx).lane;
+}
+
 // A working-set candidate: global point id (-1 = none) and its f.  Candidates carry f because in the
 // distributed solve a GPU holds f only for its own points (every GPU holds alpha and y for all).
 struct CandRec {
@@ -337,45 +361,49 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       la = cl ? a[e] : la;
       li = cl ? k : li;
     }
-    VIL wmn, wmx;
-    wave_arg_pair(VI{hv, hi}, VI{lv, li}, wmn, wmx);
-    const double awmn = read_lane64(ha, wmn.lane), awmx = read_lane64(la, wmx.lane);
+    int lmn, lmx;  // the lanes holding the wave's winners publish them (no cross-lane reads)
+    wave_arg_pair_lanes(VI{hv, hi}, VI{lv, li}, lmn, lmx);
     stamp(0);
-    if (lane == 0) {
-      pv[par][0][w] = wmn.v;
-      pi[par][0][w] = wmn.i;
-      pa[par][0][w] = awmn;
-      pv[par][1][w] = wmx.v;
-      pi[par][1][w] = wmx.i;
-      pa[par][1][w] = awmx;
+    if (lane == lmn) {
+      pv[par][0][w] = hv;
+      pi[par][0][w] = hi;
+      pa[par][0][w] = ha;
+    }
+    if (lane == lmx) {
+      pv[par][1][w] = lv;
+      pi[par][1][w] = li;
+      pa[par][1][w] = la;
     }
     __syncthreads();
     stamp(1);
     // the same pairwise tree fold in every lane (value, then lowest position): log2(NW) dependent steps
-    double fv[2][NW], fa[2][NW];
+    // fold (value, position) only, tracking the winning wave; its alpha is read from LDS afterwards
+    double fv[2][NW];
     uint32_t fi[2][NW];
+    int fw[2][NW];
 #pragma unroll
     for (int q = 0; q < NW; ++q)
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd) {
         fv[sd][q] = pv[par][sd][q];
-        fa[sd][q] = pa[par][sd][q];
         fi[sd][q] = pi[par][sd][q];
+        fw[sd][q] = q;
       }
 #pragma unroll
     for (int st = 1; st < NW; st <<= 1)
 #pragma unroll
       for (int q = 0; q + st < NW; q += 2 * st) {
-        const bool th = fv[0][q + st] < fv[0][q] || (fv[0][q + st] == fv[0][q] && fi[0][q + st] < fi[0][q]);
-        const bool tl = fv[1][q + st] > fv[1][q] || (fv[1][q + st] == fv[1][q] && fi[1][q + st] < fi[1][q]);
+        // bitwise, not short-circuit: the compiler turned || / && on these uniform values into branches
+        const bool th = (fv[0][q + st] < fv[0][q]) | ((fv[0][q + st] == fv[0][q]) & (fi[0][q + st] < fi[0][q]));
+        const bool tl = (fv[1][q + st] > fv[1][q]) | ((fv[1][q + st] == fv[1][q]) & (fi[1][q + st] < fi[1][q]));
         fv[0][q] = th ? fv[0][q + st] : fv[0][q];
-        fa[0][q] = th ? fa[0][q + st] : fa[0][q];
         fi[0][q] = th ? fi[0][q + st] : fi[0][q];
+        fw[0][q] = th ? fw[0][q + st] : fw[0][q];
         fv[1][q] = tl ? fv[1][q + st] : fv[1][q];
-        fa[1][q] = tl ? fa[1][q + st] : fa[1][q];
         fi[1][q] = tl ? fi[1][q + st] : fi[1][q];
+        fw[1][q] = tl ? fw[1][q + st] : fw[1][q];
       }
-    double bh = fv[0][0], bl = fv[1][0], ah = fa[0][0], al = fa[1][0];
+    double bh = fv[0][0], bl = fv[1][0];
     uint32_t uih = fi[0][0], uil = fi[1][0];
     stamp(2);
     if (uih == kSentinel || uil == kSentinel) {
@@ -388,7 +416,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       break;
     }
     int ih = int(uih), il = int(uil);
-    double K12, bl_upd = bl;  // the second index's f in the update (first order: b_low)
+    double K12, bl_upd = bl, al;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
     if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
@@ -396,9 +424,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const int k = t + NT * e;
-        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
-        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+        const double vh = Kw[int64_t(ih) * ldw + k], vl = Kw[int64_t(il) * ldw + k];  // in bounds: k < ldw
+        kh[e] = k < m ? vh : 0.0;
+        kl[e] = k < m ? vl : 0.0;
       }
+      al = pa[par][1][fw[1][0]];
     } else {
       // second-order choice of the second index (smo_cpu.cpp / persist_solve WSS2): row i_high, then
       // the maximum of (f_t - b_high)^2 / a_t over I_low points above b_high (a_t = 2 - 2 K(i, t),
@@ -407,7 +437,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const int k = t + NT * e;
-        kh[e] = k < m ? Kw[int64_t(ih) * ldw + k] : 0.0;
+        const double v = Kw[int64_t(ih) * ldw + k];  // unconditional (k < ldw): no exec-mask branch per load
+        kh[e] = k < m ? v : 0.0;
       }
       if constexpr (PROF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -430,46 +461,54 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         gk = c ? kh[e] : gk;
         gi = c ? uint32_t(t + NT * e) : gi;
       }
-      const VIL wc = wave_arg<true>(VI{gv, gi});
-      const double wa = read_lane64(ga, wc.lane), wf = read_lane64(gf, wc.lane), wk = read_lane64(gk, wc.lane);
+      const int lc = wave_arg_lane<true>(VI{gv, gi});
       stamp(9);
-      if (lane == 0) {
-        qv[par][w] = wc.v;
-        qi[par][w] = wc.i;
-        qa[par][w] = wa;
-        qf[par][w] = wf;
-        qk[par][w] = wk;
+      if (lane == lc) {
+        qv[par][w] = gv;
+        qi[par][w] = gi;
+        qa[par][w] = ga;
+        qf[par][w] = gf;
+        qk[par][w] = gk;
       }
       __syncthreads();
       stamp(10);
-      double cv = qv[par][0];
-      uint32_t ci = qi[par][0];
-      al = qa[par][0];
-      bl_upd = qf[par][0];
-      K12 = qk[par][0];
+      // the same (value, lowest position) order as a serial fold, as a tree over (value, position);
+      // the winner's alpha, f and K(i, j) are read from its wave's slot afterwards
+      double cv[NW];
+      uint32_t cj[NW];
+      int cw[NW];
 #pragma unroll
-      for (int q = 1; q < NW; ++q) {
-        const double v = qv[par][q];
-        const uint32_t i2 = qi[par][q];
-        const bool tk = v < cv || (v == cv && i2 < ci);
-        cv = tk ? v : cv;
-        ci = tk ? i2 : ci;
-        al = tk ? qa[par][q] : al;
-        bl_upd = tk ? qf[par][q] : bl_upd;
-        K12 = tk ? qk[par][q] : K12;
+      for (int q = 0; q < NW; ++q) {
+        cv[q] = qv[par][q];
+        cj[q] = qi[par][q];
+        cw[q] = q;
       }
-      if (ci == kSentinel) {  // no I_low point above b_high (cannot happen while the gap is open)
+#pragma unroll
+      for (int st = 1; st < NW; st <<= 1)
+#pragma unroll
+        for (int q = 0; q + st < NW; q += 2 * st) {
+          const bool tk = (cv[q + st] < cv[q]) | ((cv[q + st] == cv[q]) & (cj[q + st] < cj[q]));
+          cv[q] = tk ? cv[q + st] : cv[q];
+          cj[q] = tk ? cj[q + st] : cj[q];
+          cw[q] = tk ? cw[q + st] : cw[q];
+        }
+      if (cj[0] == kSentinel) {  // no I_low point above b_high (cannot happen while the gap is open)
         reason = SVM_STOP_NO_CANDIDATE;
         break;
       }
-      il = int(ci);
+      il = int(cj[0]);
       stamp(11);
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const int k = t + NT * e;
-        kl[e] = k < m ? Kw[int64_t(il) * ldw + k] : 0.0;
+        const double v = Kw[int64_t(il) * ldw + k];
+        kl[e] = k < m ? v : 0.0;
       }
+      al = qa[par][cw[0]];
+      bl_upd = qf[par][cw[0]];
+      K12 = qk[par][cw[0]];
     }
+    const double ah = pa[par][0][fw[0][0]];
     const int32_t yh = sy[ih], yl = sy[il];
     if constexpr (PROF) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

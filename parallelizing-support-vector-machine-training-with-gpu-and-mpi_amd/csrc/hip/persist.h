@@ -160,6 +160,25 @@ __device__ __forceinline__ VIL wave_arg(VI a) {
   return VIL{read_lane64(a.v, src), uint32_t(__builtin_amdgcn_readlane(int(a.i), src)), src};
 }
 
+// wave_arg's winning lane only (wave-uniform): the caller reads or publishes the winner's fields.
+template <bool MIN, int L = 64>
+__device__ __forceinline__ int wave_arg_lane(VI a) {
+  const uint64_t k = order_key(a.v);
+  const uint32_t kh = uint32_t(k >> 32), kl = uint32_t(k);
+  const uint32_t bh = group_pick32<MIN, L>(kh);
+  unsigned long long tie = __ballot(kh == bh);
+  if (__popcll(tie) != 1) {
+    const uint32_t bl = group_pick32<MIN, L>(kh == bh ? kl : (MIN ? 0xFFFFFFFFu : 0u));
+    const bool same = kh == bh && kl == bl;
+    tie = __ballot(same);
+    if (__popcll(tie) != 1) {
+      const uint32_t bi = group_pick32<true, L>(same ? a.i : 0xFFFFFFFFu);
+      tie = __ballot(same && a.i == bi);
+    }
+  }
+  return __builtin_ctzll(tie);
+}
+
 struct PersistShared {
   double wv[2][16], wa[2][16];  // per-wave candidates [min|max][wave]
   uint32_t wi[2][16];
