@@ -444,8 +444,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(8);
       }
-      double gv = inf, ga = 0.0, gf = 0.0, gk = 0.0;
-      uint32_t gi = kSentinel;
+      double gv = inf;
+      int ge = 0;  // the element of the thread's best gain: its alpha, f and K(i, j) are read by the winner
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const bool below = a[e] < c_hi, above = a[e] > c_lo;
@@ -456,14 +456,19 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         const double gain = -(bb * bb) * __builtin_amdgcn_rcp(at);
         const bool c = in_low && ft[e] > bh && gain < gv;
         gv = c ? gain : gv;
-        ga = c ? a[e] : ga;
-        gf = c ? ft[e] : gf;
-        gk = c ? kh[e] : gk;
-        gi = c ? uint32_t(t + NT * e) : gi;
+        ge = c ? e : ge;
       }
+      const uint32_t gi = gv < inf ? uint32_t(t + NT * ge) : kSentinel;
       const int lc = wave_arg_lane<true>(VI{gv, gi});
       stamp(9);
       if (lane == lc) {
+        double ga = a[0], gf = ft[0], gk = kh[0];
+#pragma unroll
+        for (int e = 1; e < PER; ++e) {
+          ga = ge == e ? a[e] : ga;
+          gf = ge == e ? ft[e] : gf;
+          gk = ge == e ? kh[e] : gk;
+        }
         qv[par][w] = gv;
         qi[par][w] = gi;
         qa[par][w] = ga;

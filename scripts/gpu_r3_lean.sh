@@ -17,3 +17,10 @@ for w in 2 1; do
 done
 timeout -k 10 200 python -u scripts/decomp_timing.py 250000 1024 2 noref > gpurun_out/lean_250k.txt 2>&1 || { tail -20 gpurun_out/lean_250k.txt; exit 1; }
 grep "decomp q" gpurun_out/lean_250k.txt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lean_prof_k -o run -- python3 scripts/decomp_timing.py 60000 1024 3 noref > gpurun_out/lean_prof_k.log 2>&1 || { tail -20 gpurun_out/lean_prof_k.log; exit 1; }
+f=$(find gpurun_out/lean_prof_k -name "*kernel_stats.csv" | head -1)
+python -c "
+import csv
+for r in csv.DictReader(open('$f')):
+    print('   ', r['Name'][:70].ljust(70), r['Calls'].rjust(6), '%10.3f ms' % (int(r['TotalDurationNs']) / 1e6), '%9.1f us' % (float(r['AverageNs']) / 1e3))
+" > gpurun_out/lean_prof_k.txt; head -12 gpurun_out/lean_prof_k.txt
