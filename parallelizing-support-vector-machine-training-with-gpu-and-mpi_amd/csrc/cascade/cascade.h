@@ -236,6 +236,12 @@ class Transport {
     (void)what;
     return false;
   }
+  // The same for a recorded event (a hipEvent_t) of the rank's stream.
+  virtual bool event_wait(void* event, const char* what) {
+    (void)event;
+    (void)what;
+    return false;
+  }
   virtual void send_i64(int64_t v, int peer) = 0;
   virtual int64_t recv_i64(int peer) = 0;
   virtual void send(const void* buf, int64_t bytes, int peer) = 0;

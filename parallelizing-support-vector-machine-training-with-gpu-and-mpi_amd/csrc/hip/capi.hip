@@ -96,7 +96,9 @@ SVM_API void* svmd_create(int32_t device) {
   ctx->device = device;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_out, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_out, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_ctl[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_ctl[1], hipEventDisableTiming) != hipSuccess) {
     set_error("svmd_create: stream/event creation failed");
     delete ctx;
     return nullptr;
@@ -126,6 +128,8 @@ SVM_API void svmd_destroy(void* h) {
   if (ctx->count_d) (void)hipFree(ctx->count_d);
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
   if (ctx->ev_out) (void)hipEventDestroy(ctx->ev_out);
+  for (hipEvent_t e : ctx->ev_ctl)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

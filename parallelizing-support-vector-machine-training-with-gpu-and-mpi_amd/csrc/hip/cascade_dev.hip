@@ -631,6 +631,10 @@ class RcclTransport final : public Transport {
     wait(what);
     return true;
   }
+  bool event_wait(void* event, const char* what) override {
+    wait(what, static_cast<hipEvent_t>(event));
+    return true;
+  }
   void send_i64(int64_t v, int peer) override {
     pinned_[2] = v;
     HIPT(hipMemcpyAsync(scratch_ + 2, pinned_ + 2, 8, hipMemcpyHostToDevice, stream_));
@@ -665,10 +669,10 @@ class RcclTransport final : public Transport {
 
  private:
   // Poll instead of hipStreamSynchronize: a peer that never arrives must not hang this thread.
-  void wait(const char* what) {
+  void wait(const char* what, hipEvent_t event = nullptr) {
     const auto t0 = std::chrono::steady_clock::now();
     for (int spin = 0;; ++spin) {
-      const hipError_t e = hipStreamQuery(stream_);
+      const hipError_t e = event ? hipEventQuery(event) : hipStreamQuery(stream_);
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) throw TransportError(std::string(what) + ": " + hipGetErrorString(e));
       ncclResult_t ae = ncclSuccess;
@@ -825,7 +829,7 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   DecompAllGather ag;
   if (tr)
     ag = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
-          [tr]() { return tr->stream_wait("decomposition SMO: candidate all-gather + working-set build"); }};
+          [tr](void* ev) { return tr->event_wait(ev, "decomposition SMO: a batch of outer iterations"); }};
   bool used = false;
   double prep = 0.0;
   svm_result res{};

@@ -12,6 +12,7 @@ struct DeviceCtx {
   hipStream_t ext = nullptr;     // caller's stream (PyTorch current stream), may be null
   bool has_ext = false;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipEvent_t ev_ctl[2] = {nullptr, nullptr};  // decomposition solver: its control readbacks (decomp.hip)
   void* ws = nullptr;
   size_t ws_bytes = 0;
   void* pinned = nullptr;
@@ -139,7 +140,7 @@ int quantize_rows(hipStream_t s, const double* X, int64_t n, int64_t ld, const Q
                   int32_t* N0, double* WN, bool* ok);
 // copy_stw = false: the step weights are already in stw (no host-to-device copy on the stream).
 int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, double* stw, int64_t n,
-                     const QuantPlan& P, double gamma, double* K, int64_t ldk, bool copy_stw = true);
+                     const QuantPlan& P, double gamma, double* K, int64_t ldk, bool copy_stw = true, const int32_t* gate = nullptr);
 int launch_igram_slab(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                       int64_t n, int64_t col0, int64_t ncols, const QuantPlan& P, double gamma, double* K,
                       int64_t ldk);

@@ -19,11 +19,12 @@ struct DecompShape {
 DecompShape decomp_shape(int64_t n, int qws, int world);
 
 // All-gather of `bytes` from every GPU into recv (world * bytes, GPU-major), ordered on the solver's
-// stream (the distributed solve's one exchange per outer iteration), and optionally the wait for that
-// stream (true: waited; false / empty: the solver synchronises the stream itself).
+// stream (the distributed solve's one exchange per outer iteration), and optionally the wait for an
+// event recorded on that stream (true: waited under the transport's deadline / abort policy; false /
+// empty: the solver waits for it itself).
 struct DecompAllGather {
   std::function<void(const void* send, int64_t bytes, void* recv)> gather;
-  std::function<bool()> wait;
+  std::function<bool(void* event)> wait;
   explicit operator bool() const { return bool(gather); }
 };
 

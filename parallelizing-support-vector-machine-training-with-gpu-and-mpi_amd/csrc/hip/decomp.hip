@@ -38,15 +38,25 @@
 namespace svm355 {
 namespace {
 
-struct DecompHost {  // pinned: written by the kernels, read by the host once per outer iteration
-  double b_high, b_low;
-  int32_t m, stop;
-  int64_t inner_it;
-  int32_t inner_reason, changed;  // changed: points whose alpha the inner solve moved
-  int64_t prof[12];  // PROF builds: clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall
-                     // ticks; [8..11] the second-order j phase split (row i, gains + wave reduction, publish +
+struct DecompHost {  // pinned: the PROF build's phase totals (the loop state is DecompCtl, on the device)
+  int64_t prof[12];  // clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall ticks;
+                     // [8..11] the second-order j phase split (row i, gains + wave reduction, publish +
                      // barrier, fold)
 };
+
+// The outer loop's state on the device: the kernels of an outer iteration read and advance it, so the
+// host enqueues several outer iterations between synchronisations (a stopped solve turns the rest of
+// the batch into no-op launches).  stop = SVM_STOP_RUNNING (0) while running; kStopInternal: the working
+// set came out outside [2, kMaxWS] (a bug).
+struct DecompCtl {
+  int32_t stop, m;
+  double b_high, b_low;      // of the last working-set build
+  double tau_in;             // the next inner solve's stop tolerance
+  int64_t max_inner;         // and its iteration cap
+  int64_t outer, inner_total, changed_total, last_inner_it;
+  int32_t last_inner_reason, pad;
+};
+constexpr int32_t kStopInternal = -100;
 
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
 constexpr int kMaxWS = 1024;             // working-set capacity (one 1024-thread inner workgroup)
@@ -126,7 +136,9 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
                                                            const double* __restrict__ alpha,
                                                            const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
                                                            int64_t per, int T, double C, double eps,
-                                                           CandRec* __restrict__ cand_h, CandRec* __restrict__ cand_l) {
+                                                           CandRec* __restrict__ cand_h, CandRec* __restrict__ cand_l,
+                                                           const DecompCtl* __restrict__ ctl) {
+  if (ctl->stop != SVM_STOP_RUNNING) return;
   constexpr int NW = kSelNT / 64;
   __shared__ double sv[2][NW];
   __shared__ uint32_t si[2][NW];
@@ -192,8 +204,10 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
 // and the working set = the candidates' ids sorted, without duplicates (a free SV may be in both
 // lists), with their f (Wf).  Independent of the order the candidates arrive in.
 __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restrict__ cand, int L, int Lr, int Lh,
-                                                          double tau, int32_t* __restrict__ W,
-                                                          double* __restrict__ Wf, DecompHost* __restrict__ hs) {
+                                                          double tau, double tau_frac, int64_t max_iter,
+                                                          int32_t* __restrict__ W, double* __restrict__ Wf,
+                                                          DecompCtl* __restrict__ ctl, int32_t* __restrict__ mcount) {
+  if (ctl->stop != SVM_STOP_RUNNING) return;
   __shared__ int32_t s[kMaxWS];
   __shared__ double sf[kMaxWS];
   __shared__ int32_t wsum[kMaxWS / 64];
@@ -256,23 +270,38 @@ __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restr
       bh = fmin(bh, red[0][q]);
       bl = fmax(bl, red[1][q]);
     }
-    hs->m = m;
-    hs->b_high = bh;
-    hs->b_low = bl;
-    // no candidate on either side: the reference's "i_high or i_low not found" (main3.cpp:205-209)
-    hs->stop = !(bh < __builtin_inf()) || !(bl > -__builtin_inf()) ? SVM_STOP_NO_CANDIDATE
-               : (bl <= bh + 2.0 * tau)                             ? SVM_STOP_CONVERGED
-                                                                    : SVM_STOP_RUNNING;
+    ctl->b_high = bh;
+    ctl->b_low = bl;
+    int32_t st = SVM_STOP_RUNNING;
+    if (ctl->outer > 0 && ctl->last_inner_it == 0)  // no progress on the last W (a reference stop reason in it)
+      st = ctl->last_inner_reason == SVM_STOP_CONVERGED ? SVM_STOP_NO_CANDIDATE : ctl->last_inner_reason;
+    else if (!(bh < __builtin_inf()) || !(bl > -__builtin_inf()))  // "i_high or i_low not found" (main3.cpp:205-209)
+      st = SVM_STOP_NO_CANDIDATE;
+    else if (bl <= bh + 2.0 * tau)
+      st = SVM_STOP_CONVERGED;
+    else if (ctl->inner_total + 1 > max_iter)  // the reference counts num_iter from 1 (main3.cpp:283-287)
+      st = SVM_STOP_MAX_ITER;
+    else if (m < 2 || m > kMaxWS)
+      st = kStopInternal;
+    if (st != SVM_STOP_RUNNING) {
+      ctl->stop = st;
+      *mcount = 0;  // the rest of the batch's f updates are no-ops
+    } else {
+      ctl->m = m;
+      ctl->tau_in = fmax(tau, tau_frac * (bl - bh));
+      ctl->max_inner = min(int64_t(20) * m, max_iter - ctl->inner_total);
+    }
   }
 }
 
 // Qw[k] = Q[W[k]] (kq bytes), N0w[k], WNw[k]: one workgroup per working-set row.
 __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict__ Q, const int32_t* __restrict__ N0,
                                                        const double* __restrict__ WN, int kq,
-                                                       const int32_t* __restrict__ W, int m, int8_t* __restrict__ Qw,
-                                                       int32_t* __restrict__ N0w, double* __restrict__ WNw) {
+                                                       const int32_t* __restrict__ W, const DecompCtl* __restrict__ ctl,
+                                                       int8_t* __restrict__ Qw, int32_t* __restrict__ N0w,
+                                                       double* __restrict__ WNw) {
   const int k = blockIdx.x;
-  if (k >= m) return;
+  if (ctl->stop != SVM_STOP_RUNNING || k >= ctl->m) return;
   const int64_t src = W[k];
   const int4* s = reinterpret_cast<const int4*>(Q + src * int64_t(kq));
   int4* d = reinterpret_cast<int4*>(Qw + int64_t(k) * kq);
@@ -300,12 +329,15 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
 template <int NT, int PER, bool PROF = false, bool W2 = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
-                                                      const int32_t* __restrict__ W, int m,
+                                                      const int32_t* __restrict__ W, DecompCtl* __restrict__ ctl,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
                                                       const double* __restrict__ Wf, double C, double eps,
-                                                      double tau_in, int64_t max_inner, int32_t* __restrict__ cols,
-                                                      double* __restrict__ coef, int32_t* __restrict__ mcount,
-                                                      DecompHost* __restrict__ hs) {
+                                                      int32_t* __restrict__ cols, double* __restrict__ coef,
+                                                      int32_t* __restrict__ mcount, DecompHost* __restrict__ hs) {
+  if (ctl->stop != SVM_STOP_RUNNING) return;
+  const int m = ctl->m;
+  const double tau_in = ctl->tau_in;
+  const int64_t max_inner = ctl->max_inner;
   constexpr int NW = NT / 64;
   __shared__ double pv[2][2][NW], pa[2][2][NW];
   __shared__ uint32_t pi[2][2][NW];
@@ -585,9 +617,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   }
   if (t == 0) {
     *mcount = base;
-    hs->changed = base;
-    hs->inner_it = it;
-    hs->inner_reason = reason;
+    ctl->outer += 1;
+    ctl->inner_total += it;
+    ctl->changed_total += base;
+    ctl->last_inner_it = it;
+    ctl->last_inner_reason = reason;
   }
 }
 
@@ -686,10 +720,11 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
                o_all = take(size_t(sh.L) * sizeof(CandRec)), o_W = take(kMaxWS * 4), o_Wf = take(kMaxWS * 8),
                o_Qw = take(size_t(kMaxWS) * P.kq), o_N0w = take(kMaxWS * 4), o_WNw = take(kMaxWS * 8),
                o_Kw = take(size_t(kMaxWS) * ldw * 8), o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4),
-               o_mcount = take(256), o_part = take(size_t(std::max<int64_t>(nloc, 1)) * ldp * 8);
+               o_mcount = take(256), o_part = take(size_t(std::max<int64_t>(nloc, 1)) * ldp * 8),
+               o_ctl = take(sizeof(DecompCtl));
   int rc = ctx->ensure_ws(off);
   if (rc) return rc;
-  rc = ctx->ensure_pinned(sizeof(DecompHost) * 2);
+  rc = ctx->ensure_pinned(sizeof(DecompHost) * 2 + 2 * sizeof(DecompCtl));
   if (rc) return rc;
   char* ws = static_cast<char*>(ctx->ws);
   auto* f = reinterpret_cast<double*>(ws + o_f);
@@ -705,57 +740,24 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   auto* cols = reinterpret_cast<int32_t*>(ws + o_cols);
   auto* mcount = reinterpret_cast<int32_t*>(ws + o_mcount);
   auto* part = reinterpret_cast<double*>(ws + o_part);
+  auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
   auto* hs = static_cast<DecompHost*>(ctx->pinned);
+  auto* ctl_h = reinterpret_cast<DecompCtl*>(static_cast<char*>(ctx->pinned) + sizeof(DecompHost) * 2);
   std::memset(hs, 0, sizeof(DecompHost));
+  SVMD_CHECK(hipMemsetAsync(ctl, 0, sizeof(DecompCtl), s));  // stop = SVM_STOP_RUNNING, counters 0
   hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n);
   SVMD_LAUNCH_CHECK();
-  int64_t outer = 0, inner_total = 0, changed_total = 0;
-  int32_t stop = SVM_STOP_RUNNING;
-  double bh = 0.0, bl = 0.0;
-  for (;;) {
-    if (NBr > 0)
-      hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per, T,
-                         p.C, p.eps, cown, cown + NBr * T);
-    SVMD_LAUNCH_CHECK();
-    if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
-    hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
-                       W, Wf, hs);
-    SVMD_LAUNCH_CHECK();
-    if (!(world > 1 && allgather.wait && allgather.wait())) SVMD_CHECK(hipStreamSynchronize(s));
-    if (outer > 0) {  // the previous outer iteration's inner solve
-      inner_total += hs->inner_it;
-      changed_total += hs->changed;
-      if (hs->inner_it == 0) {  // no progress on W (a reference stop reason inside W, or no candidate)
-        stop = hs->inner_reason == SVM_STOP_CONVERGED ? SVM_STOP_NO_CANDIDATE : hs->inner_reason;
-        bh = hs->b_high;
-        bl = hs->b_low;
-        break;
-      }
-    }
-    bh = hs->b_high;
-    bl = hs->b_low;
-    if (hs->stop != SVM_STOP_RUNNING) {
-      stop = hs->stop;
-      break;
-    }
-    if (inner_total + 1 > p.max_iter) {  // the reference counts num_iter from 1 (main3.cpp:283-287)
-      stop = SVM_STOP_MAX_ITER;
-      break;
-    }
-    const int m = hs->m;
-    if (m < 2 || m > kMaxWS) {
-      set_error("decomposition SMO: working set of %d points", m);
-      return SVM_ERR_INTERNAL;
-    }
-    hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(m)), dim3(64), 0, s, Q, N0, WN, P.kq, W, m, Qw, N0w, WNw);
-    SVMD_LAUNCH_CHECK();
-    rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), m, P, p.gamma, Kw, ldw, false);
-    if (rc) return rc;
-    const double tau_in = std::max(p.tau, tau_frac * (bl - bh));
-    const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
+  // Outer iterations are enqueued `batch` at a time (SVM355_DECOMP_BATCH, default 1): every kernel reads
+  // the device control block, so after the stop the rest are no-op launches.  Each batch ends with a
+  // readback of the control block and an event; the host waits for batch k's event only after it has
+  // enqueued batch k + 1, so the GPU always has the next batch queued (no idle host round trip).
+  int batch = 1;  // with one batch always queued ahead, 1 already hides the host; more only adds no-op tail
+  if (const char* v = getenv("SVM355_DECOMP_BATCH")) batch = std::max(1, atoi(v));
+  int32_t* gate = &ctl->stop;
+  const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, m, y, alpha, Wf, p.C, \
-                     p.eps, tau_in, max_inner, cols, coef, mcount, hs)
+  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha, Wf,   \
+                     p.C, p.eps, cols, coef, mcount, hs)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
     SVM_WS_INNER_(NT, PER, true, true);      \
@@ -765,29 +767,67 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     SVM_WS_INNER_(NT, PER, false, true);     \
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
-    if (inner_nt == 64)
-      SVM_WS_INNER(64, 16);
-    else if (inner_nt == 128)
-      SVM_WS_INNER(128, 8);
-    else if (inner_nt == 256)
-      SVM_WS_INNER(256, 4);
-    else if (inner_nt == 512)
-      SVM_WS_INNER(512, 2);
-    else
-      SVM_WS_INNER(1024, 1);
+  const DecompCtl* fin = nullptr;  // the readback that saw the stop
+  for (int64_t bt = 0;; ++bt) {
+    for (int bi = 0; bi < batch; ++bi) {
+      if (NBr > 0)
+        hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
+                           T, p.C, p.eps, cown, cown + NBr * T, ctl);
+      SVMD_LAUNCH_CHECK();
+      if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
+      hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
+                         tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount);
+      SVMD_LAUNCH_CHECK();
+      hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, Q, N0, WN, P.kq, W, ctl, Qw, N0w,
+                         WNw);
+      SVMD_LAUNCH_CHECK();
+      // K(W, W) over the full capacity (rows beyond m are never read); skipped once stopped
+      rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
+      if (rc) return rc;
+      if (inner_nt == 64)
+        SVM_WS_INNER(64, 16);
+      else if (inner_nt == 128)
+        SVM_WS_INNER(128, 8);
+      else if (inner_nt == 256)
+        SVM_WS_INNER(256, 4);
+      else if (inner_nt == 512)
+        SVM_WS_INNER(512, 2);
+      else
+        SVM_WS_INNER(1024, 1);
+      SVMD_LAUNCH_CHECK();
+      if (nloc > 0) {
+        rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
+                               kMaxWS, P, p.gamma, part, ldp);
+        if (rc) return rc;
+        hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
+                           f, nloc);
+        SVMD_LAUNCH_CHECK();
+      }
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
-    SVMD_LAUNCH_CHECK();
-    if (nloc > 0) {
-      rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
-                             m, P, p.gamma, part, ldp);
-      if (rc) return rc;
-      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
-                         f, nloc);
-      SVMD_LAUNCH_CHECK();
     }
-    ++outer;
+    SVMD_CHECK(hipMemcpyAsync(ctl_h + (bt & 1), ctl, sizeof(DecompCtl), hipMemcpyDeviceToHost, s));
+    SVMD_CHECK(hipEventRecord(ctx->ev_ctl[bt & 1], s));
+    if (bt == 0) continue;  // keep one batch queued ahead of the wait
+    const int64_t pb = bt - 1;
+    hipEvent_t ev = ctx->ev_ctl[pb & 1];
+    if (!(world > 1 && allgather.wait && allgather.wait(ev))) SVMD_CHECK(hipEventSynchronize(ev));
+    if (ctl_h[pb & 1].stop != SVM_STOP_RUNNING) {
+      fin = ctl_h + (pb & 1);  // batch bt (queued) runs as no-ops; the state is final
+      break;
+    }
+    if (bt >= max_batches) {
+      set_error("decomposition SMO: no stop after %lld outer iterations", (long long)ctl_h[pb & 1].outer);
+      return SVM_ERR_INTERNAL;
+    }
   }
+  if (fin->stop == kStopInternal) {
+    set_error("decomposition SMO: working set outside [2, %d] points", kMaxWS);
+    return SVM_ERR_INTERNAL;
+  }
+  const int64_t outer = fin->outer, inner_total = fin->inner_total, changed_total = fin->changed_total;
+  const int32_t stop = fin->stop;
+  const double bh = fin->b_high, bl = fin->b_low;
   if (prof && inner_total > 0) {
     const double it = double(inner_total);
     fprintf(stderr, "decomp prof (clock64 ticks / inner iteration): select %.0f  publish+barrier %.0f  merge %.0f  "

@@ -303,8 +303,10 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     double* __restrict__ K, int64_t ldk, int64_t tiles, int64_t ncols, int64_t col0 = 0,
     const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
     const int32_t* __restrict__ ncount = nullptr, const int8_t* __restrict__ Qc = nullptr,
-    const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0) {
+    const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0,
+    const int32_t* __restrict__ gate = nullptr) {
   static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
+  if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch (decomp.hip)
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
   constexpr int CPR = BK / 16;            // 16-byte chunks per staged row
@@ -741,7 +743,7 @@ int run_igram(hipStream_t s, const double* X, int64_t n, int64_t ld, const Quant
 // The symmetric exact-integer Gram of quantised rows (Q, N0, WN); stw: device scratch for the step
 // weights.
 int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, double* stw, int64_t n,
-                     const QuantPlan& P, double gamma, double* K, int64_t ldk, bool copy_stw) {
+                     const QuantPlan& P, double gamma, double* K, int64_t ldk, bool copy_stw, const int32_t* gate) {
   if (copy_stw) SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
   const int64_t tiles = (n + QBM - 1) / QBM;
   const int64_t nwg = tiles * (tiles + 1);  // two 128x64 halves per upper-triangular 128x128 tile
@@ -753,7 +755,8 @@ int launch_igram_sym(hipStream_t s, const int8_t* Q, const int32_t* N0, const do
   if (const char* v = getenv("SVM355_IGRAM_BK")) bk = atoi(v) == 64 || P.kq % 128 ? 64 : 128;
 #define SVM_IGRAM(EX, B)                                                                                    \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq, P.main0, N0, \
-                     WN, stw, P.w0, -gamma, K, ldk, tiles, int64_t(0))
+                     WN, stw, P.w0, -gamma, K, ldk, tiles, int64_t(0), int64_t(0), nullptr, nullptr, nullptr, nullptr, \
+                     nullptr, nullptr, int64_t(0), gate)
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM(true, 128); else SVM_IGRAM(true, 64);
   } else {
