@@ -246,11 +246,12 @@ __global__ __launch_bounds__(1024) void nonzero_compact_kernel(const double* __r
 
 // Warm start, step 2: f_i = sum_{j in nz, ascending} alpha_j y_j K[j][i] - y_i
 // (mpi_svm_main3.cpp:169-186; column access K[j][i] is coalesced across i).  The sum stays serial in
-// ascending j per point (the reference's order); the wave-uniform idx / coef loads are read kWarmU
-// at a time and the kWarmU column loads issued before the adds consume them, so each group costs
+// ascending j per point (the reference's order); the wave-uniform idx / coef loads are read U
+// at a time and the U column loads issued before the adds consume them, so each group costs
 // one memory round trip instead of a dependent chain per term.  64-thread blocks spread a
 // cascade-sized n over many CUs.
-constexpr int kWarmU = 8;
+// PIPE: the next group's loads are issued before the current group's adds (2 U loads in flight).
+template <int U, bool PIPE>
 __global__ __launch_bounds__(64) void warm_f_kernel(const double* __restrict__ K, int64_t ldk,
                                                     const int32_t* __restrict__ y,
                                                     const int64_t* __restrict__ idx,
@@ -262,15 +263,46 @@ __global__ __launch_bounds__(64) void warm_f_kernel(const double* __restrict__ K
   const int64_t ic = i < n ? i : n - 1;  // tail lanes read a valid column, store nothing
   double sum = 0.0;
   int64_t k = 0;
-  for (; k + kWarmU <= cnt; k += kWarmU) {
-    double kv[kWarmU], c[kWarmU];
+  if constexpr (PIPE) {
+    double kv[U], c[U];
+    if (U <= cnt) {
 #pragma unroll
-    for (int u = 0; u < kWarmU; ++u) {
-      c[u] = coef[k + u];
-      kv[u] = K[idx[k + u] * ldk + ic];
+      for (int u = 0; u < U; ++u) {
+        c[u] = coef[u];
+        kv[u] = K[idx[u] * ldk + ic];
+      }
     }
+    for (; k + U <= cnt; k += U) {
+      double kn[U], cn[U];
+      const bool more = k + 2 * U <= cnt;  // wave-uniform
+      if (more) {
 #pragma unroll
-    for (int u = 0; u < kWarmU; ++u) sum += c[u] * kv[u];
+        for (int u = 0; u < U; ++u) {
+          cn[u] = coef[k + U + u];
+          kn[u] = K[idx[k + U + u] * ldk + ic];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum += c[u] * kv[u];
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          c[u] = cn[u];
+          kv[u] = kn[u];
+        }
+      }
+    }
+  } else {
+    for (; k + U <= cnt; k += U) {
+      double kv[U], c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c[u] = coef[k + u];
+        kv[u] = K[idx[k + u] * ldk + ic];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum += c[u] * kv[u];
+    }
   }
   for (; k < cnt; ++k) sum += coef[k] * K[idx[k] * ldk + ic];
   if (i < n) f[i] = sum - static_cast<double>(y[i]);
@@ -913,8 +945,16 @@ int run_smo(DeviceCtx* ctx, const double* K, int64_t ldk, const int32_t* y, int6
   } else {
     hipLaunchKernelGGL(nonzero_compact_kernel, dim3(1), dim3(1024), 0, s, alpha, y, n, idx, coef, cnt, st);
     SVMD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(warm_f_kernel, dim3(unsigned((n + 63) / 64)), dim3(64), 0, s, K, ldk, y, idx, coef, cnt, f,
-                       n);
+    // SVM355_WARM_U = 8 (one group of 8 in flight) | 16 | 32 (two groups in flight, pipelined)
+    int wu = 16;
+    if (const char* v = getenv("SVM355_WARM_U")) wu = atoi(v);
+    const dim3 wg(unsigned((n + 63) / 64));
+    if (wu == 8)
+      hipLaunchKernelGGL((warm_f_kernel<8, false>), wg, dim3(64), 0, s, K, ldk, y, idx, coef, cnt, f, n);
+    else if (wu == 32)
+      hipLaunchKernelGGL((warm_f_kernel<32, true>), wg, dim3(64), 0, s, K, ldk, y, idx, coef, cnt, f, n);
+    else
+      hipLaunchKernelGGL((warm_f_kernel<16, true>), wg, dim3(64), 0, s, K, ldk, y, idx, coef, cnt, f, n);
     SVMD_LAUNCH_CHECK();
   }
 
