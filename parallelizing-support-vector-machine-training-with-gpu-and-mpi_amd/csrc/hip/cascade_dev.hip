@@ -806,7 +806,12 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
     if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
   };
   DeviceCtx* ctx = be.device_ctx();
-  auto* Xd = static_cast<uint8_t*>(be.alloc(n * d));
+  const int world = tr ? tr->world() : 1, rank = tr ? tr->rank() : 0;
+  // Each GPU copies 1/world of the rows from the host over its own link and the rows are all-gathered
+  // over xGMI (in place), instead of every GPU pulling all n rows through the host: world concurrent
+  // pageable copies of the whole set would be staged through host memory world times.
+  const int64_t rows_per = (n + world - 1) / world, chunk = rows_per * d;
+  auto* Xd = static_cast<uint8_t*>(be.alloc(chunk * world));
   auto* yd = static_cast<int32_t*>(be.alloc(n * 4));
   auto* ad = static_cast<double*>(be.alloc(n * 8));
   auto* mm = static_cast<double*>(be.alloc(2 * d * 8));
@@ -817,13 +822,18 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
       for (void* q : ptrs) b.free(q);
     }
   } fr{be, {Xd, yd, ad, mm}};
-  be.h2d(Xd, X, n * d);
+  const int64_t r0 = std::min<int64_t>(n, rank * rows_per), r1 = std::min<int64_t>(n, r0 + rows_per);
+  if (world > 1) {
+    be.h2d(Xd + rank * chunk, X + r0 * d, (r1 - r0) * d);
+    tr->allgather(Xd + rank * chunk, chunk, Xd);  // rank r's slice at r * chunk = row r * rows_per
+  } else {
+    be.h2d(Xd, X, n * d);
+  }
   be.h2d(yd, y, n * 4);
   check(svmd_minmax_u8(ctx, Xd, n, d, mm, mm + d), "svmd_minmax_u8");
   std::vector<double> mmh(size_t(2 * d));
   be.d2h(mmh.data(), mm, 2 * d * 8);
   if (mm_out) std::memcpy(mm_out, mmh.data(), size_t(2 * d) * 8);
-  const int world = tr ? tr->world() : 1, rank = tr ? tr->rank() : 0;
   // RCCL: the all-gather is only enqueued; the solver's one host wait per outer iteration (after the
   // working-set build that reads the gathered candidates) polls under the transport's deadline
   DecompAllGather ag;
