@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
                                                            const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
                                                            int64_t per, int T, double C, double eps,
                                                            CandRec* __restrict__ cand_h, CandRec* __restrict__ cand_l,
-                                                           const DecompCtl* __restrict__ ctl, int per_wave) {
+                                                           const DecompCtl* __restrict__ ctl) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   constexpr int NW = kSelNT / 64;
   __shared__ double sv[2][NW];
@@ -157,37 +157,6 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
       if ((yi == 1 && a < c_hi) || (yi == -1 && a > c_lo)) fh[e] = fi;
       if ((yi == 1 && a > c_lo) || (yi == -1 && a < c_hi)) fl[e] = fi;
     }
-  }
-  if (per_wave) {
-    // every wave picks its own T / NW most violating points per side (its lanes' points of the block;
-    // no barrier): the block still contributes T per side, each wave's first picks are its extremes,
-    // so the union still holds the global extremes (the stop test's b_high / b_low)
-    const int Tw = T / NW;
-    for (int k = 0; k < Tw; ++k) {
-      VI mn{inf, kSentinel}, mx{-inf, kSentinel};
-#pragma unroll
-      for (int e = 0; e < kSelE; ++e) {
-        const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
-        const bool ch = fh[e] < mn.v, cl = fl[e] > mx.v;
-        mn = ch ? VI{fh[e], i} : mn;
-        mx = cl ? VI{fl[e], i} : mx;
-      }
-      VIL a, b;
-      wave_arg_pair(mn, mx, a, b);
-      if (lane == 0) {
-        const int64_t slot = int64_t(blockIdx.x) * T + w * Tw + k;
-        const bool hok = a.i != kSentinel && a.v < inf, lok = b.i != kSentinel && b.v > -inf;
-        cand_h[slot] = CandRec{hok ? a.v : 0.0, hok ? int32_t(a.i) : -1, 0};
-        cand_l[slot] = CandRec{lok ? b.v : 0.0, lok ? int32_t(b.i) : -1, 0};
-      }
-#pragma unroll
-      for (int e = 0; e < kSelE; ++e) {
-        const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
-        if (i == a.i) fh[e] = inf;
-        if (i == b.i) fl[e] = -inf;
-      }
-    }
-    return;
   }
   for (int k = 0; k < T; ++k) {
     VI mn{inf, kSentinel}, mx{-inf, kSentinel};
@@ -782,10 +751,6 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   // the device control block, so after the stop the rest are no-op launches.  Each batch ends with a
   // readback of the control block and an event; the host waits for batch k's event only after it has
   // enqueued batch k + 1, so the GPU always has the next batch queued (no idle host round trip).
-  // per-wave candidate picks in the selection (no barriers), when T splits evenly over the waves:
-  // SVM355_DECOMP_SELW = 0 | 1
-  bool sel_wave = T % (kSelNT / 64) == 0;
-  if (const char* v = getenv("SVM355_DECOMP_SELW")) sel_wave = sel_wave && atoi(v) != 0;
   int batch = 1;  // with one batch always queued ahead, 1 already hides the host; more only adds no-op tail
   if (const char* v = getenv("SVM355_DECOMP_BATCH")) batch = std::max(1, atoi(v));
   int32_t* gate = &ctl->stop;
@@ -807,7 +772,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     for (int bi = 0; bi < batch; ++bi) {
       if (NBr > 0)
         hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
-                           T, p.C, p.eps, cown, cown + NBr * T, ctl, int(sel_wave));
+                           T, p.C, p.eps, cown, cown + NBr * T, ctl);
       SVMD_LAUNCH_CHECK();
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
       hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
