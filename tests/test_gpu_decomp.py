@@ -78,6 +78,30 @@ def test_decomp_fp64_rows_equal_the_byte_path():
     np.testing.assert_array_equal(a.predict(te.X), b.predict(te.X.astype(np.float64)))
 
 
+def test_decomp_stop_reasons_of_the_device_loop():
+    """The outer loop runs on a device-side control block (batches of launches, no host read per outer
+    iteration): the iteration cap still stops it with the reference's reason and count, and every batch
+    size gives the same model."""
+    import os
+
+    tr = synthetic_mnist(6000, seed=81).compact()
+    m = SVC(device="cuda:0", solver="decomp", max_iter=300).fit(tr.X, tr.y)
+    assert m.stop_reason_ == "max_iter" and m.n_iter_ == 301  # the reference counts from 1
+    ref = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    old = os.environ.get("SVM355_DECOMP_BATCH")
+    try:
+        os.environ["SVM355_DECOMP_BATCH"] = "5"
+        m5 = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    finally:
+        if old is None:
+            os.environ.pop("SVM355_DECOMP_BATCH", None)
+        else:
+            os.environ["SVM355_DECOMP_BATCH"] = old
+    assert m5.n_iter_ == ref.n_iter_ and m5.b_ == ref.b_
+    np.testing.assert_array_equal(m5.alpha_, ref.alpha_)
+    assert m5.timings_["outer_iterations"] == ref.timings_["outer_iterations"]
+
+
 def test_decomp_refuses_what_it_does_not_cover():
     tr = synthetic_mnist(500, seed=3)
     rng = np.random.default_rng(5)
