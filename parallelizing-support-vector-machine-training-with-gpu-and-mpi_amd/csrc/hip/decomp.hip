@@ -61,66 +61,6 @@ constexpr int32_t kStopInternal = -100;
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
 constexpr int kMaxWS = 1024;             // working-set capacity (one 1024-thread inner workgroup)
 
-// Both of an iteration's wave arg-reductions in lockstep (minimum over I_high, maximum over I_low):
-// the two high-word butterflies are independent DPP chains and interleave; each side falls back to
-// wave_arg (low words, then the lowest index) only when its high word ties.  Same results as two
-// wave_arg calls.
-__device__ __forceinline__ void wave_arg_pair(VI mn, VI mx, VIL& rmn, VIL& rmx) {
-  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
-  uint32_t a = k1, b = k2;
-  a = min(a, dpp32<0xB1>(a));
-  b = max(b, dpp32<0xB1>(b));
-  a = min(a, dpp32<0x4E>(a));
-  b = max(b, dpp32<0x4E>(b));
-  a = min(a, dpp32<0x141>(a));
-  b = max(b, dpp32<0x141>(b));
-  a = min(a, dpp32<0x140>(a));
-  b = max(b, dpp32<0x140>(b));
-  a = swap_pick32<true, false>(a);
-  b = swap_pick32<false, false>(b);
-  a = swap_pick32<true, true>(a);
-  b = swap_pick32<false, true>(b);
-  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
-  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
-  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
-  if (__popcll(t1) == 1) {
-    const int src = __builtin_ctzll(t1);
-    rmn = VIL{read_lane64(mn.v, src), uint32_t(__builtin_amdgcn_readlane(int(mn.i), src)), src};
-  } else {
-    rmn = wave_arg<true>(mn);
-  }
-  if (__popcll(t2) == 1) {
-    const int src = __builtin_ctzll(t2);
-    rmx = VIL{read_lane64(mx.v, src), uint32_t(__builtin_amdgcn_readlane(int(mx.i), src)), src};
-  } else {
-    rmx = wave_arg<false>(mx);
-  }
-}
-
-// The lanes holding wave_arg_pair's two winners (wave-uniform), without reading their values: the
-// winning lanes publish their own registers.
-__device__ __forceinline__ void wave_arg_pair_lanes(VI mn, VI mx, int& lmn, int& lmx) {
-  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
-  uint32_t a = k1, b = k2;
-  a = min(a, dpp32<0xB1>(a));
-  b = max(b, dpp32<0xB1>(b));
-  a = min(a, dpp32<0x4E>(a));
-  b = max(b, dpp32<0x4E>(b));
-  a = min(a, dpp32<0x141>(a));
-  b = max(b, dpp32<0x141>(b));
-  a = min(a, dpp32<0x140>(a));
-  b = max(b, dpp32<0x140>(b));
-  a = swap_pick32<true, false>(a);
-  b = swap_pick32<false, false>(b);
-  a = swap_pick32<true, true>(a);
-  b = swap_pick32<false, true>(b);
-  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
-  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
-  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
-  lmn = __popcll(t1) == 1 ? __builtin_ctzll(t1) : wave_arg<true>(mn).lane;
-  lmx = __popcll(t2) == 1 ? __builtin_ctzll(t2) : wave_arg<false>(mx).lane;
-}
-
 // A working-set candidate: global point id (-1 = none) and its f.  Candidates carry f because in the
 // distributed solve a GPU holds f only for its own points (every GPU holds alpha and y for all).
 struct CandRec {

@@ -179,6 +179,66 @@ __device__ __forceinline__ int wave_arg_lane(VI a) {
   return __builtin_ctzll(tie);
 }
 
+// Both of an iteration's wave arg-reductions in lockstep (minimum over I_high, maximum over I_low):
+// the two high-word butterflies are independent DPP chains and interleave; each side falls back to
+// wave_arg (low words, then the lowest index) only when its high word ties.  Same results as two
+// wave_arg calls.
+__device__ __forceinline__ void wave_arg_pair(VI mn, VI mx, VIL& rmn, VIL& rmx) {
+  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
+  uint32_t a = k1, b = k2;
+  a = min(a, dpp32<0xB1>(a));
+  b = max(b, dpp32<0xB1>(b));
+  a = min(a, dpp32<0x4E>(a));
+  b = max(b, dpp32<0x4E>(b));
+  a = min(a, dpp32<0x141>(a));
+  b = max(b, dpp32<0x141>(b));
+  a = min(a, dpp32<0x140>(a));
+  b = max(b, dpp32<0x140>(b));
+  a = swap_pick32<true, false>(a);
+  b = swap_pick32<false, false>(b);
+  a = swap_pick32<true, true>(a);
+  b = swap_pick32<false, true>(b);
+  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
+  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
+  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
+  if (__popcll(t1) == 1) {
+    const int src = __builtin_ctzll(t1);
+    rmn = VIL{read_lane64(mn.v, src), uint32_t(__builtin_amdgcn_readlane(int(mn.i), src)), src};
+  } else {
+    rmn = wave_arg<true>(mn);
+  }
+  if (__popcll(t2) == 1) {
+    const int src = __builtin_ctzll(t2);
+    rmx = VIL{read_lane64(mx.v, src), uint32_t(__builtin_amdgcn_readlane(int(mx.i), src)), src};
+  } else {
+    rmx = wave_arg<false>(mx);
+  }
+}
+
+// The lanes holding wave_arg<true>(mn) and wave_arg<false>(mx) (wave-uniform), with the two high-word
+// butterflies interleaved; the caller's winning lanes publish their own fields.
+__device__ __forceinline__ void wave_arg_pair_lanes(VI mn, VI mx, int& lmn, int& lmx) {
+  const uint32_t k1 = uint32_t(order_key(mn.v) >> 32), k2 = uint32_t(order_key(mx.v) >> 32);
+  uint32_t a = k1, b = k2;
+  a = min(a, dpp32<0xB1>(a));
+  b = max(b, dpp32<0xB1>(b));
+  a = min(a, dpp32<0x4E>(a));
+  b = max(b, dpp32<0x4E>(b));
+  a = min(a, dpp32<0x141>(a));
+  b = max(b, dpp32<0x141>(b));
+  a = min(a, dpp32<0x140>(a));
+  b = max(b, dpp32<0x140>(b));
+  a = swap_pick32<true, false>(a);
+  b = swap_pick32<false, false>(b);
+  a = swap_pick32<true, true>(a);
+  b = swap_pick32<false, true>(b);
+  const uint32_t h1 = uint32_t(__builtin_amdgcn_readfirstlane(int(a)));
+  const uint32_t h2 = uint32_t(__builtin_amdgcn_readfirstlane(int(b)));
+  const unsigned long long t1 = __ballot(k1 == h1), t2 = __ballot(k2 == h2);
+  lmn = __popcll(t1) == 1 ? __builtin_ctzll(t1) : wave_arg_lane<true>(mn);
+  lmx = __popcll(t2) == 1 ? __builtin_ctzll(t2) : wave_arg_lane<false>(mx);
+}
+
 struct PersistShared {
   double wv[2][16], wa[2][16];  // per-wave candidates [min|max][wave]
   uint32_t wi[2][16];
@@ -678,6 +738,7 @@ __device__ __forceinline__ uint32_t persist_solve(
       if (stamping) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sprev)::"memory");
     }
     // ---- 1. local selection over the register slice (ascending index within a thread)
+    // branch-free: selects, not exec-mask branches, over the E points
     VI mn{inf, kSentinel}, mx{-inf, kSentinel};
     double amn = 0.0, amx = 0.0;
 #pragma unroll
@@ -685,28 +746,30 @@ __device__ __forceinline__ uint32_t persist_solve(
       const uint32_t i = uint32_t(lo + t + NT * e);
       const double a = ar[e], fi = fr[e];
       const int32_t yi = yr[e];
-      const bool in_high = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
-      const bool in_low = (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi);
-      if (in_high && fi < mn.v) {
-        mn = VI{fi, i};
-        amn = a;
-      }
-      if (in_low && fi > mx.v) {
-        mx = VI{fi, i};
-        amx = a;
-      }
+      const bool in_high = ((yi == 1) & (a < c_hi)) | ((yi == -1) & (a > c_lo));
+      const bool in_low = ((yi == 1) & (a > c_lo)) | ((yi == -1) & (a < c_hi));
+      const bool ch = in_high & (fi < mn.v), cl = in_low & (fi > mx.v);
+      mn.v = ch ? fi : mn.v;
+      mn.i = ch ? i : mn.i;
+      amn = ch ? a : amn;
+      mx.v = cl ? fi : mx.v;
+      mx.i = cl ? i : mx.i;
+      amx = cl ? a : amx;
     }
     {
-      const VIL wmn = wave_arg<true>(mn), wmx = wave_arg<false>(mx);
-      const double awmn = read_lane64(amn, wmn.lane), awmx = read_lane64(amx, wmx.lane);
+      // both reductions interleaved; the winning lanes publish their own value, index and alpha
+      int lmn, lmx;
+      wave_arg_pair_lanes(mn, mx, lmn, lmx);
       PSTAMP(0);
-      if (lane == 0) {
-        sh.wv[0][w] = wmn.v;
-        sh.wi[0][w] = wmn.i;
-        sh.wa[0][w] = awmn;
-        sh.wv[1][w] = wmx.v;
-        sh.wi[1][w] = wmx.i;
-        sh.wa[1][w] = awmx;
+      if (lane == lmn) {
+        sh.wv[0][w] = mn.v;
+        sh.wi[0][w] = mn.i;
+        sh.wa[0][w] = amn;
+      }
+      if (lane == lmx) {
+        sh.wv[1][w] = mx.v;
+        sh.wi[1][w] = mx.i;
+        sh.wa[1][w] = amx;
       }
     }
     __syncthreads();
@@ -836,7 +899,8 @@ __device__ __forceinline__ uint32_t persist_solve(
       if (STAMP && RPL == 1 && g == 0 && lane == 0 && epoch >= kStampFrom && epoch < kStampFrom + kSkewEpochs)
         stamps[kSkewBase + kMaxG * kSkewEpochs + (epoch - kStampFrom)] = __builtin_amdgcn_s_memrealtime();
       PSTAMP(3);
-      const VIL wgm = wave_arg<true>(gm), wgx = wave_arg<false>(gx);
+      VIL wgm, wgx;
+      wave_arg_pair(gm, gx, wgm, wgx);  // the two reductions interleaved
       const double awgm = read_lane64(agm, wgm.lane), awgx = read_lane64(agx, wgx.lane);
       if (lane == 0) {
         sh.gv[0] = wgm.v;
