@@ -920,7 +920,8 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
     set_error("igram gemv: bad partial stride or problem too large");
     return SVM_ERR_ARG;
   }
-  const int bk = P.kq % 128 == 0 ? 128 : 64;
+  int bk = P.kq % 128 == 0 ? 128 : 64;
+  if (const char* v = getenv("SVM355_GEMV_BK")) bk = atoi(v) == 64 || P.kq % 128 ? 64 : 128;  // A/B knob
 #define SVM_IGRAM_GEMV(EX, B)                                                                                       \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,        \
                      P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, m, int64_t(0), cols, coef, mcount, Qc, N0c, WNc, \
