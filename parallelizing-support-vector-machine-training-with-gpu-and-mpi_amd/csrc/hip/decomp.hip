@@ -252,8 +252,9 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
   }
 }
 
-// First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER points
-// W[t + NT e] (f, alpha, y in registers).  Per iteration:
+// First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER contiguous
+// points W[t PER + e] (f, alpha, y in registers; its entries of a K(W, W) row are PER / 2 16-byte loads).
+// Per iteration:
 //   select   branch-free thread-local (value, lowest position) minimum over I_high and maximum over
 //            I_low, carrying the winner's alpha, then the wave64 arg-reductions (wave_arg);
 //   publish  lane 0 of every wave writes its two candidates to LDS (double-buffered by iteration
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   const double tau_in = ctl->tau_in;
   const int64_t max_inner = ctl->max_inner;
   constexpr int NW = NT / 64;
+  static_assert(PER % 2 == 0, "row entries are loaded 16 bytes at a time");
   __shared__ double pv[2][2][NW], pa[2][2][NW];
   __shared__ uint32_t pi[2][2][NW];
   __shared__ double qv[2][NW], qa[2][NW], qf[2][NW], qk[2][NW];  // W2: the second index's candidates
@@ -286,12 +288,16 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   __shared__ int8_t sy[NT * PER];
   __shared__ int32_t wcnt[PER][NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // position of this thread's element e: pair h = e / 2 of every lane is one 16-byte piece; a wave's 64
+  // pieces of pair h are one contiguous kilobyte, and the NT / 64 waves' kilobytes of pair h are adjacent
+  const int pbase = w * 128 + 2 * lane;
+  auto pos = [&](int e) { return pbase + (e >> 1) * (2 * NT) + (e & 1); };
   double a[PER], a0[PER], ft[PER];
   bool yp[PER], yn[PER];  // y = +1 / y = -1 (padding: neither, so in neither set)
   int64_t gid[PER];
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
-    const int k = t + NT * e;
+    const int k = pos(e);
     const bool valid = k < m;
     gid[e] = valid ? W[k] : 0;
     a[e] = valid ? alpha[gid[e]] : 0.0;
@@ -309,6 +315,17 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   int64_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t pt = PROF ? int64_t(clock64()) : 0;
   const int64_t pc0 = pt, pw0 = PROF ? int64_t(wall_clock64()) : 0;
+  // this thread's PER contiguous entries of row r of K(W, W) as 16-byte loads (in bounds: t PER + e <
+  // NT PER <= ldw; the row base is 16-byte aligned: ldw even), zero beyond m
+  auto row = [&](int r, double* out) {
+    const double2* src = reinterpret_cast<const double2*>(Kw + int64_t(r) * ldw + pbase);
+#pragma unroll
+    for (int h = 0; h < PER / 2; ++h) {
+      const double2 v = src[NT * h];
+      out[2 * h] = pos(2 * h) < m ? v.x : 0.0;
+      out[2 * h + 1] = pos(2 * h + 1) < m ? v.y : 0.0;
+    }
+  };
   auto stamp = [&](int k) {
     if constexpr (PROF) {
       const int64_t now = int64_t(clock64());
@@ -325,7 +342,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       const bool in_high = (yp[e] && below) || (yn[e] && above);
       const bool in_low = (yp[e] && above) || (yn[e] && below);
       const bool ch = in_high && ft[e] < hv, cl = in_low && ft[e] > lv;
-      const uint32_t k = uint32_t(t + NT * e);
+      const uint32_t k = uint32_t(pos(e));
       hv = ch ? ft[e] : hv;
       ha = ch ? a[e] : ha;
       hi = ch ? k : hi;
@@ -393,25 +410,15 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
       K12 = Kw[int64_t(ih) * ldw + il];
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int k = t + NT * e;
-        const double vh = Kw[int64_t(ih) * ldw + k], vl = Kw[int64_t(il) * ldw + k];  // in bounds: k < ldw
-        kh[e] = k < m ? vh : 0.0;
-        kl[e] = k < m ? vl : 0.0;
-      }
+      row(ih, kh);
+      row(il, kl);
       al = pa[par][1][fw[1][0]];
     } else {
       // second-order choice of the second index (smo_cpu.cpp / persist_solve WSS2): row i_high, then
       // the maximum of (f_t - b_high)^2 / a_t over I_low points above b_high (a_t = 2 - 2 K(i, t),
       // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
       // and fold, then row j
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int k = t + NT * e;
-        const double v = Kw[int64_t(ih) * ldw + k];  // unconditional (k < ldw): no exec-mask branch per load
-        kh[e] = k < m ? v : 0.0;
-      }
+      row(ih, kh);  // unconditional loads (no exec-mask branch per load)
       if constexpr (PROF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(8);
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         gv = c ? gain : gv;
         ge = c ? e : ge;
       }
-      const uint32_t gi = gv < inf ? uint32_t(t + NT * ge) : kSentinel;
+      const uint32_t gi = gv < inf ? uint32_t(pos(ge)) : kSentinel;
       const int lc = wave_arg_lane<true>(VI{gv, gi});
       stamp(9);
       if (lane == lc) {
@@ -475,12 +482,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       }
       il = int(cj[0]);
       stamp(11);
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int k = t + NT * e;
-        const double v = Kw[int64_t(il) * ldw + k];
-        kl[e] = k < m ? v : 0.0;
-      }
+      row(il, kl);
       al = qa[par][cw[0]];
       bl_upd = qf[par][cw[0]];
       K12 = qk[par][cw[0]];
@@ -518,36 +520,44 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     const double cl = (al_new - al) * double(yl);
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int k = t + NT * e;
+      const int k = pos(e);
       ft[e] += ch * kh[e] + cl * kl[e];  // main3.cpp:274 operation order
       a[e] = k == ih ? ah_new : k == il ? al_new : a[e];
     }
     ++it;
     stamp(4);
   }
-  unsigned long long bal[PER];
+  // compaction in position order: pair h, then wave, then lane, then e & 1
+  bool chg[PER];
+  int below[PER / 2];
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
-    const int k = t + NT * e;
-    const bool changed = k < m && a[e] != a0[e];
-    if (changed) alpha[gid[e]] = a[e];
-    bal[e] = __ballot(changed);
-    if (lane == 0) wcnt[e][w] = __popcll(bal[e]);
+    chg[e] = pos(e) < m && a[e] != a0[e];
+    if (chg[e]) alpha[gid[e]] = a[e];
+  }
+#pragma unroll
+  for (int h = 0; h < PER / 2; ++h) {
+    const unsigned long long b0 = __ballot(chg[2 * h]), b1 = __ballot(chg[2 * h + 1]);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    below[h] = __popcll(b0 & lt) + __popcll(b1 & lt);
+    if (lane == 0) wcnt[h][w] = __popcll(b0) + __popcll(b1);
   }
   __syncthreads();
   int base = 0;
 #pragma unroll
-  for (int e = 0; e < PER; ++e) {  // position order k = t + NT e: e-major, then wave, then lane
-    int off = base;
+  for (int h = 0; h < PER / 2; ++h) {
+    int j = base + below[h];
     for (int q = 0; q < NW; ++q) {
-      if (q < w) off += wcnt[e][q];
-      base += wcnt[e][q];
+      if (q < w) j += wcnt[h][q];
+      base += wcnt[h][q];
     }
-    if ((bal[e] >> lane) & 1ull) {
-      const int j = off + __popcll(bal[e] & ((1ull << lane) - 1ull));
-      cols[j] = int32_t(gid[e]);
-      coef[j] = (a[e] - a0[e]) * (yp[e] ? 1.0 : -1.0);
-    }
+#pragma unroll
+    for (int e = 2 * h; e < 2 * h + 2; ++e)
+      if (chg[e]) {
+        cols[j] = int32_t(gid[e]);
+        coef[j] = (a[e] - a0[e]) * (yp[e] ? 1.0 : -1.0);
+        ++j;
+      }
   }
   if (PROF && t == 0) {
     for (int k = 0; k < 5; ++k) hs->prof[k] += pacc[k];
@@ -636,9 +646,10 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   const int64_t nloc = hi - lo;
   const int T = sh.T;
   const int64_t Lr = 2 * NBr * T;  // this GPU's candidate records (I_high picks, then I_low)
-  // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512 | 1024
+  // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512
   int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
+  if (inner_nt != 64 && inner_nt != 128 && inner_nt != 512) inner_nt = 256;
   // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
   double tau_frac = 0.1;
   if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
@@ -730,10 +741,8 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
         SVM_WS_INNER(128, 8);
       else if (inner_nt == 256)
         SVM_WS_INNER(256, 4);
-      else if (inner_nt == 512)
-        SVM_WS_INNER(512, 2);
       else
-        SVM_WS_INNER(1024, 1);
+        SVM_WS_INNER(512, 2);
       SVMD_LAUNCH_CHECK();
       if (nloc > 0) {
         rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
