@@ -407,6 +407,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     int ih = int(uih), il = int(uil);
     double K12, bl_upd = bl, al;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
+    double2 rj[PER / 2];  // second order: row j's raw pieces, consumed only after the clip arithmetic
     if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
       K12 = Kw[int64_t(ih) * ldw + il];
@@ -482,7 +483,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       }
       il = int(cj[0]);
       stamp(11);
-      row(il, kl);
+      {  // issued now, consumed after the clip / division below, which then runs under the loads' latency
+        const double2* src = reinterpret_cast<const double2*>(Kw + int64_t(il) * ldw + pbase);
+#pragma unroll
+        for (int h = 0; h < PER / 2; ++h) rj[h] = src[NT * h];
+      }
       al = qa[par][cw[0]];
       bl_upd = qf[par][cw[0]];
       K12 = qk[par][cw[0]];
@@ -518,6 +523,16 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     const double ah_new = ah + double(s) * (al - al_new);
     const double ch = (ah_new - ah) * double(yh);
     const double cl = (al_new - al) * double(yl);
+    if constexpr (W2) {
+#pragma unroll
+      for (int h = 0; h < PER / 2; ++h) {
+        double x = rj[h].x, z = rj[h].y;
+        // an empty asm reading cl: the wait for row j's data lands here, after the division, not inside it
+        asm volatile("" : "+v"(x), "+v"(z) : "v"(cl));
+        kl[2 * h] = pos(2 * h) < m ? x : 0.0;
+        kl[2 * h + 1] = pos(2 * h + 1) < m ? z : 0.0;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int k = pos(e);
