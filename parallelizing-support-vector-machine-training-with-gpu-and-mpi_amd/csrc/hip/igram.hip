@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
     const int32_t* __restrict__ ncount = nullptr, const int8_t* __restrict__ Qc = nullptr,
     const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0,
-    const int32_t* __restrict__ gate = nullptr) {
+    const int32_t* __restrict__ gate = nullptr, int64_t cstride = 0) {
   static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
   if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch (decomp.hip)
   using Cfg = IgramCfg<BK>;
@@ -338,12 +338,20 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   } else {
     tri_tile(wg >> 1, tiles, tm, tn);
   }
-  const int64_t bm = tm * QBM, bn = tn * QBM + (wg & 1) * QBN;
+  const int64_t bm_ = tm * QBM;
+  int64_t bn = tn * QBM + (wg & 1) * QBN;
   // column bound (block-local); GEMV: the device-side count, whole workgroups beyond it exit
   const int64_t ncol = GEMV ? int64_t(*ncount) : RECT ? ncols : n;
-  if (GEMV && bn >= ncol) return;
   // global row of block column j: c0 + j, or colid[j] (GEMV)
   auto crow = [&](int64_t j) -> int64_t { return GEMV ? int64_t(colid[j]) : c0 + j; };
+  // GEMV with cstride > 0: the grid covers ncols columns per row tile and each workgroup walks its
+  // half, then the halves cstride columns further on, up to *ncount (few workgroups exit unused)
+  for (;;) {
+  if (GEMV && bn >= ncol) return;
+  // opaque per pass: nothing derived from the row tile is hoisted out of the GEMV loop (that held
+  // its addresses live across the whole k-loop and spilled)
+  int64_t bm = bm_;
+  if constexpr (GEMV) asm volatile("" : "+s"(bm));
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int main_step0 = main0 / 32;
@@ -489,7 +497,10 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
         if (gi < n) K[gi * ldk + part] = rs[r];
       }
     }
-    return;
+    if (cstride <= 0) return;
+    bn += cstride;
+    __syncthreads();  // the next half rewrites the column tables the epilogue has just read
+    continue;
   }
   // ---- epilogue in the 32x32 accumulator layout: col = lane & 31,
   // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
@@ -560,6 +571,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
+  return;
+  }  // for (GEMV column halves)
 }
 
 }  // namespace
@@ -915,7 +928,15 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
                       double gamma, double* part, int64_t ldp) {
   if (n <= 0 || m <= 0) return SVM_OK;
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
-  const int64_t nwg = 2 * tiles * ctiles;
+  // the grid covers gc 128-column tiles per row tile; its workgroups walk further halves when *mcount
+  // exceeds them (SVM355_GEMV_GC; 0 = one workgroup per half of all m columns, most exiting at once).
+  // gc = 1 measured best: 113 -> 90 us per call at 60k, the 250k fit 136 -> 109 ms
+  // (profiles/r3_decomp_gemv_grid_ab.txt)
+  int64_t gc = 1;
+  if (const char* v = getenv("SVM355_GEMV_GC")) gc = atoi(v);
+  if (gc <= 0 || gc > ctiles) gc = ctiles;
+  const int64_t cstride = gc < ctiles ? gc * QBM : 0;
+  const int64_t nwg = 2 * tiles * gc;
   if (ldp < 2 * ctiles || nwg > 0x7FFFFFFF) {
     set_error("igram gemv: bad partial stride or problem too large");
     return SVM_ERR_ARG;
@@ -924,8 +945,8 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
   if (const char* v = getenv("SVM355_GEMV_BK")) bk = atoi(v) == 64 || P.kq % 128 ? 64 : 128;  // A/B knob
 #define SVM_IGRAM_GEMV(EX, B)                                                                                       \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,        \
-                     P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, m, int64_t(0), cols, coef, mcount, Qc, N0c, WNc, \
-                     row_off)
+                     P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, gc * QBM, int64_t(0), cols, coef, mcount, Qc,  \
+                     N0c, WNc, row_off, nullptr, cstride)
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM_GEMV(true, 128); else SVM_IGRAM_GEMV(true, 64);
   } else {
