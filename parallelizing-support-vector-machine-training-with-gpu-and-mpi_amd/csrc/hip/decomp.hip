@@ -668,6 +668,12 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
   double tau_frac = 0.1;
   if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
+  // at 0.5 and above the working set's stop (its gap <= tau_frac x 2 gap) holds before any update, so the
+  // solve could make no progress (it would stop at once with a zero model)
+  if (!(tau_frac >= 0.0 && tau_frac < 0.5)) {
+    set_error("decomposition SMO: SVM355_DECOMP_TAU_FRAC must be in [0, 0.5), got %g", tau_frac);
+    return SVM_ERR_ARG;
+  }
   // SVM355_DECOMP_PROF=1: clock64 phase totals of the inner solves on stderr (diagnostic build)
   const bool prof = getenv("SVM355_DECOMP_PROF") && atoi(getenv("SVM355_DECOMP_PROF")) == 1;
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at

@@ -111,6 +111,17 @@ def test_decomp_refuses_what_it_does_not_cover():
         SVC(device="cuda:0", solver="decomp").fit(tr.compact().X, tr.y, alpha0=np.zeros(tr.n))
 
 
+def test_decomp_rejects_an_inner_stop_that_cannot_progress(monkeypatch):
+    """At tau_frac >= 0.5 the working set's stop holds before any update: an error, not a zero model."""
+    tr = synthetic_mnist(2000, seed=4).compact()
+    monkeypatch.setenv("SVM355_DECOMP_TAU_FRAC", "0.5")
+    with pytest.raises(Exception, match="TAU_FRAC"):
+        SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    monkeypatch.setenv("SVM355_DECOMP_TAU_FRAC", "0.3")
+    m = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    assert m.stop_reason_ == "converged" and len(m.support_) > 0
+
+
 @pytest.mark.parametrize("n,world", [(6000, 2), (6000, 8), (20000, 4)])
 def test_distributed_rehearsal_equals_one_gpu(n, world):
     """P ranks rehearsed on the one GPU (loopback transport, thread ranks): the global block partition
