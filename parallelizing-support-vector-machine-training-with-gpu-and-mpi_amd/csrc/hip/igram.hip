@@ -330,16 +330,21 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   const int32_t* __restrict__ N0b = GEMV ? N0c : N0;
   const double* __restrict__ WNb = GEMV ? WNc : WN;
   const int64_t ntile = RECT ? tiles * ctiles : tiles * (tiles + 1) / 2;
-  const int64_t wg = xcd_remap(blockIdx.x, 2 * ntile);
+  // GEMV with cstride == QBN: one workgroup per row tile walks every column half
+  const bool walk_all = GEMV && cstride == QBN;
+  const int64_t wg = xcd_remap(blockIdx.x, walk_all ? tiles : 2 * ntile);
   int64_t tm, tn;
-  if (RECT) {
+  if (walk_all) {
+    tm = wg;
+    tn = 0;
+  } else if (RECT) {
     tm = (wg >> 1) / ctiles;
     tn = (wg >> 1) - tm * ctiles;
   } else {
     tri_tile(wg >> 1, tiles, tm, tn);
   }
   const int64_t bm_ = tm * QBM;
-  int64_t bn = tn * QBM + (wg & 1) * QBN;
+  int64_t bn = tn * QBM + (walk_all ? 0 : (wg & 1) * QBN);
   // column bound (block-local); GEMV: the device-side count, whole workgroups beyond it exit
   const int64_t ncol = GEMV ? int64_t(*ncount) : RECT ? ncols : n;
   // global row of block column j: c0 + j, or colid[j] (GEMV)
@@ -929,14 +934,17 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
   if (n <= 0 || m <= 0) return SVM_OK;
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
   // the grid covers gc 128-column tiles per row tile; its workgroups walk further halves when *mcount
-  // exceeds them (SVM355_GEMV_GC; 0 = one workgroup per half of all m columns, most exiting at once).
-  // gc = 1 measured best: 113 -> 90 us per call at 60k, the 250k fit 136 -> 109 ms
+  // exceeds them (SVM355_GEMV_GC; 0 = one workgroup per half of all m columns, most exiting at once;
+  // -1, the default = one workgroup per row tile walking every half).  Measured (per call at 60k /
+  // 250k fit): gc 0 113 us / 137 ms, gc 1 90 us / 109 ms, -1 82 us / 98 ms
   // (profiles/r3_decomp_gemv_grid_ab.txt)
-  int64_t gc = 1;
+  int64_t gc = -1;
   if (const char* v = getenv("SVM355_GEMV_GC")) gc = atoi(v);
-  if (gc <= 0 || gc > ctiles) gc = ctiles;
-  const int64_t cstride = gc < ctiles ? gc * QBM : 0;
-  const int64_t nwg = 2 * tiles * gc;
+  const bool walk_all = gc < 0;  // -1: one workgroup per row tile walking every 64-column half
+  if (!walk_all && (gc == 0 || gc > ctiles)) gc = ctiles;
+  const int64_t cstride = walk_all ? QBN : gc < ctiles ? gc * QBM : 0;
+  if (walk_all) gc = 1;
+  const int64_t nwg = walk_all ? tiles : 2 * tiles * gc;
   if (ldp < 2 * ctiles || nwg > 0x7FFFFFFF) {
     set_error("igram gemv: bad partial stride or problem too large");
     return SVM_ERR_ARG;
