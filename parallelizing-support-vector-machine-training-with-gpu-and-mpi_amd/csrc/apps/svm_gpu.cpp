@@ -85,8 +85,19 @@ int main(int argc, char** argv) {
     CK(svmd_preprocess(dev.ctx, Xd, n, d, ld, mn, mx, sqn, 0));
     CK(svmd_memcpy_d2h(dev.ctx, mnh.data(), mn, d * 8));
     CK(svmd_memcpy_d2h(dev.ctx, mxh.data(), mx, d * 8));
-    CK(svmd_train_q(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm, mnh.data(), mxh.data(),
-                    d, o.gram_mode, &int_gram));
+    if (o.solver == 1) {  // working-set decomposition (no stored Gram; exact-integer kernel values)
+      int32_t used = 0;
+      CK(svmd_train_decomp_rows(dev.ctx, Xd, n, ld, d, mnh.data(), mxh.data(), yd, alpha, &o.p, 1024, &r, &tm,
+                                nullptr, &used));
+      if (!used) {
+        fprintf(stderr, "svm_gpu: --solver decomp needs integer pixel rows (an exact-integer kernel plan)\n");
+        return 1;
+      }
+      int_gram = 1;
+    } else {
+      CK(svmd_train_q(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm, mnh.data(), mxh.data(),
+                      d, o.gram_mode, &int_gram));
+    }
     CK(svmd_synchronize(dev.ctx));
     t1 = std::chrono::steady_clock::now();
   }
@@ -145,8 +156,9 @@ int main(int argc, char** argv) {
   printf("The prediction time: %.3f milliseconds\n", pred_ms);
   printf("The elapsed time: %.3f milliseconds\n", train_ms + pred_ms);
   if (!o.quiet)
-    fprintf(stderr, "[svm_gpu] gram %.3f ms (%s), smo %.3f ms, iterations %lld\n", tm.gram_ms,
-            int_gram ? "int8-exact" : "fp64", tm.smo_ms, (long long)r.iterations);
+    fprintf(stderr, "[svm_gpu] %s: gram %.3f ms (%s), smo %.3f ms, iterations %lld\n",
+            o.solver == 1 ? "decomposition" : "pairwise SMO", tm.gram_ms, int_gram ? "int8-exact" : "fp64", tm.smo_ms,
+            (long long)r.iterations);
   if (!o.model_dir.empty()) {
     std::vector<int32_t> lab(static_cast<size_t>(nsv));
     std::vector<double> as(static_cast<size_t>(nsv));
@@ -158,8 +170,8 @@ int main(int argc, char** argv) {
       fprintf(stderr, "%s\n", svm_last_error());
   }
   char extra[256];
-  snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f, \"gram_path\": \"%s\"", tm.gram_ms,
-           tm.smo_ms, int_gram ? "int8-exact" : "fp64");
+  snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f, \"gram_path\": \"%s\", \"solver\": \"%s\"",
+           tm.gram_ms, tm.smo_ms, int_gram ? "int8-exact" : "fp64", o.solver == 1 ? "decomp" : "smo");
   cli::write_json(o.json, "svm_gpu", o, n, d, r, correct, m, train_ms, pred_ms, train_ms + pred_ms, extra);
   return 0;
 }

@@ -61,6 +61,13 @@ SVM_API int svmd_train_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, 
 SVM_API int svmd_train_decomp_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
                                  const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params* p,
                                  int32_t q, svm_result* r, svmd_timing* timing, int64_t* stats, int32_t* used);
+// The same solve from min-max scaled FP64 rows on the device (X_d: n x ld, scaled with the training
+// statistics mn_h / mx_h, e.g. by svmd_preprocess): quantised into the same integers as the uint8 path,
+// so the model is identical.  *used = 0 when the values admit no exact-integer plan.
+SVM_API int svmd_train_decomp_rows(void* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d,
+                                   const double* mn_h, const double* mx_h, const int32_t* y_d, double* alpha_d,
+                                   const svm_params* p, int32_t q, svm_result* r, svmd_timing* timing,
+                                   int64_t* stats, int32_t* used);
 SVM_API int svmd_minmax_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, double* mn_d, double* mx_d);
 SVM_API int svmd_rbf_gram_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
                              const double* mx_h, double gamma, double* K_d, int64_t ldk, int32_t* used);
