@@ -935,10 +935,12 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
   // the grid covers gc 128-column tiles per row tile; its workgroups walk further halves when *mcount
   // exceeds them (SVM355_GEMV_GC; 0 = one workgroup per half of all m columns, most exiting at once;
-  // -1, the default = one workgroup per row tile walking every half).  Measured (per call at 60k /
-  // 250k fit): gc 0 113 us / 137 ms, gc 1 90 us / 109 ms, -1 82 us / 98 ms
+  // -1 = one workgroup per row tile walking every half).  Measured (per call at 60k / 250k fit): gc 0
+  // 113 us / 137 ms, gc 1 90 us / 109 ms, -1 82 us / 98 ms
   // (profiles/r3_decomp_gemv_grid_ab.txt)
-  int64_t gc = -1;
+  // Walking needs enough row tiles to fill the chip: below 256 (fewer than 32k rows, e.g. one GPU's
+  // share in the distributed solve) one workgroup per half keeps every half of every tile in flight.
+  int64_t gc = tiles >= 256 ? -1 : 0;
   if (const char* v = getenv("SVM355_GEMV_GC")) gc = atoi(v);
   const bool walk_all = gc < 0;  // -1: one workgroup per row tile walking every 64-column half
   if (!walk_all && (gc == 0 || gc > ctiles)) gc = ctiles;
