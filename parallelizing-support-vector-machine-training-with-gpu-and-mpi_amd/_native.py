@@ -118,6 +118,64 @@ class SvmCascadeOut(ctypes.Structure):
     ]
 
 
+class SvmDecompTrace(ctypes.Structure):
+    _fields_ = [
+        ("cap", c_int64),
+        ("count", c_int64),
+        ("n", c_int64),
+        ("m", c_void_p),
+        ("W", c_void_p),
+        ("moved", c_void_p),
+        ("cols", c_void_p),
+        ("coef", c_void_p),
+        ("inner", c_void_p),
+        ("bounds", c_void_p),
+        ("alpha", c_void_p),
+        ("f", c_void_p),
+    ]
+
+
+DECOMP_MAX_WS = 1024  # svm355.h SVM_DECOMP_MAX_WS
+
+
+class DecompTrace:
+    """Host buffers of an ``svm_decomp_trace`` (per outer iteration of a decomposition solve: working
+    set, moved columns and coefficients, inner iterations, bounds, optionally alpha / f snapshots)."""
+
+    def __init__(self, cap: int, n: int = 0):
+        import numpy as np
+
+        w = DECOMP_MAX_WS
+        self.m = np.zeros(cap, dtype=np.int32)
+        self.W = np.full((cap, w), -1, dtype=np.int32)
+        self.moved = np.zeros(cap, dtype=np.int32)
+        self.cols = np.full((cap, w), -1, dtype=np.int32)
+        self.coef = np.zeros((cap, w), dtype=np.float64)
+        self.inner = np.zeros(cap, dtype=np.int64)
+        self.bounds = np.zeros((cap, 2), dtype=np.float64)
+        self.alpha = np.zeros((cap, n), dtype=np.float64) if n else None
+        self.f = np.zeros((cap, n), dtype=np.float64) if n else None
+        self.struct = SvmDecompTrace(cap, 0, n, *(ptr(a) for a in (self.m, self.W, self.moved, self.cols, self.coef,
+                                                                    self.inner, self.bounds, self.alpha, self.f)))
+
+    @property
+    def count(self) -> int:
+        return int(self.struct.count)
+
+    def records(self) -> list:
+        """One dict per recorded outer iteration (arrays trimmed to their sizes)."""
+        out = []
+        for o in range(self.count):
+            m, k = int(self.m[o]), int(self.moved[o])
+            rec = {"m": m, "W": self.W[o, :m].copy(), "moved": k, "cols": self.cols[o, :k].copy(),
+                   "coef": self.coef[o, :k].copy(), "inner": int(self.inner[o]), "bounds": self.bounds[o].copy()}
+            if self.alpha is not None:
+                rec["alpha"] = self.alpha[o].copy()
+                rec["f"] = self.f[o].copy()
+            out.append(rec)
+        return out
+
+
 SOLVE_COLS = 12  # svm355.h SVM_CASCADE_SOLVE_COLS
 CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
                   "final", "setup")
@@ -142,6 +200,9 @@ _CORE_SIGS = {
                                 POINTER(SvmResult), _P, c_int64]),
     "svm_smo_train_gram": (c_int32, [_P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
                                      POINTER(SvmResult), _P, c_int64]),
+    "svm_decomp_train_gram": (c_int32, [_P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32, c_double,
+                                        c_int32, POINTER(SvmResult), POINTER(c_int64), POINTER(SvmDecompTrace)]),
+    "svm_decomp_gemv_ref": (c_int32, [_P, c_int64, c_int64, _P, _P, c_int64, _P]),
     "svm_decision": (c_int32, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_double, c_double, _P,
                                c_int32]),
     "svm_sv_indices": (c_int64, [_P, c_int64, c_double, _P]),
@@ -203,6 +264,11 @@ _HIP_SIGS = {
     "svmd_train_decomp_rows": (c_int32, [c_void_p, _P, c_int64, c_int64, c_int64, _P, _P, _P, _P, POINTER(SvmParams),
                                          c_int32, POINTER(SvmResult), POINTER(SvmdTiming), POINTER(c_int64),
                                          POINTER(c_int32)]),
+    "svmd_train_decomp": (c_int32, [c_void_p, _P, c_int32, c_int64, c_int64, c_int64, _P, _P, _P, _P,
+                                    POINTER(SvmParams), c_int32, c_int32, POINTER(SvmResult), POINTER(SvmdTiming),
+                                    POINTER(c_int64), POINTER(c_int32), POINTER(SvmDecompTrace)]),
+    "svmd_decomp_gemv_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, c_double, c_int64, c_int64, _P, _P,
+                                      c_int32, _P, POINTER(c_int32)]),
     "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
     "svmd_cascade_group_decomp": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32, _P,
                                             POINTER(SvmResult), POINTER(c_int64), _P, _P]),

@@ -1,0 +1,378 @@
+// CPU oracle of the working-set decomposition SMO (csrc/hip/decomp.hip), on a precomputed kernel
+// matrix.  Given the device's own kernel values it reproduces the device trajectory bit for bit:
+// every working set, every moved column and coefficient, alpha and f after every outer iteration
+// (tests/test_gpu_decomp_oracle.py).  What has to match, and how:
+//   * selection (ws_select_kernel): blocks of `per` points; per block T rounds of an arg-min over
+//     I_high and an arg-max over I_low in (value, lowest index) order -- a total order, so the
+//     device's thread / wave / workgroup reduction tree gives the lexicographic extreme and so does a
+//     plain scan here;
+//   * build (ws_build_kernel): b_high / b_low over the candidates, the reference's stop test
+//     (main3.cpp:213), the working set = the candidates' ids sorted without duplicates;
+//   * inner solve (ws_inner_kernel): i = argmin f over I_high, j second order (Fan, Chen & Lin gain
+//     -(f_t - b_high)^2 / (2 - 2 K(i, t)), exact division as on the device) or first order, the
+//     reference's clip / eta / update arithmetic (main3.cpp:235-275) with the same operation order
+//     (both sides build with -ffp-contract=off), W's own stop max(tau, tau_frac * gap);
+//   * f update (igram GEMV epilogue + ws_fsum_count_kernel): per row, per 64-column half, lane l's
+//     two terms (columns l and 32 + l) summed from 0, a 32-lane xor butterfly (16, 8, 4, 2, 1), and
+//     the halves added in index order before the one add into f.
+// The kernel values themselves come from the caller (the device Gram on the exact-integer path).
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <limits>
+#include <vector>
+
+#include "internal.h"
+
+using namespace svm355;
+
+namespace {
+
+constexpr int kMaxWS = SVM_DECOMP_MAX_WS;
+constexpr int64_t kSelPts = 256 * 16;  // points per selection block at most (ws_select_kernel)
+
+struct Shape {
+  bool ok = false;
+  int q = 0, T = 0;
+  int64_t NB = 0, per = 0, L = 0;
+};
+
+// decomp_shape (decomp.hip) at world = 1
+Shape shape(int64_t n, int qws) {
+  Shape d;
+  d.q = std::max(4, std::min(qws, kMaxWS));
+  const int64_t nb0 = std::max<int64_t>((n + kSelPts - 1) / kSelPts, std::min<int64_t>(64, (n + 63) / 64));
+  d.NB = (nb0 + 7) / 8 * 8;
+  d.per = (n + d.NB - 1) / d.NB;
+  d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
+  d.L = 2 * d.NB * d.T;
+  d.ok = n >= 2 && n < int64_t(UINT32_MAX) && d.L <= kMaxWS && d.per <= kSelPts;
+  return d;
+}
+
+struct Cand {
+  double f;
+  int32_t id;
+};
+
+// One device GEMV + half-sum pass: f[i] += sum over halves c of half(c, i) (see the header comment).
+void gemv_update(const double* K, int64_t ldk, int64_t n, const int32_t* cols, const double* coef, int64_t cnt,
+                 double* f, WorkerTeam& team) {
+  if (cnt <= 0) return;
+  const int64_t halves = (cnt + 63) / 64;
+  team.parallel_for(n, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      const double* Ki = K + i * ldk;
+      double s = 0.0;
+      for (int64_t c = 0; c < halves; ++c) {
+        double v[32];
+        for (int l = 0; l < 32; ++l) {
+          double r = 0.0;
+          for (int bj = 0; bj < 2; ++bj) {
+            const int64_t j = c * 64 + bj * 32 + l;
+            r += j < cnt ? coef[j] * Ki[cols[j]] : 0.0;
+          }
+          v[l] = r;
+        }
+        for (int off = 16; off > 0; off >>= 1) {
+          double w[32];
+          for (int l = 0; l < 32; ++l) w[l] = v[l] + v[l ^ off];
+          for (int l = 0; l < 32; ++l) v[l] = w[l];
+        }
+        s += v[0];
+      }
+      f[i] += s;
+    }
+  });
+}
+
+}  // namespace
+
+extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n,
+                                             double* alpha, int32_t warm, const svm_params* pp, int32_t qws,
+                                             double tau_frac, int32_t inner_wss, svm_result* res, int64_t* stats,
+                                             svm_decomp_trace* tr) {
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  if (!K || !y || !alpha || n < 2 || ldk < n) {
+    set_error("svm_decomp_train_gram: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  if (!(tau_frac >= 0.0 && tau_frac < 0.5)) {
+    set_error("svm_decomp_train_gram: tau_frac must be in [0, 0.5)");
+    return SVM_ERR_ARG;
+  }
+  const Shape sh = shape(n, qws > 0 ? qws : kMaxWS);
+  if (!sh.ok) {
+    set_error("svm_decomp_train_gram: n = %lld is outside the solver's shapes", (long long)n);
+    return SVM_ERR_ARG;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  WorkerTeam team(std::max<int32_t>(1, std::min<int32_t>(resolve_threads(p.n_threads), int32_t(n / 256) + 1)));
+  const double C = p.C, eps = p.eps, tau = p.tau, c_hi = C - eps, c_lo = 0.0 + eps;
+  const double inf = std::numeric_limits<double>::infinity();
+  auto in_high = [&](int32_t yi, double a) { return (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo); };
+  auto in_low = [&](int32_t yi, double a) { return (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi); };
+
+  // ---- start: cold (alpha = 0, f = -y: ws_init_kernel) or warm (f = -y + K (alpha y) over the
+  // nonzero alphas, ascending, in chunks of kMaxWS columns: decomp.hip's warm start)
+  std::vector<double> f(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) f[size_t(i)] = -static_cast<double>(y[i]);
+  if (!warm) {
+    for (int64_t i = 0; i < n; ++i) alpha[i] = 0.0;
+  } else {
+    std::vector<int32_t> nzc;
+    std::vector<double> nzv;
+    for (int64_t j = 0; j < n; ++j)
+      if (alpha[j] != 0.0) {
+        nzc.push_back(int32_t(j));
+        nzv.push_back(alpha[j] * double(y[j]));
+      }
+    for (size_t c0 = 0; c0 < nzc.size(); c0 += kMaxWS)
+      gemv_update(K, ldk, n, nzc.data() + c0, nzv.data() + c0, int64_t(std::min<size_t>(kMaxWS, nzc.size() - c0)),
+                  f.data(), team);
+  }
+
+  int64_t outer = 0, inner_total = 0, changed_total = 0, last_inner_it = 0;
+  int32_t last_reason = SVM_STOP_CONVERGED, stop = SVM_STOP_RUNNING;
+  double bh = inf, bl = -inf;
+  std::vector<Cand> cand(size_t(sh.L));
+  std::vector<int32_t> W;
+  std::vector<double> a, a0, ft, kh, kl;
+  std::vector<int32_t> yw, cols;
+  std::vector<double> coef;
+  if (tr) tr->count = 0;
+  for (;;) {
+    // ---- selection: per block, T picks per side in (value, lowest index) order
+    const int64_t Lh = sh.NB * sh.T;
+    team.parallel_for(sh.NB, [&](int64_t blo, int64_t bhi) {
+      std::vector<char> th, tl;
+      for (int64_t b = blo; b < bhi; ++b) {
+        const int64_t b0 = b * sh.per, b1 = std::min<int64_t>(n, b0 + sh.per);
+        const int64_t cnt = std::max<int64_t>(0, b1 - b0);
+        th.assign(size_t(cnt), 0);
+        tl.assign(size_t(cnt), 0);
+        for (int k = 0; k < sh.T; ++k) {
+          double mv = inf, xv = -inf;
+          int64_t mi = -1, xi = -1;
+          for (int64_t i = b0; i < b1; ++i) {
+            const double ai = alpha[i], fi = f[size_t(i)];
+            if (!th[size_t(i - b0)] && in_high(y[i], ai) && fi < mv) {
+              mv = fi;
+              mi = i;
+            }
+            if (!tl[size_t(i - b0)] && in_low(y[i], ai) && fi > xv) {
+              xv = fi;
+              xi = i;
+            }
+          }
+          cand[size_t(b * sh.T + k)] = mi >= 0 ? Cand{mv, int32_t(mi)} : Cand{0.0, -1};
+          cand[size_t(Lh + b * sh.T + k)] = xi >= 0 ? Cand{xv, int32_t(xi)} : Cand{0.0, -1};
+          if (mi >= 0) th[size_t(mi - b0)] = 1;
+          if (xi >= 0) tl[size_t(xi - b0)] = 1;
+        }
+      }
+    });
+    // ---- build: bounds, stop test, the sorted de-duplicated working set
+    bh = inf;
+    bl = -inf;
+    std::vector<std::pair<int32_t, double>> ids;
+    ids.reserve(cand.size());
+    for (int64_t t = 0; t < sh.L; ++t) {
+      const Cand& c = cand[size_t(t)];
+      if (c.id < 0) continue;
+      if (t < Lh)
+        bh = std::fmin(bh, c.f);
+      else
+        bl = std::fmax(bl, c.f);
+      ids.emplace_back(c.id, c.f);
+    }
+    std::sort(ids.begin(), ids.end(), [](const auto& u, const auto& v) { return u.first < v.first; });
+    W.clear();
+    std::vector<double> Wf;
+    for (size_t t = 0; t < ids.size(); ++t)
+      if (t == 0 || ids[t].first != ids[t - 1].first) {
+        W.push_back(ids[t].first);
+        Wf.push_back(ids[t].second);
+      }
+    const int m = int(W.size());
+    if (outer > 0 && last_inner_it == 0)
+      stop = last_reason == SVM_STOP_CONVERGED ? SVM_STOP_NO_CANDIDATE : last_reason;
+    else if (!(bh < inf) || !(bl > -inf))
+      stop = SVM_STOP_NO_CANDIDATE;
+    else if (bl <= bh + 2.0 * tau)
+      stop = SVM_STOP_CONVERGED;
+    else if (inner_total + 1 > p.max_iter)
+      stop = SVM_STOP_MAX_ITER;
+    else if (m < 2 || m > kMaxWS) {
+      set_error("svm_decomp_train_gram: working set outside [2, %d]", kMaxWS);
+      return SVM_ERR_INTERNAL;
+    }
+    if (stop != SVM_STOP_RUNNING) break;
+    const double tau_in = std::fmax(tau, tau_frac * (bl - bh));
+    const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
+
+    // ---- inner solve on W (positions 0..m-1 = ascending ids)
+    a.assign(size_t(m), 0.0);
+    yw.assign(size_t(m), 0);
+    ft.assign(Wf.begin(), Wf.end());
+    for (int k = 0; k < m; ++k) {
+      a[size_t(k)] = alpha[W[size_t(k)]];
+      yw[size_t(k)] = y[W[size_t(k)]];
+    }
+    a0 = a;
+    kh.assign(size_t(m), 0.0);
+    kl.assign(size_t(m), 0.0);
+    int64_t it = 0;
+    int32_t reason = SVM_STOP_CONVERGED;
+    for (;;) {
+      double hv = inf, lv = -inf;
+      int ih = -1, il = -1;
+      for (int k = 0; k < m; ++k) {
+        if (in_high(yw[size_t(k)], a[size_t(k)]) && ft[size_t(k)] < hv) {
+          hv = ft[size_t(k)];
+          ih = k;
+        }
+        if (in_low(yw[size_t(k)], a[size_t(k)]) && ft[size_t(k)] > lv) {
+          lv = ft[size_t(k)];
+          il = k;
+        }
+      }
+      if (ih < 0 || il < 0) {
+        reason = SVM_STOP_NO_CANDIDATE;
+        break;
+      }
+      if (lv <= hv + 2.0 * tau_in) break;
+      if (it >= max_inner) {
+        reason = SVM_STOP_MAX_ITER;
+        break;
+      }
+      const double* Ki = K + int64_t(W[size_t(ih)]) * ldk;
+      for (int k = 0; k < m; ++k) kh[size_t(k)] = Ki[W[size_t(k)]];
+      double bl_upd = lv;
+      if (inner_wss != 1) {
+        double gv = inf;
+        int gj = -1;
+        for (int k = 0; k < m; ++k) {
+          if (!in_low(yw[size_t(k)], a[size_t(k)]) || !(ft[size_t(k)] > hv)) continue;
+          const double bb = ft[size_t(k)] - hv;
+          double at = 2.0 - 2.0 * kh[size_t(k)];
+          at = at <= 0.0 ? eps : at;
+          const double gain = -(bb * bb) / at;
+          if (gain < gv) {
+            gv = gain;
+            gj = k;
+          }
+        }
+        if (gj < 0) {
+          reason = SVM_STOP_NO_CANDIDATE;
+          break;
+        }
+        il = gj;
+        bl_upd = ft[size_t(il)];
+      }
+      const double K12 = kh[size_t(il)];
+      const double* Kj = K + int64_t(W[size_t(il)]) * ldk;
+      for (int k = 0; k < m; ++k) kl[size_t(k)] = Kj[W[size_t(k)]];
+      const double ah = a[size_t(ih)], al = a[size_t(il)];
+      const int32_t yh = yw[size_t(ih)], yl = yw[size_t(il)];
+      const int s = yh * yl;
+      const double eta = 1.0 + 1.0 - 2.0 * K12;
+      double U, V;
+      if (s == -1) {
+        U = std::fmax(0.0, al - ah);
+        V = std::fmin(C, C + al - ah);
+      } else {
+        U = std::fmax(0.0, al + ah - C);
+        V = std::fmin(C, al + ah);
+      }
+      if (!(U <= V + 1e-12)) {
+        reason = SVM_STOP_INFEASIBLE;
+        break;
+      }
+      if (eta <= eps) {
+        reason = SVM_STOP_NONPOS_ETA;
+        break;
+      }
+      double al_new = al + double(yl) * (hv - bl_upd) / eta;
+      if (al_new > V) al_new = V;
+      if (al_new < U) al_new = U;
+      const double ah_new = ah + double(s) * (al - al_new);
+      const double ch = (ah_new - ah) * double(yh);
+      const double cl = (al_new - al) * double(yl);
+      for (int k = 0; k < m; ++k) ft[size_t(k)] += ch * kh[size_t(k)] + cl * kl[size_t(k)];
+      a[size_t(ih)] = ah_new;
+      a[size_t(il)] = al_new;
+      ++it;
+    }
+    // ---- moved columns (ascending position = ascending id), alpha written back
+    cols.clear();
+    coef.clear();
+    for (int k = 0; k < m; ++k)
+      if (a[size_t(k)] != a0[size_t(k)]) {
+        alpha[W[size_t(k)]] = a[size_t(k)];
+        cols.push_back(W[size_t(k)]);
+        coef.push_back((a[size_t(k)] - a0[size_t(k)]) * (yw[size_t(k)] == 1 ? 1.0 : -1.0));
+      }
+    ++outer;
+    inner_total += it;
+    changed_total += int64_t(cols.size());
+    last_inner_it = it;
+    last_reason = reason;
+    gemv_update(K, ldk, n, cols.data(), coef.data(), int64_t(cols.size()), f.data(), team);
+    if (tr && tr->count < tr->cap) {
+      const int64_t o = tr->count++;
+      if (tr->m) tr->m[o] = m;
+      if (tr->W)
+        for (int k = 0; k < kMaxWS; ++k) tr->W[o * kMaxWS + k] = k < m ? W[size_t(k)] : -1;
+      if (tr->moved) tr->moved[o] = int32_t(cols.size());
+      for (int k = 0; k < kMaxWS; ++k) {
+        const bool v = k < int(cols.size());
+        if (tr->cols) tr->cols[o * kMaxWS + k] = v ? cols[size_t(k)] : -1;
+        if (tr->coef) tr->coef[o * kMaxWS + k] = v ? coef[size_t(k)] : 0.0;
+      }
+      if (tr->inner) tr->inner[o] = it;
+      if (tr->bounds) {
+        tr->bounds[2 * o] = bh;
+        tr->bounds[2 * o + 1] = bl;
+      }
+      if (tr->n == n && tr->alpha) std::copy(alpha, alpha + n, tr->alpha + o * n);
+      if (tr->n == n && tr->f) std::copy(f.begin(), f.end(), tr->f + o * n);
+    }
+  }
+  if (stats) {
+    stats[0] = outer;
+    stats[1] = inner_total;
+    stats[2] = sh.L;
+    stats[3] = int64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    stats[4] = changed_total;
+    stats[5] = 0;
+  }
+  if (res) {
+    res->iterations = inner_total + 1;
+    res->b_high = bh;
+    res->b_low = bl;
+    res->b = (bh + bl) / 2;
+    res->stop_reason = stop;
+    res->reserved = 0;
+    res->n_sv = svm_sv_indices(alpha, n, p.sv_tol, nullptr);
+    res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return SVM_OK;
+}
+
+// The device f-update GEMV's arithmetic alone (tests): f[i] += sum_k coef[k] K(i, cols[k]), k < cnt,
+// for the n rows of K (row stride ldk), in the device's summation order (gemv_update).
+extern "C" SVM_API int svm_decomp_gemv_ref(const double* K, int64_t ldk, int64_t n, const int32_t* cols,
+                                           const double* coef, int64_t cnt, double* f) {
+  if (!K || n < 0 || cnt < 0 || (cnt > 0 && (!cols || !coef)) || !f) {
+    set_error("svm_decomp_gemv_ref: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  WorkerTeam team(std::max<int32_t>(1, std::min<int32_t>(resolve_threads(0), int32_t(n / 256) + 1)));
+  gemv_update(K, ldk, n, cols, coef, cnt, f, team);
+  return SVM_OK;
+}

@@ -145,7 +145,7 @@ SVM_API int svmd_selftest_exp(void* h, const double* x_d, int64_t n, double* lib
 
 static int release_gram(DeviceCtx* ctx) {
   if (ctx->gram) {
-    SVMD_CHECK(hipSetDevice(ctx->device));
+    ScopedDevice on(ctx->device);
     SVMD_CHECK(hipStreamSynchronize(ctx->stream));
     SVMD_CHECK(hipFree(ctx->gram));
     ctx->gram = nullptr;
@@ -171,7 +171,7 @@ SVM_API int svmd_cache_bytes(void* h, int64_t* gram, int64_t* slab) {
 SVM_API int svmd_release_slab(void* h) {  // the row-cache slab only (the resident Gram stays)
   SVMD_CTX(h);
   if (ctx->rc_cache) {
-    SVMD_CHECK(hipSetDevice(ctx->device));
+    ScopedDevice on(ctx->device);
     SVMD_CHECK(hipStreamSynchronize(ctx->stream));
     SVMD_CHECK(hipFree(ctx->rc_cache));
     ctx->rc_cache = nullptr;

@@ -836,15 +836,16 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   if (mm_out) std::memcpy(mm_out, mmh.data(), size_t(2 * d) * 8);
   // RCCL: the all-gather is only enqueued; the solver's one host wait per outer iteration (after the
   // working-set build that reads the gathered candidates) polls under the transport's deadline
-  DecompAllGather ag;
+  DecompOpts o;
+  o.world = world;
+  o.rank = rank;
   if (tr)
-    ag = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
-          [tr](void* ev) { return tr->event_wait(ev, "decomposition SMO: a batch of outer iterations"); }};
+    o.allgather = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
+                   [tr](void* ev) { return tr->event_wait(ev, "decomposition SMO: a batch of outer iterations"); }};
   bool used = false;
   double prep = 0.0;
   svm_result res{};
-  check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, world, rank,
-                      ag),
+  check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, o),
         "decomposition SMO");
   if (!used) throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan)");
   if (alpha_out) be.d2h(alpha_out, ad, n * 8);

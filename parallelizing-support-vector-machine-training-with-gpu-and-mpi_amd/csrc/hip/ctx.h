@@ -6,6 +6,21 @@
 
 namespace svm355 {
 
+// The calling thread's current device for the scope, restored on exit: entry points that only free or
+// query a context (possibly another GPU's) must not move the caller's (PyTorch's) current device.
+struct ScopedDevice {
+  int prev = -1;
+  explicit ScopedDevice(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~ScopedDevice() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  ScopedDevice(const ScopedDevice&) = delete;
+  ScopedDevice& operator=(const ScopedDevice&) = delete;
+};
+
 struct DeviceCtx {
   int device = 0;
   hipStream_t stream = nullptr;  // private non-blocking stream (graph-capturable)

@@ -28,20 +28,31 @@ struct DecompAllGather {
   explicit operator bool() const { return bool(gather); }
 };
 
+// How a solve runs beyond its problem: the distributed form (world > 1: this GPU's rank and the
+// candidate all-gather), a warm start (alpha holds the start; f = K (alpha y) - y over its nonzero
+// entries), and an optional per-outer-iteration trace (tests; one GPU only, one synchronisation per
+// outer iteration).
+struct DecompOpts {
+  int world = 1, rank = 0;
+  DecompAllGather allgather;
+  bool warm = false;
+  svm_decomp_trace* trace = nullptr;
+};
+
 int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
-               svm_result* r, int64_t* stats, int world = 1, int rank = 0, const DecompAllGather& allgather = {});
+               svm_result* r, int64_t* stats, const DecompOpts& o = {});
 
 // Quantise the device uint8 rows (all n) into the context's grow-only buffer and run the solve.
 // *used = false (nothing done) when the rows' statistics do not admit the exact-integer plan.
 // prep_ms: the quantisation's host-side time.
 int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
                   const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
-                  bool* used, double* prep_ms, int world = 1, int rank = 0, const DecompAllGather& allgather = {});
+                  bool* used, double* prep_ms, const DecompOpts& o = {});
 
 // The same from min-max scaled FP64 rows on the device (X_d: n x ld), one GPU.
 int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
                     const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
-                    int64_t* stats, bool* used, double* prep_ms);
+                    int64_t* stats, bool* used, double* prep_ms, const DecompOpts& o = {});
 
 }  // namespace svm355

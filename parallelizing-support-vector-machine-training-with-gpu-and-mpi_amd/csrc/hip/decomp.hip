@@ -433,7 +433,9 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         const double bb = ft[e] - bh;
         double at = 2.0 - 2.0 * kh[e];
         at = at <= 0.0 ? eps : at;
-        const double gain = -(bb * bb) * __builtin_amdgcn_rcp(at);
+        // IEEE division (not v_rcp_f64): the choice is then reproducible on the host bit for bit
+        // (svm_decomp_train_gram, the CPU oracle)
+        const double gain = -(bb * bb) / at;
         const bool c = in_low && ft[e] > bh && gain < gv;
         gv = c ? gain : gv;
         ge = c ? e : ge;
@@ -604,10 +606,68 @@ __global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __rest
 }
 
 __global__ void ws_init_kernel(const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f,
-                               int64_t lo, int64_t nloc, int64_t n) {
+                               int64_t lo, int64_t nloc, int64_t n, int warm) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) alpha[i] = 0.0;
+  if (i < n && !warm) alpha[i] = 0.0;
   if (i < nloc) f[i] = -static_cast<double>(y[lo + i]);  // main3.cpp:165-172
+}
+
+// Warm start: the ascending ids j with alpha_j != 0 into cols, alpha_j y_j into coef, their number to
+// *count (device) and *count_h (pinned host).  One 1024-thread workgroup; each thread takes 8
+// consecutive points of a 8192-point chunk, a workgroup exclusive scan of the per-thread counts
+// places them (ascending order preserved).
+__global__ __launch_bounds__(1024) void ws_nz_compact_kernel(const double* __restrict__ alpha,
+                                                             const int32_t* __restrict__ y, int64_t n,
+                                                             int32_t* __restrict__ cols, double* __restrict__ coef,
+                                                             int32_t* __restrict__ count, int64_t* __restrict__ count_h) {
+  constexpr int E = 8, NW = 1024 / 64;
+  __shared__ int32_t wtot[NW];
+  __shared__ int64_t base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < n; c0 += int64_t(1024) * E) {
+    const int64_t i0 = c0 + int64_t(t) * E;
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) cnt += (i0 + e < n && alpha[i0 + e] != 0.0) ? 1 : 0;
+    int incl = cnt;  // inclusive wave scan
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    int64_t pos = base + incl - cnt;
+    for (int q = 0; q < w; ++q) pos += wtot[q];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = i0 + e;
+      if (i < n && alpha[i] != 0.0) {
+        cols[pos] = int32_t(i);
+        coef[pos] = alpha[i] * double(y[i]);
+        ++pos;
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      int64_t tot = 0;
+      for (int q = 0; q < NW; ++q) tot += wtot[q];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    *count = int32_t(base);
+    *count_h = base;
+  }
+}
+
+// counts[c] = the columns of warm-start chunk c (kMaxWS per chunk; the last one partial).
+__global__ void ws_chunk_counts_kernel(const int32_t* __restrict__ count, int32_t* __restrict__ counts, int nchunks) {
+  const int c = int(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c < nchunks) counts[c] = max(0, min(kMaxWS, *count - c * kMaxWS));
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -626,6 +686,9 @@ DecompShape decomp_shape(int64_t n, int qws, int world) {
   const int64_t mult = (8 % world == 0) ? 8 : int64_t(8) * world;
   d.NB = (nb0 + mult - 1) / mult * mult;
   d.per = (n + d.NB - 1) / d.NB;
+  // T picks per block and side; at least one, so the working-set capacity L = 2 NB T is the
+  // requested q rounded down to the blocks, or 2 NB when q < 2 NB (every block contributes its extreme
+  // pair: the union must hold the globally maximal violating pair).  stats[2] reports L.
   d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
   d.L = 2 * d.NB * d.T;
   d.ok = n >= 2 && n < int64_t(kSentinel) && d.L <= kMaxWS && d.per <= int64_t(kSelNT) * kSelE && world >= 1;
@@ -639,15 +702,22 @@ DecompShape decomp_shape(int64_t n, int qws, int world) {
 // records once per outer iteration through `allgather`; every GPU then builds the same working set and
 // runs the same inner solve on the same inputs (alpha is replicated and updated identically), and
 // updates f for its own points.  With world dividing 8 the trajectory is the one-GPU trajectory.
-// stats (6 int64): outer iterations, inner iterations, working-set size, solve microseconds, columns
+// stats (6 int64): outer iterations, inner iterations, working-set capacity, solve microseconds, columns
 // of the f updates (points moved, summed over the outer iterations), inner workgroup size.
 int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
-               svm_result* r, int64_t* stats, int world, int rank, const DecompAllGather& allgather) {
+               svm_result* r, int64_t* stats, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   hipStream_t s = ctx->stream;
+  const int world = o.world, rank = o.rank;
+  const DecompAllGather& allgather = o.allgather;
   if (world < 1 || rank < 0 || rank >= world || (world > 1 && !allgather)) {
     set_error("decomposition SMO: bad world / rank / exchange");
+    return SVM_ERR_ARG;
+  }
+  svm_decomp_trace* tr = o.trace;
+  if (tr && (world != 1 || tr->cap < 0 || (tr->n != 0 && tr->n != n))) {
+    set_error("decomposition SMO: a trace needs one GPU and snapshots of n = %lld", (long long)n);
     return SVM_ERR_ARG;
   }
   const DecompShape sh = decomp_shape(n, qws, world);
@@ -694,9 +764,13 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
                o_Kw = take(size_t(kMaxWS) * ldw * 8), o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4),
                o_mcount = take(256), o_part = take(size_t(std::max<int64_t>(nloc, 1)) * ldp * 8),
                o_ctl = take(sizeof(DecompCtl));
+  // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
+  const int64_t nchunks = (n + kMaxWS - 1) / kMaxWS;
+  const size_t o_wcols = o.warm ? take(size_t(n) * 4) : 0, o_wcoef = o.warm ? take(size_t(n) * 8) : 0,
+               o_wcnt = o.warm ? take(size_t(nchunks + 1) * 4) : 0;
   int rc = ctx->ensure_ws(off);
   if (rc) return rc;
-  rc = ctx->ensure_pinned(sizeof(DecompHost) * 2 + 2 * sizeof(DecompCtl));
+  rc = ctx->ensure_pinned(sizeof(DecompHost) * 2 + 2 * sizeof(DecompCtl) + 64);
   if (rc) return rc;
   char* ws = static_cast<char*>(ctx->ws);
   auto* f = reinterpret_cast<double*>(ws + o_f);
@@ -717,14 +791,51 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   auto* ctl_h = reinterpret_cast<DecompCtl*>(static_cast<char*>(ctx->pinned) + sizeof(DecompHost) * 2);
   std::memset(hs, 0, sizeof(DecompHost));
   SVMD_CHECK(hipMemsetAsync(ctl, 0, sizeof(DecompCtl), s));  // stop = SVM_STOP_RUNNING, counters 0
-  hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n);
+  hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n,
+                     int(o.warm));
   SVMD_LAUNCH_CHECK();
+  if (o.warm) {
+    // f = -y + K(:, nz) (alpha y)_nz: the nonzero alphas compacted (ascending ids), then the GEMV in
+    // chunks of kMaxWS columns, each summed into f in order (svm_decomp_train_gram does the same)
+    auto* wcols = reinterpret_cast<int32_t*>(ws + o_wcols);
+    auto* wcoef = reinterpret_cast<double*>(ws + o_wcoef);
+    auto* wcnt = reinterpret_cast<int32_t*>(ws + o_wcnt);
+    auto* nz_h = reinterpret_cast<int64_t*>(static_cast<char*>(ctx->pinned) + sizeof(DecompHost) * 2 +
+                                            2 * sizeof(DecompCtl));
+    *nz_h = -1;
+    hipLaunchKernelGGL(ws_nz_compact_kernel, dim3(1), dim3(1024), 0, s, alpha, y, n, wcols, wcoef, wcnt + nchunks,
+                       nz_h);
+    SVMD_LAUNCH_CHECK();
+    SVMD_CHECK(hipStreamSynchronize(s));  // the one host read of a warm start: how many chunks
+    const int64_t nz = *nz_h;
+    if (nz < 0 || nz > n) {
+      set_error("decomposition SMO: warm-start compaction returned no count");
+      return SVM_ERR_INTERNAL;
+    }
+    const int nch = int((nz + kMaxWS - 1) / kMaxWS);
+    if (nch > 0) {
+      hipLaunchKernelGGL(ws_chunk_counts_kernel, dim3(unsigned((nch + 255) / 256)), dim3(256), 0, s, wcnt + nchunks,
+                         wcnt, nch);
+      SVMD_LAUNCH_CHECK();
+    }
+    for (int c = 0; c < nch && nloc > 0; ++c) {
+      rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN,
+                             wcols + int64_t(c) * kMaxWS, wcoef + int64_t(c) * kMaxWS, wcnt + c, kMaxWS, P, p.gamma,
+                             part, ldp);
+      if (rc) return rc;
+      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp,
+                         wcnt + c, f, nloc);
+      SVMD_LAUNCH_CHECK();
+    }
+  }
+  if (tr) tr->count = 0;
   // Outer iterations are enqueued `batch` at a time (SVM355_DECOMP_BATCH, default 1): every kernel reads
   // the device control block, so after the stop the rest are no-op launches.  Each batch ends with a
   // readback of the control block and an event; the host waits for batch k's event only after it has
   // enqueued batch k + 1, so the GPU always has the next batch queued (no idle host round trip).
   int batch = 1;  // with one batch always queued ahead, 1 already hides the host; more only adds no-op tail
   if (const char* v = getenv("SVM355_DECOMP_BATCH")) batch = std::max(1, atoi(v));
+  if (tr) batch = 1;  // the trace reads every outer iteration back
   int32_t* gate = &ctl->stop;
   const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
@@ -776,6 +887,47 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
     }
+    if (tr) {  // trace: every outer iteration is read back before the next is enqueued
+      SVMD_CHECK(hipMemcpyAsync(ctl_h, ctl, sizeof(DecompCtl), hipMemcpyDeviceToHost, s));
+      SVMD_CHECK(hipStreamSynchronize(s));
+      if (ctl_h->stop != SVM_STOP_RUNNING) {
+        fin = ctl_h;
+        break;
+      }
+      if (tr->count < tr->cap) {
+        const int64_t oi = tr->count++;
+        const int m = ctl_h->m;
+        int32_t mv = 0;
+        SVMD_CHECK(hipMemcpy(&mv, mcount, 4, hipMemcpyDeviceToHost));
+        if (tr->m) tr->m[oi] = m;
+        if (tr->W) {
+          SVMD_CHECK(hipMemcpy(tr->W + oi * kMaxWS, W, size_t(m) * 4, hipMemcpyDeviceToHost));
+          for (int k = m; k < kMaxWS; ++k) tr->W[oi * kMaxWS + k] = -1;
+        }
+        if (tr->moved) tr->moved[oi] = mv;
+        if (tr->cols) {
+          SVMD_CHECK(hipMemcpy(tr->cols + oi * kMaxWS, cols, size_t(mv) * 4, hipMemcpyDeviceToHost));
+          for (int k = mv; k < kMaxWS; ++k) tr->cols[oi * kMaxWS + k] = -1;
+        }
+        if (tr->coef) {
+          SVMD_CHECK(hipMemcpy(tr->coef + oi * kMaxWS, coef, size_t(mv) * 8, hipMemcpyDeviceToHost));
+          for (int k = mv; k < kMaxWS; ++k) tr->coef[oi * kMaxWS + k] = 0.0;
+        }
+        if (tr->inner) tr->inner[oi] = ctl_h->last_inner_it;
+        if (tr->bounds) {
+          tr->bounds[2 * oi] = ctl_h->b_high;
+          tr->bounds[2 * oi + 1] = ctl_h->b_low;
+        }
+        if (tr->n == n && tr->alpha)
+          SVMD_CHECK(hipMemcpy(tr->alpha + oi * n, alpha, size_t(n) * 8, hipMemcpyDeviceToHost));
+        if (tr->n == n && tr->f) SVMD_CHECK(hipMemcpy(tr->f + oi * n, f, size_t(n) * 8, hipMemcpyDeviceToHost));
+      }
+      if (bt >= max_batches) {
+        set_error("decomposition SMO: no stop after %lld outer iterations", (long long)ctl_h->outer);
+        return SVM_ERR_INTERNAL;
+      }
+      continue;
+    }
     SVMD_CHECK(hipMemcpyAsync(ctl_h + (bt & 1), ctl, sizeof(DecompCtl), hipMemcpyDeviceToHost, s));
     SVMD_CHECK(hipEventRecord(ctx->ev_ctl[bt & 1], s));
     if (bt == 0) continue;  // keep one batch queued ahead of the wait
@@ -813,7 +965,7 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   if (stats) {
     stats[0] = outer;
     stats[1] = inner_total;
-    stats[2] = sh.q;
+    stats[2] = sh.L;  // the working-set capacity actually used (see decomp_shape)
     stats[3] = int64_t(ms_since(t0) * 1000.0);
     stats[4] = changed_total;
     stats[5] = inner_nt;
@@ -836,12 +988,11 @@ namespace {
 // The solve after quantisation: step weights to the device, the decomposition, the SV count.
 int decomp_after_quant(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, double* stw,
                        const QuantPlan& P, const int32_t* y_d, double* alpha_d, int64_t n, const svm_params& p, int q,
-                       svm_result* r, int64_t* stats, int world, int rank, const DecompAllGather& allgather) {
+                       svm_result* r, int64_t* stats, const DecompOpts& o) {
   SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
   {
     TraceRange ts("svm355:decomp");
-    const int rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, world, rank,
-                              allgather);
+    const int rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, o);
     if (rc) return rc;
   }
   if (r) {
@@ -886,7 +1037,7 @@ int decomp_quant_buffers(DeviceCtx* ctx, int64_t n, const QuantPlan& P, size_t a
 // path, so the trajectory and the model are the uint8 path's.
 int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
                     const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
-                    int64_t* stats, bool* used, double* prep_ms) {
+                    int64_t* stats, bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
   QuantPlan P;
@@ -905,7 +1056,7 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
   }
   if (!ok) return SVM_OK;
   if (prep_ms) *prep_ms = ms_since(t0);
-  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, 1, 0, {});
+  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, o);
   if (rc) return rc;
   *used = true;
   return SVM_OK;
@@ -913,7 +1064,7 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
 
 int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
                   const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
-                  bool* used, double* prep_ms, int world, int rank, const DecompAllGather& allgather) {
+                  bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
   QuantPlan P;
@@ -932,7 +1083,7 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
   }
   if (!ok) return SVM_OK;
   if (prep_ms) *prep_ms = ms_since(t0);
-  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, world, rank, allgather);
+  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, o);
   if (rc) return rc;
   *used = true;
   return SVM_OK;
@@ -1007,6 +1158,109 @@ SVM_API int svmd_train_decomp_rows(void* h, const double* X_d, int64_t n, int64_
     timing->smo_ms = timing->total_ms - prep;
   }
   if (used_out) *used_out = used ? 1 : 0;
+  return ctx->end();
+}
+
+// The general entry: uint8 rows (is_u8, X_d n x d) or min-max scaled FP64 rows (X_d n x ld), cold or
+// warm start (alpha_d holds the start), an optional per-outer-iteration trace (tests: one
+// synchronisation per outer iteration).  *used = 0 and nothing done without an exact-integer plan.
+SVM_API int svmd_train_decomp(void* h, const void* X_d, int32_t is_u8, int64_t n, int64_t ld, int64_t d,
+                              const double* mn_h, const double* mx_h, const int32_t* y_d, double* alpha_d,
+                              const svm_params* pp, int32_t q, int32_t warm, svm_result* r, svmd_timing* timing,
+                              int64_t* stats, int32_t* used_out, svm_decomp_trace* trace) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!X_d || n < 2 || d <= 0 || (!is_u8 && ld < d) || !mn_h || !mx_h || !y_d || !alpha_d) {
+    set_error("svmd_train_decomp: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ctx->begin();
+  if (rc) return rc;
+  bool used = false;
+  double prep = 0.0;
+  DecompOpts o;
+  o.warm = warm != 0;
+  o.trace = trace;
+  rc = is_u8 ? decomp_fit_u8(ctx, static_cast<const uint8_t*>(X_d), n, d, mn_h, mx_h, y_d, alpha_d, p, q, r, stats,
+                             &used, &prep, o)
+             : decomp_fit_rows(ctx, static_cast<const double*>(X_d), n, ld, d, mn_h, mx_h, y_d, alpha_d, p, q, r,
+                               stats, &used, &prep, o);
+  if (rc) return rc;
+  if (used && timing) {
+    timing->gram_ms = prep;
+    timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    timing->smo_ms = timing->total_ms - prep;
+  }
+  if (used_out) *used_out = used ? 1 : 0;
+  return ctx->end();
+}
+
+// The decomposition solver's f-update GEMV alone (tests): the uint8 rows quantised as a solve would,
+// then f_out[i] = sum_k coef[k] K(lo + i, cols[k]) over k < m for the rows [lo, lo + nloc) -- the GEMV
+// kernel with the device-side count m, its partial halves summed in order (the f update of a solve,
+// from f = 0).  cols / coef / f_out are host arrays; m <= 1024.  *used = 0 without an exact plan.
+SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
+                                const double* mx_h, double gamma, int64_t lo, int64_t nloc, const int32_t* cols_h,
+                                const double* coef_h, int32_t m, double* f_out, int32_t* used_out) {
+  SVMD_CTX(h);
+  if (used_out) *used_out = 0;
+  if (!Xu_d || n < 1 || d <= 0 || lo < 0 || nloc < 1 || lo + nloc > n || m < 1 || m > kMaxWS || !cols_h || !coef_h ||
+      !f_out) {
+    set_error("svmd_decomp_gemv_u8: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  for (int k = 0; k < m; ++k)
+    if (cols_h[k] < 0 || cols_h[k] >= n) {
+      set_error("svmd_decomp_gemv_u8: column %d out of range", cols_h[k]);
+      return SVM_ERR_ARG;
+    }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  QuantPlan P;
+  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return ctx->end();
+  int8_t* Q;
+  int32_t* N0;
+  double *WN, *stw;
+  void* aux;
+  rc = decomp_quant_buffers(ctx, n, P, quantize_u8_aux_bytes(P), &Q, &N0, &WN, &stw, &aux);
+  if (rc) return rc;
+  bool ok = false;
+  rc = quantize_u8_rows(s, Xu_d, n, d, mn_h, mx_h, P, aux, Q, N0, WN, &ok);
+  if (rc) return rc;
+  if (!ok) return ctx->end();
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, s));
+  const int64_t ldp = 2 * (kMaxWS / 128);
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t o_cols = 0, o_coef = al(kMaxWS * 4), o_cnt = o_coef + al(kMaxWS * 8), o_f = o_cnt + 256,
+               o_part = o_f + al(size_t(nloc) * 8), need = o_part + size_t(nloc) * ldp * 8;
+  rc = ctx->ensure_ws(need);
+  if (rc) return rc;
+  char* ws = static_cast<char*>(ctx->ws);
+  auto* cols = reinterpret_cast<int32_t*>(ws + o_cols);
+  auto* coef = reinterpret_cast<double*>(ws + o_coef);
+  auto* cnt = reinterpret_cast<int32_t*>(ws + o_cnt);
+  auto* f = reinterpret_cast<double*>(ws + o_f);
+  auto* part = reinterpret_cast<double*>(ws + o_part);
+  SVMD_CHECK(hipMemcpyAsync(cols, cols_h, size_t(m) * 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(coef, coef_h, size_t(m) * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(cnt, &m, 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemsetAsync(f, 0, size_t(nloc) * 8, s));
+  rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, cnt, kMaxWS,
+                         P, gamma, part, ldp);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f,
+                     nloc);
+  SVMD_LAUNCH_CHECK();
+  SVMD_CHECK(hipMemcpyAsync(f_out, f, size_t(nloc) * 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  if (used_out) *used_out = 1;
   return ctx->end();
 }
 

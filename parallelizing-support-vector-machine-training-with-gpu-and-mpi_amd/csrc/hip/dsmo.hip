@@ -26,7 +26,8 @@
 //   * a rehearsal: P teams in ONE launch on one GPU (uncached receive arrays in its own HBM), which
 //     checks the trajectory and measures the exchange through uncached memory without peers.
 // Every spin is bounded (a peer that never launches or dies ends every workgroup's wait with an
-// error), and svmd_dsmo_selftest runs a small solve against the single-GPU solver before use.
+// error).  Before a timed run, bench.py's preflight solves 4,096 rows distributed and on one GPU and
+// requires the same iterations, b and alphas (bench.py, PREFLIGHT_ROWS).
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>

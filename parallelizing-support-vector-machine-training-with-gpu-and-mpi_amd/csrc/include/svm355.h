@@ -106,6 +106,43 @@ SVM_API int svm_smo_train_gram(const double* K, int64_t ldk, const int32_t* y, i
                                double* alpha, int32_t warm, const svm_params* p, svm_result* r,
                                int64_t* trace, int64_t trace_cap);
 
+// ---------------------------------------------------------------- working-set decomposition (L3)
+// Per-outer-iteration record of a working-set decomposition solve: the device solver's test trace
+// (svmd_train_decomp with a trace) and its CPU oracle's (svm_decomp_train_gram).  Caller-allocated
+// arrays for `cap` outer iterations; the stopping build is not recorded.
+#define SVM_DECOMP_MAX_WS 1024
+typedef struct svm_decomp_trace {
+  int64_t cap;     // capacity in outer iterations
+  int64_t count;   // out: outer iterations recorded
+  int64_t n;       // length of the alpha / f snapshots (0 = none)
+  int32_t* m;      // cap: working-set size
+  int32_t* W;      // cap x SVM_DECOMP_MAX_WS: the working set, ascending ids
+  int32_t* moved;  // cap: points whose alpha changed in the inner solve
+  int32_t* cols;   // cap x SVM_DECOMP_MAX_WS: their ids, ascending
+  double* coef;    // cap x SVM_DECOMP_MAX_WS: (alpha_new - alpha_old) y
+  int64_t* inner;  // cap: inner iterations (pair updates)
+  double* bounds;  // cap x 2: b_high, b_low of the build
+  double* alpha;   // cap x n or NULL: alpha after the outer iteration
+  double* f;       // cap x n or NULL: f after the outer iteration's update
+} svm_decomp_trace;
+
+// CPU oracle of the device decomposition solver (csrc/hip/decomp.hip) on a precomputed kernel matrix
+// K (n x n, row stride ldk; the device's own kernel values for a bit-for-bit comparison): the same
+// block selection, working-set build and stop test, the inner solve's arithmetic and tie rules, and
+// the f update in the device GEMV's summation order.  q: working-set size (<= 1024); tau_frac: inner
+// stop fraction (device default 0.1); inner_wss: 2 = second-order second index (device default), 1 =
+// first order.  warm = 1: alpha holds the start and f = K (alpha y) - y over its nonzero entries in
+// chunks of 1024 columns (the device's warm start).  stats (6 int64, may be NULL) as the device's:
+// outer, inner iterations, working-set capacity, microseconds, moved columns, 0.
+SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
+                                  int32_t warm, const svm_params* p, int32_t q, double tau_frac, int32_t inner_wss,
+                                  svm_result* r, int64_t* stats, svm_decomp_trace* trace);
+
+// The device f-update GEMV's arithmetic alone: f[i] += sum_{k < cnt} coef[k] K(i, cols[k]) for the n
+// rows of K, in the device's summation order (bit-for-bit tests of the GEMV kernel).
+SVM_API int svm_decomp_gemv_ref(const double* K, int64_t ldk, int64_t n, const int32_t* cols, const double* coef,
+                                int64_t cnt, double* f);
+
 // ---------------------------------------------------------------- evaluation (L4)
 // out[i] = sum_k alphas[k]*ys[k]*K(Xq_i, Xs_k) - b, summed in SV order from -b (main3.cpp:391-402).
 SVM_API int svm_decision(const double* Xs, const int32_t* ys, const double* alphas, int64_t nsv,

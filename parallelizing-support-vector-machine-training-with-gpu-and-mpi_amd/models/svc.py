@@ -119,10 +119,11 @@ class SVC:
         device = torch.device(dev)
         decomp = self.solver == "decomp"
         if decomp:
-            if not self.scale or alpha0 is not None:
-                raise ValueError("solver='decomp' needs scale=True and a cold start")
+            if not self.scale:
+                raise ValueError("solver='decomp' needs scale=True (its kernel values come from the scaled rows' "
+                                 "exact-integer plan)")
             if X.dtype == np.uint8:
-                if not self._fit_cuda_u8(X, y, None, device):
+                if not self._fit_cuda_u8(X, y, alpha0, device):
                     raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
                 return
             # FP64 host rows (the reference's format): scaled on the device, then quantised into the
@@ -146,7 +147,8 @@ class SVC:
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
         if decomp:
-            out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set)
+            out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set,
+                                      warm=alpha0 is not None)
             if out is None:
                 raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
             res, tm = out
@@ -201,7 +203,8 @@ class SVC:
         mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
         t1 = time.perf_counter()
         if decomp:
-            out = D.train_decomp_u8(Xu, yd, alpha, self.params, mn_h, mx_h, working_set=self.working_set)
+            out = D.train_decomp_u8(Xu, yd, alpha, self.params, mn_h, mx_h, working_set=self.working_set,
+                                    warm=alpha0 is not None)
         else:
             out = D.train_u8(Xu, yd, alpha, self.params, mn_h, mx_h, warm=alpha0 is not None)
         if out is None:  # nothing ran (not an integer plan): the FP64-row path takes over

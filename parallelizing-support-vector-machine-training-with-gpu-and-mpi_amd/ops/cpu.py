@@ -61,6 +61,28 @@ def smo_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optio
     return a, res, trace
 
 
+def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[np.ndarray] = None,
+                      q: int = 1024, tau_frac: float = 0.1, inner_wss: int = 2, trace_cap: int = 0,
+                      snapshots: bool = False):
+    """CPU oracle of the device decomposition solver (csrc/core/decomp_cpu.cpp) on a kernel matrix K.
+    alpha given = warm start.  Returns (alpha, SMOResult, stats dict, N.DecompTrace or None)."""
+    K = _c64(K)
+    y = _c32(y)
+    n = y.shape[0]
+    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    r = N.SvmResult()
+    st = (ctypes.c_int64 * 6)()
+    tr = N.DecompTrace(trace_cap, n if snapshots else 0) if trace_cap > 0 else None
+    p = params.to_struct()
+    N.check(N.core().svm_decomp_train_gram(N.ptr(K), K.shape[1], N.ptr(y), n, N.ptr(a), int(alpha is not None),
+                                           ctypes.byref(p), int(q), float(tau_frac), int(inner_wss), ctypes.byref(r),
+                                           st, ctypes.byref(tr.struct) if tr is not None else None),
+            "svm_decomp_train_gram")
+    stats = {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
+             "solve_us": int(st[3]), "update_columns": int(st[4])}
+    return a, SMOResult.from_struct(r), stats, tr
+
+
 def rbf_matrix(A: np.ndarray, B: np.ndarray, gamma: float, n_threads: int = 0) -> np.ndarray:
     """Reference-exact RBF kernel matrix (direct sum of squared differences)."""
     A = _c64(A)

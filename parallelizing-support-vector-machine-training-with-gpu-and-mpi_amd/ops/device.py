@@ -402,53 +402,67 @@ def train_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVM
                                       "rows": "uint8"}
 
 
-def train_decomp_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn: torch.Tensor,
-                    mx: torch.Tensor, working_set: int = 1024) -> Optional[Tuple[SMOResult, dict]]:
-    """Working-set decomposition SMO straight from the bytes (svmd_train_decomp_u8, decomp.hip): the
-    reference's stop test on all n points, reached by first-order SMO on working sets of up to
-    ``working_set`` points; no n x n Gram.  Cold start only.  None when the integer plan does not
-    apply."""
-    n, d = Xu.shape
-    ctx = _ctx_for(Xu)
-    a, b, _ = _host_stats(mn, mx)
-    r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
-    st = (ctypes.c_int64 * 6)()
-    p = params.to_struct()
-    N.check(ctx.lib.svmd_train_decomp_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(a), N.ptr(b), N.ptr(y), N.ptr(alpha),
-                                         ctypes.byref(p), int(working_set), ctypes.byref(r), ctypes.byref(tm), st,
-                                         ctypes.byref(used)), "svmd_train_decomp_u8")
-    if not used.value:
-        return None
-    return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
-                                      "kcache": "none", "gram_path": "int8-exact", "rows": "uint8",
-                                      "solver": "decomp", "outer_iterations": int(st[0]),
-                                      "inner_iterations": int(st[1]), "working_set": int(st[2]),
-                                      "update_columns": int(st[4]), "inner_threads": int(st[5])}
-
-
-def train_decomp_rows(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn: torch.Tensor,
-                      mx: torch.Tensor, working_set: int = 1024) -> Optional[Tuple[SMOResult, dict]]:
-    """train_decomp_u8 from min-max scaled FP64 rows on the device (the reference's host row format;
-    svmd_train_decomp_rows): the rows quantise into the same integers, so the trajectory and the model
-    are the uint8 path's.  None when the values admit no exact-integer plan."""
-    _check_rows(X)
+def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn, mx,
+                 working_set: int = 1024, warm: bool = False,
+                 trace: Optional["N.DecompTrace"] = None) -> Optional[Tuple[SMOResult, dict]]:
+    """Working-set decomposition SMO (svmd_train_decomp, decomp.hip): the reference's stop test on all
+    n points, reached by SMO on working sets of up to ``working_set`` points; no n x n Gram.  X: device
+    uint8 pixel rows (n, d), or min-max scaled FP64 rows (n, ld) with ``d`` columns (the reference's host
+    format, d = len(mn); they quantise into the same integers, so trajectory and model are the uint8 path's).
+    warm: alpha holds the start (f = K (alpha y) - y over its nonzero entries).  trace: an
+    ``N.DecompTrace`` filled per outer iteration (tests).  None when no exact-integer plan applies."""
+    u8 = X.dtype == torch.uint8
+    if not u8:
+        _check_rows(X)
     n, ld = X.shape
-    d = int(mn.numel())
     ctx = _ctx_for(X)
-    a, b, _ = _host_stats(mn, mx)
+    a, b, dd = _host_stats(mn, mx)
+    d = ld if u8 else dd
     r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
     st = (ctypes.c_int64 * 6)()
     p = params.to_struct()
-    N.check(ctx.lib.svmd_train_decomp_rows(ctx.bind(), N.ptr(X), n, ld, d, N.ptr(a), N.ptr(b), N.ptr(y), N.ptr(alpha),
-                                           ctypes.byref(p), int(working_set), ctypes.byref(r), ctypes.byref(tm), st,
-                                           ctypes.byref(used)), "svmd_train_decomp_rows")
+    N.check(ctx.lib.svmd_train_decomp(ctx.bind(), N.ptr(X), int(u8), n, ld, d, N.ptr(a), N.ptr(b), N.ptr(y),
+                                      N.ptr(alpha), ctypes.byref(p), int(working_set), int(warm), ctypes.byref(r),
+                                      ctypes.byref(tm), st, ctypes.byref(used),
+                                      ctypes.byref(trace.struct) if trace is not None else None), "svmd_train_decomp")
     if not used.value:
         return None
     return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
-                                      "kcache": "none", "gram_path": "int8-exact", "rows": "fp64",
-                                      "solver": "decomp", "outer_iterations": int(st[0]),
+                                      "kcache": "none", "gram_path": "int8-exact", "rows": "uint8" if u8 else "fp64",
+                                      "solver": "decomp", "warm_start": bool(warm), "outer_iterations": int(st[0]),
                                       "inner_iterations": int(st[1]), "working_set": int(st[2]),
                                       "update_columns": int(st[4]), "inner_threads": int(st[5])}
+
+
+def train_decomp_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn, mx,
+                    working_set: int = 1024, warm: bool = False) -> Optional[Tuple[SMOResult, dict]]:
+    """``train_decomp`` from device uint8 pixel rows."""
+    return train_decomp(Xu, y, alpha, params, mn, mx, working_set, warm)
+
+
+def train_decomp_rows(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn, mx,
+                      working_set: int = 1024, warm: bool = False) -> Optional[Tuple[SMOResult, dict]]:
+    """``train_decomp`` from min-max scaled FP64 rows on the device (the reference's host row format)."""
+    return train_decomp(X, y, alpha, params, mn, mx, working_set, warm)
+
+
+def decomp_gemv_u8(Xu: torch.Tensor, mn, mx, gamma: float, cols: np.ndarray, coef: np.ndarray, lo: int = 0,
+                   nloc: Optional[int] = None) -> Optional[np.ndarray]:
+    """The decomposition solver's f-update GEMV alone (svmd_decomp_gemv_u8): sum_k coef[k] K(i, cols[k])
+    for rows i in [lo, lo + nloc) of the exact-integer kernel, in the solver's summation order.  None
+    when no exact-integer plan applies."""
+    n, d = Xu.shape
+    nloc = n - lo if nloc is None else int(nloc)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    coef = np.ascontiguousarray(coef, dtype=np.float64)
+    out = np.empty(nloc, dtype=np.float64)
+    a, b, _ = _host_stats(mn, mx)
+    used = ctypes.c_int32(0)
+    ctx = _ctx_for(Xu)
+    N.check(ctx.lib.svmd_decomp_gemv_u8(ctx.bind(), N.ptr(Xu), n, d, N.ptr(a), N.ptr(b), float(gamma), int(lo), nloc,
+                                        N.ptr(cols), N.ptr(coef), int(cols.size), N.ptr(out), ctypes.byref(used)),
+            "svmd_decomp_gemv_u8")
+    return out if used.value else None
 
 
 def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:

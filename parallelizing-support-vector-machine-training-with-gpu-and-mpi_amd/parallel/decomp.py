@@ -35,13 +35,11 @@ from ..utils.config import SVMParams
 
 
 def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: int, world: int) -> dict:
-    X = np.ascontiguousarray(X)
-    if X.dtype != np.uint8 or X.ndim != 2:
-        raise ValueError("the distributed decomposition solver needs uint8 pixel rows (n, d)")
-    y = np.ascontiguousarray(y, dtype=np.int32)
+    from ..utils.data import check_labels, pixel_rows
+
+    X = pixel_rows(X, "the distributed decomposition solver")
     n, d = X.shape
-    if y.shape != (n,):
-        raise ValueError("y must be (n,)")
+    y = check_labels(y, n)
     alpha = np.empty(n, dtype=np.float64)
     mm = np.empty(2 * d, dtype=np.float64)
     r = N.SvmResult()

@@ -61,17 +61,11 @@ class DsmoGroup:
 
     def fit(self, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, trace_cap: int = 0) -> dict:
         """Raw solve: alpha (host), result fields, phase times, team shape, column statistics."""
-        if np.asarray(X).dtype != np.uint8:
-            from ..utils.data import compact_pixels
+        from ..utils.data import check_labels, pixel_rows
 
-            Xc = compact_pixels(X)
-            if Xc is None:
-                raise ValueError("the distributed SMO needs integer pixel rows in [0, 255] (exact-integer Gram); "
-                                 "use CascadeSVM for other data")
-            X = Xc
-        X = np.ascontiguousarray(X, dtype=np.uint8)
-        y = np.ascontiguousarray(y, dtype=np.int32)
+        X = pixel_rows(X, "the distributed SMO (use CascadeSVM for other data)")
         n, d = X.shape
+        y = check_labels(y, n)
         params = params or SVMParams()
         p = params.to_struct()
         alpha = np.empty(n, dtype=np.float64)
@@ -205,15 +199,25 @@ class DsmoRank:
         import torch
         import torch.distributed as dist
 
-        X = np.ascontiguousarray(X, dtype=np.uint8)
-        y = np.ascontiguousarray(y, dtype=np.int32)
-        n, d = X.shape
+        from ..utils.data import check_labels, pixel_rows
+
         p = (params or SVMParams()).to_struct()
         lib, err = N.hip(), ""
         ok = torch.ones(1, dtype=torch.int32)
-        if lib.svmd_dsmo_rank_prepare(self.handle, N.ptr(X), 1, N.ptr(y), n, d, ctypes.byref(p)) != 0:
+        try:  # a bad input on any rank fails every rank through the agreement below, not a hang
+            X = pixel_rows(X, "the distributed SMO")
+            n, d = X.shape
+            y = check_labels(y, n)
+        except ValueError as e:
+            ok[0], err = 0, str(e)
+            X = np.zeros((0, 1), dtype=np.uint8)
+            n, d = 0, 1
+        if ok[0] and lib.svmd_dsmo_rank_prepare(self.handle, N.ptr(X), 1, N.ptr(y), n, d, ctypes.byref(p)) != 0:
             ok[0], err = 0, N.last_error()
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # also the launch barrier
+        if not ok[0]:  # every rank learns it here and raises: no collective of mismatched sizes follows
+            raise (ValueError if err.startswith(("the distributed", "y must", "labels")) else N.NativeError)(
+                f"distributed SMO failed on some rank ({err or 'another rank'})")
         alpha = np.zeros(n, dtype=np.float64)
         r = N.SvmResult()
         tm = np.zeros(4, dtype=np.float64)

@@ -62,6 +62,27 @@ def compact_pixels(X: np.ndarray) -> Optional[np.ndarray]:
     return Xc if np.array_equal(Xc, X) else None
 
 
+def check_labels(y, n: int) -> np.ndarray:
+    """y as int32 of shape (n,) with every label +1 or -1 (main3.cpp:49-52 maps the digit labels);
+    ValueError otherwise.  A 0 label falls in neither I_high nor I_low, so a solve would 'converge'
+    to a wrong model instead of failing."""
+    y = np.ascontiguousarray(y)
+    if y.shape != (n,):
+        raise ValueError(f"y must have shape ({n},), got {y.shape}")
+    if not np.all(np.abs(y) == 1):
+        raise ValueError("labels must be +1/-1 (use svm355.utils.data.one_vs_rest)")
+    return y.astype(np.int32, copy=False)
+
+
+def pixel_rows(X, what: str) -> np.ndarray:
+    """X as C-contiguous uint8 (n, d) when every value is an integer in [0, 255]; ValueError naming
+    `what` otherwise (never a silent cast: 3.7 or 300 would be truncated or wrapped)."""
+    Xc = compact_pixels(X)
+    if Xc is None or Xc.ndim != 2:
+        raise ValueError(f"{what} needs integer pixel rows (n, d) in [0, 255] (the exact-integer kernel values)")
+    return np.ascontiguousarray(Xc)
+
+
 def one_vs_rest(labels: np.ndarray, positive_label: int = 1) -> np.ndarray:
     """label == positive_label -> +1, else -1 (main3.cpp:49-52 with positive_label = 1)."""
     return np.where(np.asarray(labels) == positive_label, 1, -1).astype(np.int32)

@@ -1,0 +1,104 @@
+"""CPU oracle of the working-set decomposition solver (csrc/core/decomp_cpu.cpp).
+
+On the GPU the oracle is compared with the device solver bit for bit (tests/test_gpu_decomp_oracle.py).
+Here, on the CPU, it is checked against the problem itself: the reference's stop test recomputed from
+the final alphas, the pairwise CPU oracle's support vectors on the same kernel matrix, and the
+internal consistency of its per-outer-iteration trace (moved columns vs alpha, f vs K (alpha y) - y)."""
+import numpy as np
+import pytest
+
+from svm355 import SVMParams
+from svm355.ops import cpu as C
+from svm355.utils.data import MinMaxScaler, synthetic_mnist
+
+
+def _problem(n, seed):
+    tr = synthetic_mnist(n, seed=seed)
+    X = MinMaxScaler().fit_transform(tr.X)
+    sq = np.einsum("ij,ij->i", X, X)
+    K = np.exp(-0.00125 * np.maximum(sq[:, None] + sq[None, :] - 2.0 * X @ X.T, 0.0))
+    np.fill_diagonal(K, 1.0)
+    return K, tr.y.astype(np.int32)
+
+
+def _gap(K, y, a, p):
+    f = K @ (a * y) - y
+    hi = ((y == 1) & (a < p.C - p.eps)) | ((y == -1) & (a > p.eps))
+    lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < p.C - p.eps))
+    return f[lo].max() - f[hi].min()
+
+
+@pytest.fixture(scope="module")
+def prob2k():
+    return _problem(2000, 11)
+
+
+@pytest.mark.parametrize("q,inner_wss", [(1024, 2), (256, 2), (1024, 1)])
+def test_oracle_meets_the_stop_test_with_the_pairwise_svs(prob2k, q, inner_wss):
+    K, y = prob2k
+    p = SVMParams(n_threads=4)
+    a, r, st, _ = C.decomp_train_gram(K, y, p, q=q, inner_wss=inner_wss)
+    assert r.stop_reason == "converged"
+    assert st["outer_iterations"] >= 1 and r.iterations == st["inner_iterations"] + 1
+    assert _gap(K, y, a, p) <= 2 * p.tau + 1e-9
+    ref, rr, _ = C.smo_train_gram(K, y, p)
+    np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), np.flatnonzero(ref > p.sv_tol))
+    assert abs(r.b - rr.b) <= 10 * p.tau
+    assert np.all((a >= -1e-9) & (a <= p.C + 1e-9))  # the clip arithmetic rounds
+    assert abs(float(a @ y)) < 1e-9 * max(1.0, a.sum())
+
+
+def test_oracle_trace_is_consistent(prob2k):
+    K, y = prob2k
+    p = SVMParams(n_threads=4)
+    a, r, st, tr = C.decomp_train_gram(K, y, p, trace_cap=200, snapshots=True)
+    recs = tr.records()
+    assert len(recs) == st["outer_iterations"]
+    assert sum(x["inner"] for x in recs) == st["inner_iterations"]
+    assert sum(x["moved"] for x in recs) == st["update_columns"]
+    prev = np.zeros_like(a)
+    for x in recs:
+        W = x["W"]
+        assert np.all(np.diff(W) > 0) and x["m"] <= st["working_set"]  # sorted, unique, within the capacity
+        assert np.all(np.isin(x["cols"], W)) and np.all(np.diff(x["cols"]) > 0)
+        d = x["alpha"] - prev
+        moved = np.flatnonzero(d != 0)
+        np.testing.assert_array_equal(moved, x["cols"])
+        np.testing.assert_array_equal(d[moved] * y[moved], x["coef"])  # (a - a0) y, exactly
+        np.testing.assert_allclose(x["f"], K @ (x["alpha"] * y) - y, rtol=0, atol=1e-10)
+        bh, bl = x["bounds"]
+        assert bl > bh + 2 * p.tau  # only running builds are recorded
+        prev = x["alpha"]
+    np.testing.assert_array_equal(prev, a)
+
+
+def test_oracle_warm_start(prob2k):
+    """Warm from its own solution the solve stops at once; warm from a feasible perturbation (a pair
+    moved along y) it converges to the same support vectors."""
+    K, y = prob2k
+    p = SVMParams(n_threads=4)
+    a, r, st, _ = C.decomp_train_gram(K, y, p)
+    a2, r2, st2, _ = C.decomp_train_gram(K, y, p, alpha=a)
+    assert st2["outer_iterations"] == 0 and r2.stop_reason == "converged"
+    np.testing.assert_array_equal(a2, a)
+    i = int(np.flatnonzero((a > 1e-3) & (a < p.C - 1e-3))[0])
+    j = int(np.flatnonzero((y == y[i]) & (a > 1e-3) & (a < p.C - 1e-3) & (np.arange(len(y)) != i))[0])
+    w = a.copy()
+    delta = 0.5 * min(a[i], p.C - a[j])
+    w[i] -= delta
+    w[j] += delta  # same label: sum y alpha unchanged
+    a3, r3, st3, _ = C.decomp_train_gram(K, y, p, alpha=w)
+    assert r3.stop_reason == "converged" and st3["outer_iterations"] >= 1
+    assert _gap(K, y, a3, p) <= 2 * p.tau + 1e-9
+    np.testing.assert_array_equal(np.flatnonzero(a3 > p.sv_tol), np.flatnonzero(a > p.sv_tol))
+
+
+def test_oracle_reports_the_real_working_set_capacity():
+    """q below 2 x blocks: every block still gives its extreme pair, so the capacity is 2 NB, and
+    stats say so (decomp_shape)."""
+    K, y = _problem(6000, 12)
+    p = SVMParams(n_threads=4)
+    a, r, st, tr = C.decomp_train_gram(K, y, p, q=64, trace_cap=400)
+    assert st["working_set"] == 128  # 64 blocks x 2 sides x 1 pick
+    assert max(x["m"] for x in tr.records()) <= 128
+    assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9

@@ -107,8 +107,8 @@ def test_decomp_refuses_what_it_does_not_cover():
     rng = np.random.default_rng(5)
     with pytest.raises(ValueError, match="integer pixel rows"):
         SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64) + rng.random(tr.X.shape) * 0.5, tr.y)
-    with pytest.raises(ValueError, match="cold start"):
-        SVC(device="cuda:0", solver="decomp").fit(tr.compact().X, tr.y, alpha0=np.zeros(tr.n))
+    with pytest.raises(ValueError, match="scale=True"):
+        SVC(device="cuda:0", solver="decomp", scale=False).fit(tr.compact().X, tr.y)
 
 
 def test_decomp_rejects_an_inner_stop_that_cannot_progress(monkeypatch):

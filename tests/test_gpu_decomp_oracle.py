@@ -1,0 +1,132 @@
+"""The decomposition solver's device kernels against host references.
+
+* The f-update GEMV (``igram_tri_kernel`` GEMV mode + ``ws_fsum_count_kernel``) alone, against numpy
+  ``K_exact[:, cols] @ coef`` (1e-13 relative) and bit for bit against the CPU emulation of its
+  summation order (``svm_decomp_gemv_ref``): device-side counts of 1 / 63 / 64 / 65 / 1024 columns, both
+  grid forms (fewer and more than 256 row tiles: n = 20k and 60k) and a distributed slice (row offset).
+* The whole solve against its CPU oracle (``svm_decomp_train_gram``, csrc/core/decomp_cpu.cpp) given
+  the device's own kernel values: every outer iteration's working set, moved columns, coefficients,
+  inner iterations, bounds, alpha and f, bit for bit, at n = 2k / 6k and q = 64 / 512 / 1024, cold and
+  warm started."""
+import numpy as np
+import pytest
+import torch
+
+from svm355 import SVC, SVMParams
+from svm355 import _native as N
+from svm355.ops import cpu as C
+from svm355.ops import device as D
+from svm355.utils.data import synthetic_mnist
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _dev_rows(tr):
+    Xu = D.upload_u8(tr.X, DEV)
+    mmd = torch.empty(2 * tr.d, dtype=torch.float64, device=DEV)
+    mn, mx = D.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    return Xu, mm[: tr.d].copy(), mm[tr.d:].copy()
+
+
+def _exact_gram_host(Xu, mn, mx, n, cols=None):
+    K = D.rbf_gram_u8(Xu, 0.00125, mn, mx)
+    assert K is not None
+    if cols is not None:
+        out = K[:n][:, torch.from_numpy(np.asarray(cols, dtype=np.int64)).to(DEV)].cpu().numpy()
+    else:
+        out = K[:n, :n].cpu().numpy()
+    del K
+    D.release_gram_buffers()
+    torch.cuda.empty_cache()
+    return np.ascontiguousarray(out)
+
+
+@pytest.mark.parametrize("n", [20000, 60000])
+def test_gemv_against_numpy_and_its_summation_order(n):
+    tr = synthetic_mnist(n, seed=31).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    rng = np.random.default_rng(n)
+    allc = np.sort(rng.choice(n, size=1024, replace=False)).astype(np.int32)
+    Ksub = _exact_gram_host(Xu, mn, mx, n, allc)  # K(:, allc), the Gram's own values
+    slices = [(0, n), (7501, 5000)] if n == 20000 else [(0, n)]
+    for m in (1, 63, 64, 65, 1024):
+        pick = np.sort(rng.choice(1024, size=m, replace=False))
+        cols, coef = allc[pick], rng.uniform(-10.0, 10.0, size=m)
+        for lo, nloc in slices:
+            out = D.decomp_gemv_u8(Xu, mn, mx, 0.00125, cols, coef, lo, nloc)
+            assert out is not None
+            rows = np.ascontiguousarray(Ksub[lo:lo + nloc][:, pick])
+            ref = np.zeros(nloc)
+            idx = np.arange(m, dtype=np.int32)  # held: the native call reads it
+            N.check(N.core().svm_decomp_gemv_ref(N.ptr(rows), rows.shape[1], nloc, N.ptr(idx), N.ptr(coef), m,
+                                                 N.ptr(ref)), "svm_decomp_gemv_ref")
+            np.testing.assert_array_equal(out, ref, err_msg=f"n={n} m={m} lo={lo}: summation order")
+            exact = rows @ coef
+            scale = np.abs(rows) @ np.abs(coef)
+            assert np.all(np.abs(out - exact) <= 1e-13 * scale + 1e-300), f"n={n} m={m} lo={lo}"
+
+
+def _compare(dt, ot):
+    dr, orr = dt.records(), ot.records()
+    assert len(dr) == len(orr) and len(dr) > 0
+    for o, (a, b) in enumerate(zip(dr, orr)):
+        assert a["m"] == b["m"], o
+        np.testing.assert_array_equal(a["W"], b["W"], err_msg=f"outer {o}: working set")
+        assert a["inner"] == b["inner"], o
+        np.testing.assert_array_equal(a["bounds"], b["bounds"], err_msg=f"outer {o}: bounds")
+        np.testing.assert_array_equal(a["cols"], b["cols"], err_msg=f"outer {o}: moved columns")
+        np.testing.assert_array_equal(a["coef"], b["coef"], err_msg=f"outer {o}: coefficients")
+        np.testing.assert_array_equal(a["alpha"], b["alpha"], err_msg=f"outer {o}: alpha")
+        np.testing.assert_array_equal(a["f"], b["f"], err_msg=f"outer {o}: f")
+
+
+@pytest.mark.parametrize("n,q", [(2000, 1024), (2000, 64), (6000, 512), (6000, 1024)])
+def test_device_trajectory_equals_the_cpu_oracle(n, q):
+    tr = synthetic_mnist(n, seed=41 + q).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    K = _exact_gram_host(Xu, mn, mx, n)
+    p = SVMParams()
+    yd = torch.from_numpy(tr.y).to(DEV)
+    alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+    dt = N.DecompTrace(400, n)
+    res, tm = D.train_decomp(Xu, yd, alpha, p, mn, mx, working_set=q, trace=dt)
+    a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), q=q, trace_cap=400, snapshots=True)
+    _compare(dt, ot)
+    assert res.stop_reason == r_o.stop_reason == "converged"
+    assert res.iterations == r_o.iterations and res.b == r_o.b
+    np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
+    assert tm["outer_iterations"] == st_o["outer_iterations"] and tm["working_set"] == st_o["working_set"]
+
+
+def test_warm_start_equals_the_oracle_and_meets_the_stop_test():
+    """A cascade-shaped warm start: the solution of the first half (feasible for the whole problem,
+    zero elsewhere) starts the solve on all rows; the device's warm f and trajectory are the oracle's,
+    and the KKT gap recomputed from the exact Gram is within 2 tau."""
+    n = 6000
+    tr = synthetic_mnist(n, seed=55).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    K = _exact_gram_host(Xu, mn, mx, n)
+    p = SVMParams()
+    half = tr.subset(0, n // 2)
+    a_half = SVC(device="cuda:0", solver="decomp").fit(half.X, half.y).alpha_
+    a0 = np.concatenate([a_half, np.zeros(n - n // 2)])
+    yd = torch.from_numpy(tr.y).to(DEV)
+    alpha = torch.from_numpy(a0.copy()).to(DEV)
+    dt = N.DecompTrace(400, n)
+    res, tm = D.train_decomp(Xu, yd, alpha, p, mn, mx, warm=True, trace=dt)
+    a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), alpha=a0, trace_cap=400, snapshots=True)
+    _compare(dt, ot)
+    a = alpha.cpu().numpy()
+    np.testing.assert_array_equal(a, a_o)
+    assert res.stop_reason == "converged" and res.b == r_o.b and tm["warm_start"]
+    y = tr.y.astype(np.float64)
+    f = K @ (a * y) - y
+    hi = ((y == 1) & (a < p.C - p.eps)) | ((y == -1) & (a > p.eps))
+    lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < p.C - p.eps))
+    assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-9
+    cold = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), cold.support_)
+    warm = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y, alpha0=a0)  # the estimator's warm start
+    np.testing.assert_array_equal(warm.alpha_, a)

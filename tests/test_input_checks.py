@@ -1,0 +1,73 @@
+"""Input validation of the distributed entry points (CPU: the checks run before any device work).
+
+SVC.fit rejects labels other than +1/-1 and non-(n, d) shapes (models/svc.py); the distributed
+solvers must too -- a 0 label falls in neither I_high nor I_low (main3.cpp:107-142), so a solve would
+'converge' to a wrong model -- and the integer-row solvers must refuse non-pixel values instead of
+casting them (3.7 -> 3, 300 -> 44)."""
+import datetime
+
+import numpy as np
+import pytest
+
+from svm355.parallel.decomp import _fit_native
+from svm355.parallel.dsmo import DsmoGroup, DsmoRank
+from svm355.utils.config import SVMParams
+from svm355.utils.data import check_labels, pixel_rows
+
+
+def _data(n=8, d=4):
+    rng = np.random.default_rng(0)
+    return rng.integers(0, 256, size=(n, d)).astype(np.uint8), np.where(np.arange(n) % 2 == 0, 1, -1)
+
+
+def test_check_labels_and_pixel_rows():
+    X, y = _data()
+    assert check_labels(y, 8).dtype == np.int32
+    with pytest.raises(ValueError, match=r"\+1/-1"):
+        check_labels(np.where(y > 0, 1, 0), 8)
+    with pytest.raises(ValueError, match="shape"):
+        check_labels(y[:5], 8)
+    assert pixel_rows(X.astype(np.float64), "x").dtype == np.uint8
+    for bad in (X.astype(np.float64) + 0.5, X.astype(np.float64) * 2, -X.astype(np.float64) - 1):
+        with pytest.raises(ValueError, match="integer pixel rows"):
+            pixel_rows(bad, "x")
+
+
+def _never(*a):  # the native solve must not be reached
+    raise AssertionError("native entry point called with invalid input")
+
+
+@pytest.mark.parametrize("bad", ["labels01", "shape", "real_rows", "wrapped_rows"])
+def test_distributed_entry_points_reject_bad_input(bad):
+    X, y = _data()
+    if bad == "labels01":
+        y = np.where(y > 0, 1, 0)
+    elif bad == "shape":
+        y = y[:5]
+    elif bad == "real_rows":
+        X = X.astype(np.float64) + 0.25
+    else:
+        X = X.astype(np.float64) + 200.0  # values above 255 would wrap in a uint8 cast
+    with pytest.raises(ValueError):
+        _fit_native(_never, None, X, y, SVMParams(), 1024, 1)
+    with pytest.raises(ValueError):
+        DsmoGroup.fit(object.__new__(DsmoGroup), X, y)
+
+
+def test_dsmo_rank_agrees_on_a_bad_input_before_any_solve():
+    """The per-process form validates inside its collective protocol: every rank learns of the failure
+    from the first all-reduce and raises (one gloo rank here)."""
+    import torch.distributed as dist
+
+    store = dist.HashStore()
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1, timeout=datetime.timedelta(seconds=30))
+    try:
+        X, y = _data()
+        r = object.__new__(DsmoRank)
+        r.handle = None
+        with pytest.raises(ValueError, match="failed on some rank"):
+            DsmoRank.fit(r, X, np.where(y > 0, 1, 0))
+        with pytest.raises(ValueError, match="failed on some rank"):
+            DsmoRank.fit(r, X.astype(np.float64) + 0.5, y)
+    finally:
+        dist.destroy_process_group()
