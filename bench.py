@@ -20,15 +20,20 @@ domain because MNIST itself is not available offline):
   the other solver's fit next to the headline either way.
 * N > 1, ``--parallel auto`` with the decomposition solver (the default): the distributed
   decomposition solver (every GPU owns 1/N of the selection blocks and of f; one RCCL all-gather of
-  candidate records per outer iteration); bit-identical to the one-GPU decomposition solver.
+  candidate records per outer iteration); bit-identical to the one-GPU decomposition solver.  After
+  it, on the same ranks and under the same bracket (max over ranks), the star and the tree cascade
+  (BASELINE configs 5 and 4, every solve the warm-started decomposition): ``cascade_star_ms``,
+  ``cascade_tree_ms`` and their rounds, SV history and critical path (``--cascade-steps``).
 * N > 1, ``--parallel smo`` (``auto`` with ``--solver smo``): ONE first-order SMO over the N GPUs
   (csrc/hip/dsmo.hip): each GPU owns 1/N of the points and its slab K(:, own) of the exact-integer
   Gram, and the per-iteration arg-min / arg-max candidates cross the GPUs over xGMI -- the same
   problem, the same stop test and the same model as one GPU, bit for bit (strong scaling).
-* N > 1, ``--parallel cascade``: the reference's multi-processor algorithm, the Cascade SVM (modified
-  two-layer star, mpi_svm_main2.cpp, default; ``--topology tree`` = classical mpi_svm_main3.cpp), one
-  rank per GPU over RCCL.  ``auto`` falls back to it when the distributed SMO is not applicable
-  (non-pixel data) or its preflight fails.
+* N > 1, ``--parallel cascade`` (or ``--cascade``): the reference's multi-processor algorithm as the
+  headline, the Cascade SVM (modified two-layer star, mpi_svm_main2.cpp, default; ``--topology tree``
+  = classical mpi_svm_main3.cpp), one rank per GPU over RCCL; every local / merge solve is the
+  warm-started decomposition (``--solver smo``: the reference's pairwise trajectory).  ``auto`` with
+  ``--solver smo`` falls back to it when the distributed SMO is not applicable (non-pixel data) or its
+  preflight fails.
 Launch: directly (``python bench.py --gpus N``: N thread-ranks of this process, one GPU each) or by
 torchrun (WORLD_SIZE = N: one rank per process on GPU LOCAL_RANK; the distributed SMO exchanges the
 receive arrays' IPC handles, the cascade the ncclUniqueId, over the launcher's store).
@@ -58,6 +63,13 @@ REF_GPU_PRED_S = 38.297  # GPU prediction time, 60k train /
 REF_STAR_S = {4: 886.733, 8: 649.773, 16: 440.705, 32: 333.696, 64: 301.263}
 REF_TREE_S = {4: 1194.269, 8: 839.406, 16: 662.153, 32: 671.448, 64: 673.580}
 METRIC = "SMO train time (s) + speedup vs serial, MNIST-60k RBF; accuracy/#SV parity"
+
+
+def ids_digest(ids) -> str:
+    """Short digest of a support-vector id set (order-free), to compare SV sets across runs."""
+    import hashlib
+
+    return hashlib.sha1(np.sort(np.asarray(ids, dtype=np.int64)).tobytes()).hexdigest()[:16]
 PREFLIGHT_ROWS = 4096
 
 
@@ -81,6 +93,10 @@ def main(argv=None):
     ap.add_argument("--input", choices=["u8", "f64"], default="u8",
                     help="host row format: uint8 pixels (default) or FP64 as in the reference")
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
+    ap.add_argument("--cascade-steps", type=int, default=2,
+                    help="N > 1 with the distributed decomposition headline: the star and tree cascades (BASELINE "
+                         "configs 5 / 4) are timed after it with this many fits each, same bracket and max over "
+                         "ranks (0 = skip)")
     ap.add_argument("--baseline-1gpu", type=int, default=3,
                     help="N > 1: single-GPU fits timed after the run for speedup_vs_1gpu (0 = skip)")
     ap.add_argument("--wss", choices=["first", "second"], default="first",
@@ -116,11 +132,11 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
-    if a.solver is None:  # the pairwise solver family for the CPU oracle, the cascade and the distributed SMO
-        a.solver = "smo" if (cpu or a.cascade or a.parallel in ("smo", "cascade")) else "decomp"
-    if a.solver == "decomp" and (cpu or a.cascade or a.parallel in ("smo", "cascade")):
-        print("bench.py: --solver decomp runs on GPUs (N > 1: --parallel auto | decomp); the cascade and the "
-              "distributed pairwise SMO are --solver smo", file=sys.stderr)
+    if a.solver is None:  # the decomposition on GPUs (every cascade solve too); the pairwise SMO on the CPU oracle
+        a.solver = "smo" if (cpu or a.parallel == "smo") else "decomp"
+    if a.solver == "decomp" and (cpu or a.parallel == "smo"):
+        print("bench.py: --solver decomp runs on GPUs; the CPU oracle and the distributed pairwise SMO "
+              "(--parallel smo) are --solver smo", file=sys.stderr)
         return 2
     ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
     if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
@@ -169,7 +185,7 @@ def main(argv=None):
         te = te.compact() if te is not None else None
     pixel = full.X.dtype == np.uint8 and full.X.dtype == part.X.dtype
 
-    mode = "single" if not distributed else a.parallel
+    mode = "single" if not distributed else ("cascade" if a.cascade else a.parallel)
     if mode == "auto" and a.solver == "decomp" and pixel:
         mode = "decomp"  # the headline solver, distributed (bit-identical to its one-GPU trajectory)
     auto = mode == "auto"
@@ -210,7 +226,7 @@ def main(argv=None):
             pre = full.subset(0, min(PREFLIGHT_ROWS, a.n))
             try:
                 m = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(pre.X, pre.y)
-                ref = SVC(device=str(dev)).fit(pre.X, pre.y)
+                ref = SVC(device=str(dev), solver="smo").fit(pre.X, pre.y)
                 if not (m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)):
                     err = (f"preflight differs from the single-GPU solve (iterations {m.n_iter_} vs {ref.n_iter_}, "
                            f"b {m.b_!r} vs {ref.b_!r})")
@@ -273,12 +289,14 @@ def main(argv=None):
             model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
         elif mode == "decomp":
             model = DistributedDecompSVC(a.gpus, group=group, rank=crank).fit(full.X, full.y)
-        elif multiproc:
-            model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit_rank(
-                crank, part.X, part.y, np.arange(lo, hi), a.n)
         else:
-            model = CascadeSVM(params, topology=a.topology, comm_timeout_s=a.comm_timeout).fit(
-                full.X, full.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
+            model = cascade_fit(a.topology)
+
+    def cascade_fit(topology):
+        c = CascadeSVM(params, topology=topology, comm_timeout_s=a.comm_timeout, solver=a.solver)
+        if multiproc:
+            return c.fit_rank(crank, part.X, part.y, np.arange(lo, hi), a.n)
+        return c.fit(full.X, full.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
 
     def guarded_step():
         try:
@@ -352,6 +370,60 @@ def main(argv=None):
 
     ms = elapsed / a.steps * 1e3
     value = ms / 1e3
+
+    # BASELINE configs 5 / 4 (the reference's multi-processor programs, mpi_svm_main2.cpp star and
+    # mpi_svm_main3.cpp tree) on the same ranks after the headline: each timed like the headline steps
+    # (barrier + device sync on both sides, max over ranks), with its rounds, SV history and critical path.
+    cascades = {}
+    if mode == "decomp" and a.cascade_steps > 0 and not cpu:
+        for topo in ("star", "tree"):
+            if topo == "tree" and a.gpus & (a.gpus - 1):
+                cascades[f"cascade_{topo}"] = {"skipped": "the classical cascade needs a power-of-2 number of GPUs"}
+                continue
+            cm = None
+
+            def cstep():
+                nonlocal cm
+                try:
+                    cm = cascade_fit(topo)
+                except Exception as e:  # noqa: BLE001
+                    if multiproc:
+                        print(f"bench.py rank {rank}: cascade ({topo}) failed: {e}", file=sys.stderr, flush=True)
+                        os._exit(1)
+                    raise
+
+            cstep()  # warm
+            barrier_sync()
+            tc = time.perf_counter()
+            for _ in range(a.cascade_steps):
+                cstep()
+            barrier_sync()
+            cel = (time.perf_counter() - tc) / a.cascade_steps
+            if dist is not None:
+                e = torch.tensor([cel], dtype=torch.float64)
+                dist.all_reduce(e, op=dist.ReduceOp.MAX)
+                cel = float(e.item())
+            r = cm.result
+            solves = r.solves
+            if dist is not None:
+                allv = [None] * world_env
+                dist.all_gather_object(allv, solves)
+                solves = [s for v in allv for s in v]
+            crit, crit_ms = critical_path(solves, topo)
+            ref = (REF_STAR_S if topo == "star" else REF_TREE_S).get(a.gpus)
+            rec = {"ms": round(cel * 1e3, 3), "steps": a.cascade_steps, "rounds": r.rounds, "converged": r.converged,
+                   "n_sv": int(len(r.ids)), "sv_ids_digest": ids_digest(r.ids), "b": r.b,
+                   "sv_history": r.sv_history, "solver": cm.solver_used,
+                   "transport": r.transport, "per_round_critical_path": crit, "critical_path_solve_ms": crit_ms,
+                   "speedup_vs_ref_cascade_same_P": round(ref / cel, 2) if ref else None,
+                   "speedup_vs_serial": round(REF_SERIAL_S / cel, 2),
+                   "b_minus_headline_b": float(r.b - model.b_)}
+            if topo == "star":
+                rec["merged_history"] = r.merged_history
+            if rank == 0:
+                rec["accuracy"] = cm.score(te.X, te.y)
+            cascades[f"cascade_{topo}_ms"] = rec["ms"]
+            cascades[f"cascade_{topo}"] = rec
     extra = {}
     if mode == "single":
         # Prediction on the 10k test rows (outside the timed region): H2D, scaling with the training
@@ -447,7 +519,8 @@ def main(argv=None):
             solves = [s for v in allv for s in v]
         crit, crit_ms = critical_path(solves, a.topology)
         r0 = [s for s in solves if s["rank"] == 0]
-        extra = {"n_sv": int(len(r.ids)), "rounds": r.rounds, "b": r.b, "converged": r.converged,
+        extra = {"n_sv": int(len(r.ids)), "sv_ids_digest": ids_digest(r.ids), "solver": model.solver_used,
+                 "rounds": r.rounds, "b": r.b, "converged": r.converged,
                  "sv_history": r.sv_history, "merged_history": r.merged_history,
                  "round_ms": [round(x, 3) for x in r.round_ms], "transport": r.transport,
                  "driver_train_ms": round(r.train_ms, 3), "rank0_phase_ms": r.phase_ms,
@@ -474,7 +547,7 @@ def main(argv=None):
         if dist is not None:
             dist.barrier()
         if rank == 0:
-            one_solver = "decomp" if mode == "decomp" else "smo"
+            one_solver = a.solver if mode in ("decomp", "cascade") else "smo"
             one = SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)  # warm
             ts = []
             for _ in range(a.baseline_1gpu):
@@ -493,6 +566,7 @@ def main(argv=None):
             dist.barrier()
     if auto_selection is not None:
         extra["auto_selection"] = auto_selection
+    extra.update(cascades)
     if distributed and not cpu:
         try:
             from svm355.parallel.rccl import rccl_info

@@ -93,6 +93,9 @@ def _cascade(argv) -> int:
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference) or the opt-in second-order choice")
+    ap.add_argument("--solver", choices=["auto", "decomp", "smo"], default="auto",
+                    help="every local / merge solve: the warm-started working-set decomposition (decomp; auto on "
+                         "GPUs) or the reference's pairwise SMO (smo; auto on --cpu)")
     ap.add_argument("--cpu", action="store_true", help="CPU thread-ranks on the native oracle instead of GPUs")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU; thread-ranks of this process)")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
@@ -110,7 +113,7 @@ def _cascade(argv) -> int:
         args = ["--topology", a.topology, "--gpus", str(max(1, a.gpus)), "--transport", a.transport,
                 "--max-rounds", str(a.max_rounds), "--C", str(a.C), "--gamma", str(a.gamma), "--tau", str(a.tau),
                 "--positive-label", str(a.positive_label), "--seed", str(a.seed), "--comm-timeout", str(a.comm_timeout),
-                "--wss", a.wss]
+                "--wss", a.wss, "--solver", "smo" if a.solver == "smo" else "decomp"]
         if a.synthetic:
             args += ["--synthetic", a.synthetic]
         else:
@@ -146,7 +149,8 @@ def _cascade(argv) -> int:
     params = SVMParams(C=a.C, gamma=a.gamma, tau=a.tau, n_threads=max(1, default_threads() // world),
                        wss=2 if a.wss == "second" else 1)
     model = CascadeSVM(params, topology=a.topology, max_rounds=a.max_rounds, verbose=a.verbose,
-                       checkpoint_dir=a.checkpoint_dir, resume=a.resume, comm_timeout_s=a.comm_timeout)
+                       checkpoint_dir=a.checkpoint_dir, resume=a.resume, comm_timeout_s=a.comm_timeout,
+                       solver=a.solver)
     device = "cpu" if a.cpu else "cuda"
     X = tr.X if a.cpu else tr.compact().X
     crank = None

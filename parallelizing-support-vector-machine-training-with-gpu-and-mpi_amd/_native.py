@@ -84,6 +84,8 @@ class SvmCascadeCfg(ctypes.Structure):
         ("fail_rank", c_int32),
         ("fail_round", c_int32),
         ("fail_stall_s", c_double),
+        ("solver", c_int32),
+        ("reserved", c_int32),
     ]
 
 
@@ -176,7 +178,7 @@ class DecompTrace:
         return out
 
 
-SOLVE_COLS = 12  # svm355.h SVM_CASCADE_SOLVE_COLS
+SOLVE_COLS = 13  # svm355.h SVM_CASCADE_SOLVE_COLS
 CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
                   "final", "setup")
 

@@ -37,7 +37,8 @@ struct Options {
   bool quiet = false;
   int gram_mode = 0;  // svm_gpu: 0 auto (exact-integer int8 MFMA Gram for pixel data), 1 fp64, 2 int
   int warmup = 0;     // svm_gpu: untimed training runs before the timed one
-  int solver = 0;     // svm_gpu: 0 pairwise SMO (the reference's trajectory), 1 working-set decomposition
+  int solver = 1;     // svm_gpu / svm_cascade: 1 working-set decomposition (default), 0 the pairwise SMO (the
+                      // reference's trajectory, --solver smo)
 };
 
 inline void usage(const char* prog) {

@@ -85,15 +85,16 @@ int main(int argc, char** argv) {
     CK(svmd_preprocess(dev.ctx, Xd, n, d, ld, mn, mx, sqn, 0));
     CK(svmd_memcpy_d2h(dev.ctx, mnh.data(), mn, d * 8));
     CK(svmd_memcpy_d2h(dev.ctx, mxh.data(), mx, d * 8));
-    if (o.solver == 1) {  // working-set decomposition (no stored Gram; exact-integer kernel values)
+    if (o.solver == 1) {  // working-set decomposition (the default; no stored Gram)
       int32_t used = 0;
-      CK(svmd_train_decomp_rows(dev.ctx, Xd, n, ld, d, mnh.data(), mxh.data(), yd, alpha, &o.p, 1024, &r, &tm,
-                                nullptr, &used));
+      int64_t st[8] = {};
+      CK(svmd_train_decomp_rows(dev.ctx, Xd, n, ld, d, mnh.data(), mxh.data(), yd, alpha, &o.p, 1024, &r, &tm, st,
+                                &used));
       if (!used) {
-        fprintf(stderr, "svm_gpu: --solver decomp needs integer pixel rows (an exact-integer kernel plan)\n");
+        fprintf(stderr, "svm_gpu: the decomposition solver needs a row stride that is a multiple of 16\n");
         return 1;
       }
-      int_gram = 1;
+      int_gram = st[6] == 0;  // exact-integer kernel values, or FP64 MFMA for real-valued rows
     } else {
       CK(svmd_train_q(dev.ctx, Xd, sqn, n, ld, ld, yd, alpha, 0, &o.p, &r, nullptr, 0, &tm, mnh.data(), mxh.data(),
                       d, o.gram_mode, &int_gram));

@@ -23,6 +23,7 @@ CascadeConfig config_from(const svm_cascade_cfg* c) {
   cfg.fail_rank = c->fail_rank;
   cfg.fail_round = c->fail_round;
   cfg.fail_stall_s = c->fail_stall_s;
+  cfg.solver = c->solver;
   return cfg;
 }
 
@@ -79,7 +80,7 @@ svm_cascade_out* build_cascade_out(const std::vector<const CascadeOutput*>& outs
     for (const SolveLog& s : x->solves)
       solves.insert(solves.end(), {double(s.rank), double(s.round), double(s.layer), double(s.rows),
                                    double(s.iterations), s.ms, s.b, double(s.stop), s.gram_ms,
-                                   s.skipped ? 1.0 : 0.0, s.row_cache ? 1.0 : 0.0, s.solo_ms});
+                                   s.skipped ? 1.0 : 0.0, s.row_cache ? 1.0 : 0.0, s.solo_ms, double(s.solver)});
   }
   static_assert(kNumPhases == sizeof(o->phase_ms) / sizeof(double), "svm_cascade_out.phase_ms size");
   std::copy(R.phase_ms, R.phase_ms + kNumPhases, o->phase_ms);
@@ -112,6 +113,8 @@ SVM_API void svm_cascade_default_cfg(svm_cascade_cfg* c) {
   c->fail_rank = -1;
   c->fail_round = -1;
   c->fail_stall_s = 0.0;
+  c->solver = 0;
+  c->reserved = 0;
 }
 
 SVM_API void svm_cascade_free(svm_cascade_out* o) {

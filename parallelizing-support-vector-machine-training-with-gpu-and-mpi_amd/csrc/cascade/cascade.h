@@ -134,6 +134,7 @@ struct SolveStats {
   int32_t stop = 0;
   double gram_ms = 0.0;
   bool row_cache = false;  // solved on the HBM row cache (the k x k Gram did not fit)
+  int32_t solver = 0;      // the solver that ran: 0 pairwise SMO, 1 working-set decomposition
 };
 
 class Backend {
@@ -176,9 +177,11 @@ class Backend {
       if (a[size_t(i)] > tol) keep->push_back(i);
     *keep_dev = nullptr;
   }
-  // Warm-start SMO (SMO_train(..., init=false), mpi_svm_main3.cpp:155-290) on S: alphas in S.a
-  // are updated in place.  mn_h/mx_h: the global scaling statistics (host, d values).
-  virtual SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) = 0;
+  // Warm-start solve on S (SMO_train(..., init=false), mpi_svm_main3.cpp:155-290): alphas in S.a are
+  // updated in place.  mn_h/mx_h: the global scaling statistics (host, d values).  solver: 0 the
+  // pairwise SMO, 1 the working-set decomposition (CascadeConfig::solver; the stats say which ran).
+  virtual SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h,
+                           int solver) = 0;
   // True when the warm start of S (rows [0, nz) carry every nonzero alpha) provably meets the stop
   // test b_low <= b_high + 2 tau already -- i.e. the solve would end at its first selection without
   // an update -- checked from a cross-kernel K(S, S[0:nz]) only, before any Gram work.  The margin
@@ -361,6 +364,7 @@ struct CascadeConfig {
   // with fail_stall_s > 0 stops responding for that long (its peers' exchanges hit the deadline).
   int fail_rank = -1, fail_round = -1;
   double fail_stall_s = 0.0;
+  int solver = 0;  // svm_cascade_cfg.solver: 0 pairwise SMO, 1 working-set decomposition
 };
 
 // cascade_state.bin layout (little-endian): char magic[8] = "SVM355C2"; int32 topology (0 star,
@@ -378,6 +382,7 @@ struct SolveLog {
   bool skipped = false;  // warm start already met the stop test (Backend::warm_start_converged)
   bool row_cache = false;  // SolveStats::row_cache
   double solo_ms = -1.0;   // Backend::take_solo_ms (skip check + solve), < 0 = not measured
+  int32_t solver = 0;      // SolveStats::solver
 };
 
 // Wall time of this rank per driver phase (host clock; with SVM355_CASCADE_PROFILE=1 every phase

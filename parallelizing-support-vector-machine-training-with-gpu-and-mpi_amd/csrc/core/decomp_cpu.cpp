@@ -120,6 +120,7 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
   // ---- start: cold (alpha = 0, f = -y: ws_init_kernel) or warm (f = -y + K (alpha y) over the
   // nonzero alphas, ascending, in chunks of kMaxWS columns: decomp.hip's warm start)
   std::vector<double> f(static_cast<size_t>(n));
+  int64_t warm_cols = 0;
   for (int64_t i = 0; i < n; ++i) f[size_t(i)] = -static_cast<double>(y[i]);
   if (!warm) {
     for (int64_t i = 0; i < n; ++i) alpha[i] = 0.0;
@@ -131,6 +132,7 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
         nzc.push_back(int32_t(j));
         nzv.push_back(alpha[j] * double(y[j]));
       }
+    warm_cols = int64_t(nzc.size());
     for (size_t c0 = 0; c0 < nzc.size(); c0 += kMaxWS)
       gemv_update(K, ldk, n, nzc.data() + c0, nzv.data() + c0, int64_t(std::min<size_t>(kMaxWS, nzc.size() - c0)),
                   f.data(), team);
@@ -350,6 +352,8 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
     stats[3] = int64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     stats[4] = changed_total;
     stats[5] = 0;
+    stats[6] = 0;
+    stats[7] = warm_cols;
   }
   if (res) {
     res->iterations = inner_total + 1;

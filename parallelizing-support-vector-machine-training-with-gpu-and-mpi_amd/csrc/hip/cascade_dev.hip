@@ -340,7 +340,12 @@ class HipBackend final : public Backend {
     keep->assign(kh, kh + *cnt);
     *keep_dev = static_cast<const int64_t*>(sel_d_);
   }
-  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) override {
+  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h,
+                   int solver) override {
+    if (solver == 1) {  // the decomposition solver keeps no Gram: nothing to size or hand back
+      SolveStats st;
+      if (solo([&] { return solve_decomp(S, d, p, mn_h, mx_h, &st); })) return st;
+    }
     if (!(serial_ && release_gram_)) return solo([&] { return solve_impl(S, d, p, mn_h, mx_h); });
     // Large-n rehearsals of P ranks on one GPU (SVM355_CASCADE_RELEASE_GRAM=1 with serial solves):
     // P resident Grams do not fit together, so each solve's Gram is sized before its timed region
@@ -385,6 +390,27 @@ class HipBackend final : public Backend {
     solo_any_ = true;
     post();
     return r;
+  }
+  // Warm-started working-set decomposition (decomp.hip) on the set's scaled rows: quantised with the
+  // global statistics into the exact-integer plan, f = K (alpha y) - y from the warm alphas by the
+  // solver's GEMV, then the decomposition to the reference's stop test.  False (nothing done) when
+  // the set admits no exact-integer plan or has fewer than 2 rows: the pairwise solve runs instead.
+  bool solve_decomp(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h,
+                    SolveStats* out) {
+    if (S.k < 2 || !mn_h || !mx_h) return false;
+    svm_result r{};
+    int64_t st[kDecompStats] = {};
+    bool used = false;
+    double prep = 0.0;
+    DecompOpts o;
+    o.warm = true;
+    check(decomp_fit_rows(device_ctx(), S.X.as<double>(), S.k, ld(d), d, mn_h, mx_h, S.y.as<int32_t>(),
+                          S.a.as<double>(), p, 1024, &r, st, &used, &prep, o),
+          "decomposition SMO");
+    if (!used) return false;
+    *out = SolveStats{r.iterations, r.b, r.stop_reason, prep};
+    out->solver = 1;
+    return true;
   }
   SolveStats solve_impl(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {
     const int64_t ldd = ld(d);
@@ -1039,7 +1065,7 @@ SVM_API svm_cascade_out* svmd_cascade_group_fit(void* h, const void* X, int32_t 
 
 // Distributed decomposition SMO over the group's ranks: every rank's GPU holds all n uint8 rows (host
 // X, n x d) and owns a block range of f; one candidate all-gather per outer iteration.  alpha_out
-// (host, n doubles) and r come from rank 0 (every rank's alpha is the same replica); stats: 6 int64
+// (host, n doubles) and r come from rank 0 (every rank's alpha is the same replica); stats: 8 int64
 // (decomp.h) from rank 0; rank_ms (world doubles, may be null): each rank's wall time; mm_out (2 d
 // doubles, may be null): the column min / max the model's scaling uses.
 SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,

@@ -135,6 +135,13 @@ int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m,
                     double gamma, double* K, int64_t ldk, bool sym_diag);
 int launch_gemv_rows(hipStream_t s, const double* K, int64_t ldk, int64_t m, int64_t n,
                      const double* coef, double b, double* out);
+// K(A rows, B rows) on FP64 MFMA with device-side controls (decomposition solver, FP64 rows): gate !=
+// 0 -> no-op; B rows bounded by *ncount (<= ncap; whole workgroups beyond exit); sym_diag: K_ii = 1 by
+// position; colid: B row j is training row colid[j], A row i is row_off + i, and that pair's K = 1.
+int launch_rbf_block_dev(hipStream_t s, const double* A, const double* nA, int64_t m, int64_t lda, const double* B,
+                         const double* nB, int64_t ncap, int64_t ldb, int64_t kdim, double gamma, double* K, int64_t ldk,
+                         bool sym_diag, const int32_t* gate, const int32_t* ncount, const int32_t* colid,
+                         int64_t row_off);
 // Exact-integer Gram path (igram.hip).
 struct QuantPlan {
   bool ok = false;

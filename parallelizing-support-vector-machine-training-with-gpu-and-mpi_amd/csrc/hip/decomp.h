@@ -39,9 +39,25 @@ struct DecompOpts {
   svm_decomp_trace* trace = nullptr;
 };
 
-int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
-               const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
-               svm_result* r, int64_t* stats, const DecompOpts& o = {});
+// The rows a solve reads its kernel values from: the exact-integer plan's quantised rows (Q; int8
+// MFMA, igram.hip) or the min-max scaled FP64 rows themselves (X, n x ld, ld a multiple of 16, and
+// their squared norms nrm; FP64 MFMA, gram_mfma.hip) -- the latter for real-valued data.
+struct DecompRows {
+  const int8_t* Q = nullptr;
+  const int32_t* N0 = nullptr;
+  const double* WN = nullptr;
+  const double* stw = nullptr;  // the plan's step weights, on the device
+  const QuantPlan* P = nullptr;
+  const double* X = nullptr;
+  const double* nrm = nullptr;
+  int64_t ld = 0;
+  bool fp64() const { return X != nullptr; }
+};
+
+// stats: SVM_DECOMP_STATS int64 (see run_decomp).
+constexpr int kDecompStats = 8;
+int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* alpha, int64_t n, const svm_params& p,
+               int qws, svm_result* r, int64_t* stats, const DecompOpts& o = {});
 
 // Quantise the device uint8 rows (all n) into the context's grow-only buffer and run the solve.
 // *used = false (nothing done) when the rows' statistics do not admit the exact-integer plan.
@@ -50,7 +66,10 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
                   const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r, int64_t* stats,
                   bool* used, double* prep_ms, const DecompOpts& o = {});
 
-// The same from min-max scaled FP64 rows on the device (X_d: n x ld), one GPU.
+// The same from min-max scaled FP64 rows on the device (X_d: n x ld), one GPU: quantised into the
+// exact-integer plan when the statistics admit one (the uint8 path's integers), else -- real-valued
+// data, or SVM355_DECOMP_F64=1 -- solved on the FP64 rows with FP64-MFMA kernel values (*used = false
+// only when ld is not a multiple of 16).
 int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
                     const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
                     int64_t* stats, bool* used, double* prep_ms, const DecompOpts& o = {});

@@ -592,6 +592,39 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   }
 }
 
+// FP64 rows (real-valued data): Xo[k] = X[ids[k]] (ld doubles) and no[k] = nrm[ids[k]] for k < *count,
+// one workgroup per row; no-op when gated (a stopped solve's remaining launches).
+__global__ __launch_bounds__(64) void ws_gather_f64_kernel(const double* __restrict__ X, const double* __restrict__ nrm,
+                                                           int64_t ld, const int32_t* __restrict__ ids,
+                                                           const int32_t* __restrict__ count,
+                                                           const int32_t* __restrict__ gate, double* __restrict__ Xo,
+                                                           double* __restrict__ no) {
+  const int k = blockIdx.x;
+  if ((gate && *gate != 0) || k >= *count) return;
+  const int64_t src = ids[k];
+  const double2* s = reinterpret_cast<const double2*>(X + src * ld);
+  double2* d = reinterpret_cast<double2*>(Xo + int64_t(k) * ld);
+  for (int64_t c = threadIdx.x; c < ld / 2; c += 64) d[c] = s[c];
+  if (threadIdx.x == 0) no[k] = nrm[src];
+}
+
+// FP64 rows: f[i] += sum_{k < *count} coef[k] Kc[i][k] (the block K(rows, moved columns)), one wave
+// per row, lane-strided then a fixed butterfly (deterministic).
+__global__ __launch_bounds__(256) void ws_rowsum_f64_kernel(const double* __restrict__ Kc, int64_t ldc,
+                                                            const double* __restrict__ coef,
+                                                            const int32_t* __restrict__ count, double* __restrict__ f,
+                                                            int64_t nloc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int cnt = *count;
+  if (row >= nloc || cnt <= 0) return;
+  const double* kr = Kc + row * ldc;
+  double acc = 0.0;
+  for (int k = lane; k < cnt; k += 64) acc += coef[k] * kr[k];
+  acc = wave_sum(acc);
+  if (lane == 0) f[row] += acc;
+}
+
 // f[i] += the first ceil(*mcount / 64) column halves of part (the ones the GEMV wrote).
 __global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __restrict__ part, int64_t ldp,
                                                             const int32_t* __restrict__ mcount,
@@ -702,11 +735,11 @@ DecompShape decomp_shape(int64_t n, int qws, int world) {
 // records once per outer iteration through `allgather`; every GPU then builds the same working set and
 // runs the same inner solve on the same inputs (alpha is replicated and updated identically), and
 // updates f for its own points.  With world dividing 8 the trajectory is the one-GPU trajectory.
-// stats (6 int64): outer iterations, inner iterations, working-set capacity, solve microseconds, columns
-// of the f updates (points moved, summed over the outer iterations), inner workgroup size.
-int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
-               const QuantPlan& P, const int32_t* y, double* alpha, int64_t n, const svm_params& p, int qws,
-               svm_result* r, int64_t* stats, const DecompOpts& o) {
+// stats (kDecompStats int64): outer iterations, inner iterations, working-set capacity, solve
+// microseconds, columns of the f updates (points moved, summed over the outer iterations), inner
+// workgroup size, kernel-value path (0 exact-integer int8 MFMA, 1 FP64 MFMA), warm-start columns.
+int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* alpha, int64_t n, const svm_params& p,
+               int qws, svm_result* r, int64_t* stats, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   hipStream_t s = ctx->stream;
   const int world = o.world, rank = o.rank;
@@ -715,6 +748,16 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     set_error("decomposition SMO: bad world / rank / exchange");
     return SVM_ERR_ARG;
   }
+  const bool f64 = R.fp64();
+  if (f64 ? (R.ld % 16 != 0 || !R.nrm) : (!R.Q || !R.P)) {
+    set_error("decomposition SMO: bad row source");
+    return SVM_ERR_ARG;
+  }
+  static const QuantPlan kNoPlan;
+  const QuantPlan& P = f64 ? kNoPlan : *R.P;
+  const int8_t* Q = R.Q;
+  const int32_t* N0 = R.N0;
+  const double *WN = R.WN, *stw = R.stw;
   svm_decomp_trace* tr = o.trace;
   if (tr && (world != 1 || tr->cap < 0 || (tr->n != 0 && tr->n != n))) {
     set_error("decomposition SMO: a trace needs one GPU and snapshots of n = %lld", (long long)n);
@@ -758,12 +801,18 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     off += al(bytes);
     return o;
   };
-  const size_t o_f = take(size_t(std::max<int64_t>(nloc, 1)) * 8), o_own = take(size_t(Lr) * sizeof(CandRec)),
+  const size_t nl1 = size_t(std::max<int64_t>(nloc, 1));
+  const size_t o_f = take(nl1 * 8), o_own = take(size_t(Lr) * sizeof(CandRec)),
                o_all = take(size_t(sh.L) * sizeof(CandRec)), o_W = take(kMaxWS * 4), o_Wf = take(kMaxWS * 8),
-               o_Qw = take(size_t(kMaxWS) * P.kq), o_N0w = take(kMaxWS * 4), o_WNw = take(kMaxWS * 8),
                o_Kw = take(size_t(kMaxWS) * ldw * 8), o_coef = take(kMaxWS * 8), o_cols = take(kMaxWS * 4),
-               o_mcount = take(256), o_part = take(size_t(std::max<int64_t>(nloc, 1)) * ldp * 8),
-               o_ctl = take(sizeof(DecompCtl));
+               o_mcount = take(256), o_ctl = take(sizeof(DecompCtl));
+  // exact-integer rows: the working set's quantised rows and the GEMV's column-half partials;
+  // FP64 rows: the working set's and the moved columns' rows (+ norms) and the block K(rows, columns)
+  const size_t o_Qw = f64 ? 0 : take(size_t(kMaxWS) * P.kq), o_N0w = f64 ? 0 : take(kMaxWS * 4),
+               o_WNw = f64 ? 0 : take(kMaxWS * 8), o_part = f64 ? 0 : take(nl1 * ldp * 8),
+               o_Xw = f64 ? take(size_t(kMaxWS) * R.ld * 8) : 0, o_nw = f64 ? take(kMaxWS * 8) : 0,
+               o_Xc = f64 ? take(size_t(kMaxWS) * R.ld * 8) : 0, o_nc = f64 ? take(kMaxWS * 8) : 0,
+               o_Kc = f64 ? take(nl1 * kMaxWS * 8) : 0;
   // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
   const int64_t nchunks = (n + kMaxWS - 1) / kMaxWS;
   const size_t o_wcols = o.warm ? take(size_t(n) * 4) : 0, o_wcoef = o.warm ? take(size_t(n) * 8) : 0,
@@ -786,14 +835,45 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
   auto* cols = reinterpret_cast<int32_t*>(ws + o_cols);
   auto* mcount = reinterpret_cast<int32_t*>(ws + o_mcount);
   auto* part = reinterpret_cast<double*>(ws + o_part);
+  auto* Xw = reinterpret_cast<double*>(ws + o_Xw);
+  auto* nw = reinterpret_cast<double*>(ws + o_nw);
+  auto* Xc = reinterpret_cast<double*>(ws + o_Xc);
+  auto* nc = reinterpret_cast<double*>(ws + o_nc);
+  auto* Kc = reinterpret_cast<double*>(ws + o_Kc);
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
+  // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
+  // order) or, for FP64 rows, the moved columns' rows gathered, their block on FP64 MFMA and a row sum
+  auto f_update = [&](const int32_t* cl, const double* cf, const int32_t* cnt) -> int {
+    if (nloc <= 0) return SVM_OK;
+    if (!f64) {
+      const int rc2 = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cl, cf,
+                                        cnt, kMaxWS, P, p.gamma, part, ldp);
+      if (rc2) return rc2;
+      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f,
+                         nloc);
+      SVMD_LAUNCH_CHECK();
+      return SVM_OK;
+    }
+    hipLaunchKernelGGL(ws_gather_f64_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, R.X, R.nrm, R.ld, cl, cnt,
+                       nullptr, Xc, nc);
+    SVMD_LAUNCH_CHECK();
+    const int rc2 = launch_rbf_block_dev(s, R.X + lo * R.ld, R.nrm + lo, nloc, R.ld, Xc, nc, kMaxWS, R.ld, R.ld,
+                                         p.gamma, Kc, kMaxWS, false, nullptr, cnt, cl, lo);
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(ws_rowsum_f64_kernel, dim3(unsigned((nloc + 3) / 4)), dim3(256), 0, s, Kc, int64_t(kMaxWS), cf,
+                       cnt, f, nloc);
+    SVMD_LAUNCH_CHECK();
+    return SVM_OK;
+  };
   auto* hs = static_cast<DecompHost*>(ctx->pinned);
   auto* ctl_h = reinterpret_cast<DecompCtl*>(static_cast<char*>(ctx->pinned) + sizeof(DecompHost) * 2);
   std::memset(hs, 0, sizeof(DecompHost));
   SVMD_CHECK(hipMemsetAsync(ctl, 0, sizeof(DecompCtl), s));  // stop = SVM_STOP_RUNNING, counters 0
+  if (f64) SVMD_CHECK(hipMemsetAsync(Xw, 0, size_t(kMaxWS) * R.ld * 8, s));  // rows beyond m stay finite
   hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n,
                      int(o.warm));
   SVMD_LAUNCH_CHECK();
+  int64_t warm_cols = 0;
   if (o.warm) {
     // f = -y + K(:, nz) (alpha y)_nz: the nonzero alphas compacted (ascending ids), then the GEMV in
     // chunks of kMaxWS columns, each summed into f in order (svm_decomp_train_gram does the same)
@@ -818,15 +898,11 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
                          wcnt, nch);
       SVMD_LAUNCH_CHECK();
     }
-    for (int c = 0; c < nch && nloc > 0; ++c) {
-      rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN,
-                             wcols + int64_t(c) * kMaxWS, wcoef + int64_t(c) * kMaxWS, wcnt + c, kMaxWS, P, p.gamma,
-                             part, ldp);
+    for (int c = 0; c < nch; ++c) {
+      rc = f_update(wcols + int64_t(c) * kMaxWS, wcoef + int64_t(c) * kMaxWS, wcnt + c);
       if (rc) return rc;
-      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp,
-                         wcnt + c, f, nloc);
-      SVMD_LAUNCH_CHECK();
     }
+    warm_cols = nz;
   }
   if (tr) tr->count = 0;
   // Outer iterations are enqueued `batch` at a time (SVM355_DECOMP_BATCH, default 1): every kernel reads
@@ -861,12 +937,22 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
       hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
                          tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount);
       SVMD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, Q, N0, WN, P.kq, W, ctl, Qw, N0w,
-                         WNw);
-      SVMD_LAUNCH_CHECK();
-      // K(W, W) over the full capacity (rows beyond m are never read); skipped once stopped
-      rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
-      if (rc) return rc;
+      if (!f64) {
+        hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, Q, N0, WN, P.kq, W, ctl, Qw, N0w,
+                           WNw);
+        SVMD_LAUNCH_CHECK();
+        // K(W, W) over the full capacity (rows beyond m are never read); skipped once stopped
+        rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
+        if (rc) return rc;
+      } else {
+        hipLaunchKernelGGL(ws_gather_f64_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, R.X, R.nrm, R.ld, W, &ctl->m,
+                           gate, Xw, nw);
+        SVMD_LAUNCH_CHECK();
+        // K(W, W) on FP64 MFMA, columns bounded by m, unit diagonal; skipped once stopped
+        rc = launch_rbf_block_dev(s, Xw, nw, kMaxWS, R.ld, Xw, nw, kMaxWS, R.ld, R.ld, p.gamma, Kw, ldw, true, gate,
+                                  &ctl->m, nullptr, 0);
+        if (rc) return rc;
+      }
       if (inner_nt == 64)
         SVM_WS_INNER(64, 16);
       else if (inner_nt == 128)
@@ -876,14 +962,8 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
       else
         SVM_WS_INNER(512, 2);
       SVMD_LAUNCH_CHECK();
-      if (nloc > 0) {
-        rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, mcount,
-                               kMaxWS, P, p.gamma, part, ldp);
-        if (rc) return rc;
-        hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, mcount,
-                           f, nloc);
-        SVMD_LAUNCH_CHECK();
-      }
+      rc = f_update(cols, coef, mcount);
+      if (rc) return rc;
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
     }
@@ -969,6 +1049,8 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
     stats[3] = int64_t(ms_since(t0) * 1000.0);
     stats[4] = changed_total;
     stats[5] = inner_nt;
+    stats[6] = f64 ? 1 : 0;
+    stats[7] = warm_cols;
   }
   if (r) {
     r->iterations = inner_total + 1;
@@ -986,13 +1068,11 @@ int run_decomp(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double*
 namespace {
 
 // The solve after quantisation: step weights to the device, the decomposition, the SV count.
-int decomp_after_quant(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, double* stw,
-                       const QuantPlan& P, const int32_t* y_d, double* alpha_d, int64_t n, const svm_params& p, int q,
-                       svm_result* r, int64_t* stats, const DecompOpts& o) {
-  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+int decomp_solve(DeviceCtx* ctx, const DecompRows& R, const int32_t* y_d, double* alpha_d, int64_t n,
+                 const svm_params& p, int q, svm_result* r, int64_t* stats, const DecompOpts& o) {
   {
     TraceRange ts("svm355:decomp");
-    const int rc = run_decomp(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, o);
+    const int rc = run_decomp(ctx, R, y_d, alpha_d, n, p, q > 0 ? q : 1024, r, stats, o);
     if (rc) return rc;
   }
   if (r) {
@@ -1030,33 +1110,79 @@ int decomp_quant_buffers(DeviceCtx* ctx, int64_t n, const QuantPlan& P, size_t a
   return SVM_OK;
 }
 
+// The quantised rows' solve: the step weights to the device, then the decomposition.
+int decomp_after_quant(DeviceCtx* ctx, const int8_t* Q, const int32_t* N0, const double* WN, double* stw,
+                       const QuantPlan& P, const int32_t* y_d, double* alpha_d, int64_t n, const svm_params& p, int q,
+                       svm_result* r, int64_t* stats, const DecompOpts& o) {
+  SVMD_CHECK(hipMemcpyAsync(stw, P.step_w.data(), P.step_w.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  DecompRows R;
+  R.Q = Q;
+  R.N0 = N0;
+  R.WN = WN;
+  R.stw = stw;
+  R.P = &P;
+  return decomp_solve(ctx, R, y_d, alpha_d, n, p, q, r, stats, o);
+}
+
 }  // namespace
 
 // The same solve from scaled FP64 rows (X_d: n x ld, the reference's host format, already min-max
 // scaled on the device with mn_h / mx_h): quantize_rows produces the same Q, N0, WN as the uint8
-// path, so the trajectory and the model are the uint8 path's.
+// path, so the trajectory and the model are the uint8 path's.  Rows whose statistics admit no
+// exact-integer plan (real-valued data; SVM355_DECOMP_F64=1 forces it) are solved on the FP64 rows
+// themselves, every kernel value on FP64 MFMA (gram_mfma.hip) -- gpu_svm_main3.cu:119-147's RBF on
+// arbitrary doubles.
 int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, int64_t d, const double* mn_h,
                     const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params& p, int q, svm_result* r,
                     int64_t* stats, bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
+  const char* fe = getenv("SVM355_DECOMP_F64");
+  const bool force_f64 = fe && atoi(fe) == 1;
   QuantPlan P;
-  if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;
-  int8_t* Q;
-  int32_t* N0;
-  double *WN, *stw;
-  void* aux;
-  int rc = decomp_quant_buffers(ctx, n, P, quantize_aux_bytes(P), &Q, &N0, &WN, &stw, &aux);
-  if (rc) return rc;
-  bool ok = false;
-  {
-    TraceRange tr("svm355:quantise");
-    rc = quantize_rows(ctx->stream, X_d, n, ld, P, aux, Q, N0, WN, &ok);
+  if (!force_f64 && mn_h && mx_h && plan_quant(mn_h, mx_h, d, &P) && P.kq <= 32 * 128) {
+    int8_t* Q;
+    int32_t* N0;
+    double *WN, *stw;
+    void* aux;
+    int rc = decomp_quant_buffers(ctx, n, P, quantize_aux_bytes(P), &Q, &N0, &WN, &stw, &aux);
     if (rc) return rc;
+    bool ok = false;
+    {
+      TraceRange tr("svm355:quantise");
+      rc = quantize_rows(ctx->stream, X_d, n, ld, P, aux, Q, N0, WN, &ok);
+      if (rc) return rc;
+    }
+    if (ok) {
+      if (prep_ms) *prep_ms = ms_since(t0);
+      rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, o);
+      if (rc) return rc;
+      *used = true;
+      return SVM_OK;
+    }
   }
-  if (!ok) return SVM_OK;
+  if (ld % 16 != 0 || ld < d || o.world != 1) return SVM_OK;  // the FP64 block kernel's k-steps
+  // FP64 rows: their squared norms in the context's grow-only buffer, then the solve
+  const size_t need = size_t(n) * 8;
+  if (need > ctx->gram_bytes) {
+    if (ctx->gram) {
+      SVMD_CHECK(hipStreamSynchronize(ctx->stream));
+      SVMD_CHECK(hipFree(ctx->gram));
+      ctx->gram = nullptr;
+      ctx->gram_bytes = 0;
+    }
+    SVMD_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->gram), need));
+    ctx->gram_bytes = need;
+  }
+  auto* nrm = reinterpret_cast<double*>(ctx->gram);
+  int rc = launch_scale_norms(ctx->stream, const_cast<double*>(X_d), n, d, ld, nullptr, nullptr, nrm);
+  if (rc) return rc;
   if (prep_ms) *prep_ms = ms_since(t0);
-  rc = decomp_after_quant(ctx, Q, N0, WN, stw, P, y_d, alpha_d, n, p, q, r, stats, o);
+  DecompRows R;
+  R.X = X_d;
+  R.nrm = nrm;
+  R.ld = ld;
+  rc = decomp_solve(ctx, R, y_d, alpha_d, n, p, q, r, stats, o);
   if (rc) return rc;
   *used = true;
   return SVM_OK;
@@ -1097,7 +1223,7 @@ extern "C" {
 
 // Decomposition SMO straight from uint8 pixel rows (exact-integer kernel values, no stored Gram).
 // *used = 0 and nothing done when the rows' statistics do not admit the integer plan.  stats
-// (optional, 6 int64): see run_decomp.
+// (optional, 8 int64): see run_decomp.
 SVM_API int svmd_train_decomp_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
                                  const double* mx_h, const int32_t* y_d, double* alpha_d, const svm_params* pp,
                                  int32_t q, svm_result* r, svmd_timing* timing, int64_t* stats, int32_t* used_out) {

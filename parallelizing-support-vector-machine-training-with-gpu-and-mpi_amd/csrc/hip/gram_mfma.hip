@@ -34,9 +34,16 @@ template <bool SYM, bool TRI>
 __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
     const double* __restrict__ A, const double* __restrict__ nA, int64_t m, int64_t lda,
     const double* __restrict__ B, const double* __restrict__ nB, int64_t n, int64_t ldb, int64_t kdim,
-    double neg_gamma, double* __restrict__ K, int64_t ldk, int64_t tiles_m, int64_t tiles_n) {
+    double neg_gamma, double* __restrict__ K, int64_t ldk, int64_t tiles_m, int64_t tiles_n,
+    const int32_t* __restrict__ gate = nullptr, const int32_t* __restrict__ ncount = nullptr,
+    const int32_t* __restrict__ colid = nullptr, int64_t row_off = 0) {
   __shared__ __attribute__((aligned(16))) double As[BM * LS];
   __shared__ __attribute__((aligned(16))) double Bs[BN * LS];
+  // Decomposition solver (decomp.hip, FP64 rows): gate = a stopped solve's remaining launches are
+  // no-ops; ncount = a device-side bound on the B rows (whole workgroups beyond it exit); colid = B
+  // row j is training row colid[j] (A row i is row_off + i): that pair's value is the diagonal, 1.
+  if (gate && *gate != 0) return;
+  if (ncount) n = std::min<int64_t>(n, int64_t(*ncount));
 
   int64_t tm, tn;
   if (TRI) {
@@ -52,6 +59,7 @@ __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
     tn = (wg % band) / gsz;
   }
   const int64_t bm = tm * BM, bn = tn * BN;
+  if (ncount && bn >= n) return;
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   const int lr = lane & 15, lg = lane >> 4;
@@ -143,6 +151,7 @@ __global__ __launch_bounds__(256, 2) void rbf_gram_kernel(
         dist = dist > 0.0 ? dist : 0.0;
         kv[r] = exp(neg_gamma * dist);
         if (SYM && gi == gj) kv[r] = 1.0;
+        if (!SYM && colid && gj < n && gi + row_off == int64_t(colid[gj])) kv[r] = 1.0;
         if (gi < m && gj < n) K[gi * ldk + gj] = kv[r];
       }
       if (mirror) {
@@ -256,6 +265,33 @@ int launch_rbf_gram(hipStream_t s, const double* A, const double* nA, int64_t m,
   else
     hipLaunchKernelGGL((rbf_gram_kernel<false, false>), dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
                        n, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n);
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
+
+int launch_rbf_block_dev(hipStream_t s, const double* A, const double* nA, int64_t m, int64_t lda, const double* B,
+                         const double* nB, int64_t ncap, int64_t ldb, int64_t kdim, double gamma, double* K, int64_t ldk,
+                         bool sym_diag, const int32_t* gate, const int32_t* ncount, const int32_t* colid,
+                         int64_t row_off) {
+  if (m <= 0 || ncap <= 0) return SVM_OK;
+  if (kdim % BK || lda < kdim || ldb < kdim || ldk < ncap || (lda % 2) || (ldb % 2) ||
+      (reinterpret_cast<uintptr_t>(A) & 15) || (reinterpret_cast<uintptr_t>(B) & 15)) {
+    set_error("rbf block: kdim must be a multiple of %d, lda/ldb even and >= kdim, ldk >= ncap, A/B 16-byte aligned",
+              BK);
+    return SVM_ERR_ARG;
+  }
+  const int64_t tiles_m = (m + BM - 1) / BM, tiles_n = (ncap + BN - 1) / BN;
+  const int64_t nwg = tiles_m * tiles_n;
+  if (nwg > 0x7FFFFFFF) {
+    set_error("rbf block: problem too large for one launch");
+    return SVM_ERR_ARG;
+  }
+  if (sym_diag)
+    hipLaunchKernelGGL((rbf_gram_kernel<true, false>), dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
+                       ncap, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n, gate, ncount, colid, row_off);
+  else
+    hipLaunchKernelGGL((rbf_gram_kernel<false, false>), dim3(unsigned(nwg)), dim3(256), 0, s, A, nA, m, lda, B, nB,
+                       ncap, ldb, kdim, -gamma, K, ldk, tiles_m, tiles_n, gate, ncount, colid, row_off);
   SVMD_LAUNCH_CHECK();
   return SVM_OK;
 }

@@ -132,8 +132,8 @@ typedef struct svm_decomp_trace {
 // the f update in the device GEMV's summation order.  q: working-set size (<= 1024); tau_frac: inner
 // stop fraction (device default 0.1); inner_wss: 2 = second-order second index (device default), 1 =
 // first order.  warm = 1: alpha holds the start and f = K (alpha y) - y over its nonzero entries in
-// chunks of 1024 columns (the device's warm start).  stats (6 int64, may be NULL) as the device's:
-// outer, inner iterations, working-set capacity, microseconds, moved columns, 0.
+// chunks of 1024 columns (the device's warm start).  stats (8 int64, may be NULL) as the device's:
+// outer, inner iterations, working-set capacity, microseconds, moved columns, 0, 0, warm-start columns.
 SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,
                                   int32_t warm, const svm_params* p, int32_t q, double tau_frac, int32_t inner_wss,
                                   svm_result* r, int64_t* stats, svm_decomp_trace* trace);
@@ -170,9 +170,14 @@ typedef struct svm_cascade_cfg {
   int32_t fail_rank;       // fault injection: this rank fails at the start of fail_round (-1 = off):
   int32_t fail_round;      //   it throws, or with fail_stall_s > 0 it stops responding for that long
   double fail_stall_s;     //   (the others then hit comm_timeout_s)
+  int32_t solver;          // every local / merge solve: 0 = the pairwise first-order SMO (the reference's
+                           //   trajectory, default), 1 = the warm-started working-set decomposition
+                           //   (device backend: decomp.hip; CPU backend: its oracle on the set's kernel
+                           //   matrix; sets without an exact-integer plan on the device fall back to 0)
+  int32_t reserved;
 } svm_cascade_cfg;
 
-#define SVM_CASCADE_SOLVE_COLS 12
+#define SVM_CASCADE_SOLVE_COLS 13
 // Result of a cascade fit (allocated by the library, release with svm_cascade_free).
 typedef struct svm_cascade_out {
   int32_t world, rank, rounds, converged;
@@ -195,7 +200,8 @@ typedef struct svm_cascade_out {
                            //   -1 merge, tree step), rows, SMO iterations, ms, b, stop reason, of ms
                            //   the kernel matrix, skipped (warm start already optimal), row cache
                            //   (solved on kernel rows computed on demand: the Gram did not fit),
-                           //   solo ms (device time alone, serial-solve rehearsals; < 0 otherwise)
+                           //   solo ms (device time alone, serial-solve rehearsals; < 0 otherwise),
+                           //   solver (0 pairwise SMO, 1 decomposition)
   int64_t n_ranks;
   double* rank_train_ms;   // train_ms of each rank this call drove
   char transport[16];

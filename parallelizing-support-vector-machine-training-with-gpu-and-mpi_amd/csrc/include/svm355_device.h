@@ -55,7 +55,7 @@ SVM_API int svmd_train_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, 
                           int32_t* used);
 // Working-set decomposition SMO (decomp.hip, opt-in): working sets of up to q <= 1024 points solved
 // in one workgroup, f updated by the exact-integer kernel values against the working set; no stored
-// Gram.  *used = 0 when the rows are not integer pixels.  stats (optional, 6 int64): outer
+// Gram.  *used = 0 when the rows are not integer pixels.  stats (optional, 8 int64): outer
 // iterations, inner iterations, working-set size, solve microseconds, f-update columns (points
 // moved, summed over the outer iterations), inner workgroup size.
 SVM_API int svmd_train_decomp_u8(void* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, const double* mn_h,
@@ -201,7 +201,7 @@ SVM_API int svmd_cascade_group_exercise(void* group, const char* script, double 
 // every rank's GPU holds all n uint8 rows (host X, n x d) and labels, owns a block range of f, and
 // all-gathers its candidate records once per outer iteration; the working set, inner solve and alpha
 // are replicated.  With 1, 2, 4 or 8 ranks the trajectory equals svmd_train_decomp_u8's.  alpha_out
-// (n), r, stats (6 int64, see svmd_train_decomp_u8) and mm_out (2 d: column min / max) may be null.
+// (n), r, stats (8 int64, see svmd_train_decomp_u8) and mm_out (2 d: column min / max) may be null.
 SVM_API int svmd_cascade_group_decomp(void* group, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
                                       const svm_params* p, int32_t q, double* alpha_out, svm_result* r,
                                       int64_t* stats, double* rank_ms, double* mm_out);

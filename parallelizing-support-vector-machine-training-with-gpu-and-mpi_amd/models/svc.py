@@ -44,11 +44,12 @@ class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto",
-                 wss: str = "first", solver: str = "smo", working_set: int = 1024):
+                 wss: str = "first", solver: str = "auto", working_set: int = 1024):
         if wss not in ("first", "second"):
             raise ValueError("wss must be 'first' (the reference's selection) or 'second'")
-        if solver not in ("smo", "decomp"):
-            raise ValueError("solver must be 'smo' (the reference's pairwise SMO over all n points) or 'decomp'")
+        if solver not in ("auto", "smo", "decomp"):
+            raise ValueError("solver must be 'auto' (decomp on GPUs, smo on the CPU), 'decomp' (working-set "
+                             "decomposition) or 'smo' (the reference's pairwise SMO over all n points)")
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else default_threads(),
                                 wss=2 if wss == "second" else 1)
@@ -59,10 +60,12 @@ class SVC:
         self.gram = gram  # "auto" | "fp64" | "int" (device backend Gram path, see ops.device.train)
         self.kcache = kcache  # "auto" | "full" (resident Gram) | "rows" (on-demand HBM row cache)
         self._dev = None  # device-side model state (torch tensors)
-        # "smo": the reference's solver (one pair per iteration over all n points, resident Gram or row
-        # cache).  "decomp": working sets of up to `working_set` points solved in one workgroup with
-        # the same stop test on all n points (decomp.hip; GPU, pixel rows as uint8 or FP64, cold start)
-        # -- the same support vectors, b within the stop tolerance, a different pair sequence.
+        # "decomp" (the GPU default): working sets of up to `working_set` points solved in one workgroup
+        # with the reference's stop test on all n points (decomp.hip; exact-integer kernel values for
+        # pixel rows, FP64 MFMA for real-valued rows; cold or warm start) -- the same support vectors,
+        # b within the stop tolerance, a different pair sequence.  "smo": the reference's solver (one
+        # pair per iteration over all n points, resident Gram or row cache; the CPU oracle's, the CPU
+        # default).  "auto" resolves per fit by device.
         self.solver = solver
         self.working_set = int(working_set)
 
@@ -99,7 +102,7 @@ class SVC:
         from ..ops import cpu as C
 
         if self.solver == "decomp":
-            raise ValueError("solver='decomp' runs on the GPU (device='cuda')")
+            raise ValueError("solver='decomp' runs on the GPU (device='cuda'); the CPU oracle is the pairwise SMO")
         if self.scale:
             self.scaler_ = MinMaxScaler().fit(X)
             Xs = self.scaler_.transform(X)
@@ -117,18 +120,23 @@ class SVC:
         from ..ops import device as D
 
         device = torch.device(dev)
-        decomp = self.solver == "decomp"
+        # auto: the decomposition unless a pairwise-only knob was asked for (second-order pair
+        # selection, a forced Gram path or the row cache)
+        decomp = self.solver == "decomp" or (self.solver == "auto" and self.params.wss != 2 and self.gram == "auto"
+                                             and self.kcache == "auto")
         if decomp:
             if not self.scale:
-                raise ValueError("solver='decomp' needs scale=True (its kernel values come from the scaled rows' "
-                                 "exact-integer plan)")
-            if X.dtype == np.uint8:
-                if not self._fit_cuda_u8(X, y, alpha0, device):
-                    raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
+                if self.solver == "decomp":
+                    raise ValueError("solver='decomp' needs scale=True (min-max scaled rows: its exact-integer "
+                                     "plan, or the FP64 rows it solves on)")
+                decomp = False  # auto without scaling: the pairwise solver
+            elif X.dtype == np.uint8 and self._fit_cuda_u8(X, y, alpha0, device, decomp=True):
                 return
             # FP64 host rows (the reference's format): scaled on the device, then quantised into the
-            # same integers as the byte path -- the same trajectory and model
-        if (X.dtype == np.uint8 and self.scale and self.gram in ("auto", "int") and self.kcache in ("auto", "full")
+            # same integers as the byte path (the same trajectory and model), or -- real-valued data --
+            # solved on the FP64 rows with FP64-MFMA kernel values
+        if (not decomp and X.dtype == np.uint8 and self.scale and self.gram in ("auto", "int")
+                and self.kcache in ("auto", "full")
                 and os.environ.get("SVM355_U8_TRAIN", "1") != "0" and self._fit_cuda_u8(X, y, alpha0, device)):
             return
         t0 = time.perf_counter()
@@ -150,7 +158,7 @@ class SVC:
             out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set,
                                       warm=alpha0 is not None)
             if out is None:
-                raise ValueError("solver='decomp' needs integer pixel rows (no exact-integer plan for these)")
+                raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16")
             res, tm = out
         else:
             res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
@@ -174,7 +182,7 @@ class SVC:
         self._sv_host = None  # scaled SV rows stay on the device; copied to the host on first access
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, **tm}
 
-    def _fit_cuda_u8(self, X, y, alpha0, device) -> bool:
+    def _fit_cuda_u8(self, X, y, alpha0, device, decomp: bool = False) -> bool:
         """uint8 pixel rows, resident Gram: the rows stay bytes on the device -- min/max, the exact-integer
         quantisation and the Gram read them directly, and only the support vectors are ever widened
         to scaled FP64 (for prediction).  Same Gram, trajectory and model as the FP64-row path, minus
@@ -184,7 +192,6 @@ class SVC:
         from ..ops import device as D
 
         n, d = X.shape
-        decomp = self.solver == "decomp"
         if not decomp and self.kcache == "auto" and not D.gram_fits(n, device):
             return False
         # No PyTorch kernel runs on this path (copies and the library's own kernels only): a process's
@@ -304,6 +311,31 @@ class SVC:
         if _resolve_device(device) != "cpu":
             svc._upload_model(_resolve_device(device))
         return svc
+
+    def _device_model_from_u8(self, X_sv: np.ndarray, dev: str) -> None:
+        """The device model of a fit whose rows are uint8 pixels and whose alphas, b and scaler are set
+        (the distributed trainers): only the SV rows' bytes cross PCIe, widened and scaled on the device
+        (svmd_sv_rows_u8) -- no host FP64 transform and no FP64 upload (~1 MB instead of 8.6 MB at 60k).
+        No PyTorch kernel runs (copies and the library's own kernels only)."""
+        import torch
+
+        from ..ops import device as D
+
+        device = torch.device(dev)
+        X_sv = np.ascontiguousarray(X_sv, dtype=np.uint8)
+        k, d = X_sv.shape
+        mm = torch.from_numpy(np.concatenate([self.scaler_.min_, self.scaler_.max_]).astype(np.float64)).to(device)
+        mn, mx = mm[:d], mm[d:]
+        if k:
+            Xu = D.upload_u8(X_sv, device)
+            idx = torch.from_numpy(np.arange(k, dtype=np.int64)).to(device)
+            Xs, ns = D.sv_rows_u8(Xu, idx, mn, mx)
+        else:
+            Xs = torch.empty((0, D.padded_dim(d)), dtype=torch.float64, device=device)
+            ns = torch.empty(0, dtype=torch.float64, device=device)
+        self._dev = {"Xs": Xs, "ns": ns, "coef": torch.from_numpy(np.ascontiguousarray(self.dual_coef_)).to(device),
+                     "mn": mn, "mx": mx, "d": d, "device": device}
+        self._sv_host = None
 
     def _upload_model(self, dev: str) -> None:
         import torch

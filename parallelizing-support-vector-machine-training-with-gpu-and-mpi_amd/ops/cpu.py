@@ -71,7 +71,7 @@ def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Op
     n = y.shape[0]
     a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
     r = N.SvmResult()
-    st = (ctypes.c_int64 * 6)()
+    st = (ctypes.c_int64 * 8)()
     tr = N.DecompTrace(trace_cap, n if snapshots else 0) if trace_cap > 0 else None
     p = params.to_struct()
     N.check(N.core().svm_decomp_train_gram(N.ptr(K), K.shape[1], N.ptr(y), n, N.ptr(a), int(alpha is not None),

@@ -410,7 +410,9 @@ def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: 
     uint8 pixel rows (n, d), or min-max scaled FP64 rows (n, ld) with ``d`` columns (the reference's host
     format, d = len(mn); they quantise into the same integers, so trajectory and model are the uint8 path's).
     warm: alpha holds the start (f = K (alpha y) - y over its nonzero entries).  trace: an
-    ``N.DecompTrace`` filled per outer iteration (tests).  None when no exact-integer plan applies."""
+    ``N.DecompTrace`` filled per outer iteration (tests).  FP64 rows without an exact-integer plan
+    (real-valued data) are solved with FP64-MFMA kernel values (``gram_path`` "fp64"); uint8 rows
+    without one return None (the caller widens them)."""
     u8 = X.dtype == torch.uint8
     if not u8:
         _check_rows(X)
@@ -419,7 +421,7 @@ def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: 
     a, b, dd = _host_stats(mn, mx)
     d = ld if u8 else dd
     r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
-    st = (ctypes.c_int64 * 6)()
+    st = (ctypes.c_int64 * 8)()
     p = params.to_struct()
     N.check(ctx.lib.svmd_train_decomp(ctx.bind(), N.ptr(X), int(u8), n, ld, d, N.ptr(a), N.ptr(b), N.ptr(y),
                                       N.ptr(alpha), ctypes.byref(p), int(working_set), int(warm), ctypes.byref(r),
@@ -428,8 +430,9 @@ def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: 
     if not used.value:
         return None
     return SMOResult.from_struct(r), {"gram_ms": tm.gram_ms, "smo_ms": tm.smo_ms, "total_ms": tm.total_ms,
-                                      "kcache": "none", "gram_path": "int8-exact", "rows": "uint8" if u8 else "fp64",
-                                      "solver": "decomp", "warm_start": bool(warm), "outer_iterations": int(st[0]),
+                                      "kcache": "none", "gram_path": "fp64" if st[6] else "int8-exact",
+                                      "rows": "uint8" if u8 else "fp64", "solver": "decomp", "warm_start": bool(warm),
+                                      "warm_columns": int(st[7]), "outer_iterations": int(st[0]),
                                       "inner_iterations": int(st[1]), "working_set": int(st[2]),
                                       "update_columns": int(st[4]), "inner_threads": int(st[5])}
 

@@ -21,6 +21,7 @@ from .. import _native as N
 from ..utils.config import SVMParams
 
 LAYER_NAMES = {0: "local", -1: "merge"}
+SOLVER_NAMES = {0: "smo", 1: "decomp"}
 
 
 @dataclass
@@ -58,7 +59,8 @@ class CascadeResult:
                        "layer": LAYER_NAMES.get(int(s[2]), f"layer{int(s[2])}"), "n": int(s[3]),
                        "iterations": int(s[4]), "ms": float(s[5]), "b": float(s[6]),
                        "stop": N.STOP_NAMES.get(int(s[7]), str(int(s[7]))), "gram_ms": float(s[8]), "skipped": bool(s[9]),
-                       "row_cache": bool(s[10]), "solo_ms": float(s[11])} for s in sol]
+                       "row_cache": bool(s[10]), "solo_ms": float(s[11]),
+                       "solver": SOLVER_NAMES.get(int(s[12]), str(int(s[12])))} for s in sol]
             phases = dict(zip(N.CASCADE_PHASES, [round(float(v), 3) for v in o.phase_ms]))
             return cls(arr(o.ids, o.n_sv, np.int64), arr(o.y, o.n_sv, np.int32), arr(o.alpha, o.n_sv, np.float64),
                        arr(o.sv_rows, o.n_sv * o.d, np.float64).reshape(o.n_sv, o.d), arr(o.mn, o.d, np.float64),
@@ -75,9 +77,16 @@ class CascadeSVM:
     def __init__(self, params: Optional[SVMParams] = None, topology: str = "star", max_rounds: int = 50,
                  checkpoint_dir: Optional[str] = None, resume: bool = False, verbose: int = 0,
                  comm_timeout_s: float = 600.0, fail_rank: int = -1, fail_round: int = -1,
-                 fail_stall_s: float = 0.0):
+                 fail_stall_s: float = 0.0, solver: str = "auto"):
         if topology not in ("star", "tree"):
             raise ValueError("topology must be 'star' (modified two-layer) or 'tree' (classical)")
+        if solver not in ("auto", "smo", "decomp"):
+            raise ValueError("solver must be 'auto' (decomp on GPUs, the pairwise oracle on the CPU), 'smo' (the "
+                             "reference's pairwise trajectory) or 'decomp' (warm-started working-set decomposition)")
+        # every local / merge solve: the warm-started working-set decomposition (decomp.hip; on the CPU
+        # backend its oracle on the set's kernel matrix) or the reference's pairwise SMO; "auto" resolves
+        # per fit: decomp on GPUs, the pairwise oracle on the CPU
+        self.solver = solver
         self.params = params or SVMParams()
         self.topology = topology
         self._ck = checkpoint_dir.encode() if checkpoint_dir else None  # kept alive for the C struct
@@ -90,6 +99,11 @@ class CascadeSVM:
         self.result: Optional[CascadeResult] = None
         self.device = "cpu"
 
+    def _set_solver(self, cpu: bool) -> None:
+        s = self.solver if self.solver != "auto" else ("smo" if cpu else "decomp")
+        self.cfg.solver = int(s == "decomp")
+        self.solver_used = s
+
     def _check_world(self, world: int) -> None:
         if self.topology == "tree" and world & (world - 1):  # mpi_svm_main3.cpp:420-428
             raise ValueError(f"classical (tree) cascade needs a power-of-2 number of ranks, got {world}")
@@ -97,6 +111,7 @@ class CascadeSVM:
     def fit(self, X, y, world: int = 1, device: str = "cpu", transport: str = "auto", group=None) -> "CascadeSVM":
         """Thread-ranks of this process over contiguous ceil(n / world) partitions with global ids."""
         self._check_world(world)
+        self._set_solver(device == "cpu")
         y = np.ascontiguousarray(y, dtype=np.int32)
         if device == "cpu":
             X = np.ascontiguousarray(X, dtype=np.float64)
@@ -122,6 +137,7 @@ class CascadeSVM:
         """This process's rank trains on its partition (raw rows, global ids): ``RcclRank`` (its GPU,
         RCCL) or ``HostCommRank`` (the CPU oracle over a gloo group, the multi-process CPU tests)."""
         self._check_world(rank.world)
+        self._set_solver(rank.device == "cpu")
         if rank.device == "cpu":
             self.device = "cpu"
             self.result = CascadeResult.take(rank.fit(self.cfg, X_part, y_part, ids, n_total))

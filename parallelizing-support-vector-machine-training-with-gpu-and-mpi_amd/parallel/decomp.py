@@ -43,7 +43,7 @@ def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: 
     alpha = np.empty(n, dtype=np.float64)
     mm = np.empty(2 * d, dtype=np.float64)
     r = N.SvmResult()
-    st = (ctypes.c_int64 * 6)()
+    st = (ctypes.c_int64 * 8)()
     ms = np.zeros(max(world, 1), dtype=np.float64)
     p = params.to_struct()
     t0 = time.perf_counter()
@@ -106,8 +106,12 @@ class DistributedDecompSVC:
         m.dual_coef_ = a[sup] * y[sup]
         m.b_, m.intercept_ = out["b"], -out["b"]
         m.n_iter_, m.stop_reason_ = out["iterations"], out["stop_reason"]
-        m.support_vectors_ = m.scaler_.transform(np.asarray(X)[sup])
-        m._upload_model(dev)
+        X = np.asarray(X)
+        if X.dtype == np.uint8:
+            m._device_model_from_u8(X[sup], dev)
+        else:  # pixel values held as FP64 (validated integers): widened on the host
+            m.support_vectors_ = m.scaler_.transform(X[sup])
+            m._upload_model(dev)
         self.model_ = m
         self.alpha_, self.support_, self.b_ = a, sup, out["b"]
         self.n_iter_, self.stop_reason_ = out["iterations"], out["stop_reason"]

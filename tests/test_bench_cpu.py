@@ -95,13 +95,12 @@ def test_bench_smo_refuses_cpu(capsys):
 
 
 def test_bench_decomp_solver_needs_gpus_and_its_own_parallel_mode(capsys):
-    """The decomposition solver (the GPU default) has no CPU oracle, and at N > 1 it runs as --parallel
-    auto / decomp; the cascade and the distributed pairwise SMO belong to --solver smo."""
+    """The decomposition solver (the GPU default, every cascade solve too) runs on GPUs; the CPU oracle
+    and the distributed pairwise SMO (--parallel smo) belong to --solver smo."""
     assert bench.main(["--solver", "decomp", "--device", "cpu", "--rows", "600", "--steps", "1"]) == 2
     assert "runs on GPUs" in capsys.readouterr().err
     assert bench.main(["--solver", "decomp", "--gpus", "2", "--parallel", "smo", "--transport", "loopback",
                        "--rows", "600"]) == 2
-    assert bench.main(["--solver", "decomp", "--cascade", "--rows", "600"]) == 2
 
 
 def test_bench_parallel_decomp_refuses_cpu(capsys):

@@ -169,3 +169,19 @@ def test_stalled_rank_hits_the_deadline(data):
     with pytest.raises(NativeError, match="no progress for 0.5 s"):
         CascadeSVM(P2, comm_timeout_s=0.5, fail_rank=1, fail_round=1, fail_stall_s=3.0).fit(tr.X, tr.y, world=2)
     assert time.perf_counter() - t0 < 30
+
+
+@pytest.mark.parametrize("topology,world", [("star", 2), ("star", 3), ("tree", 2)])
+def test_decomposition_solver_cascade(data, topology, world):
+    """Every local / merge solve by the warm-started decomposition (its CPU oracle on the set's direct
+    RBF Gram; decomp.hip on the GPUs): the same converged model as the pairwise cascade within the stop
+    tolerance, every solve logged as decomp."""
+    tr, te = data
+    a = CascadeSVM(P2, topology=topology, solver="smo").fit(tr.X, tr.y, world=world)
+    b = CascadeSVM(P2, topology=topology, solver="decomp").fit(tr.X, tr.y, world=world)
+    ra, rb = a.result, b.result
+    assert rb.converged and all(s["solver"] == "decomp" for s in rb.solves)
+    assert all(s["solver"] == "smo" for s in ra.solves)
+    assert abs(ra.b - rb.b) <= 10 * P2.tau
+    assert len(set(ra.ids.tolist()) ^ set(rb.ids.tolist())) <= 2
+    assert abs(a.score(te.X, te.y) - b.score(te.X, te.y)) <= 0.002

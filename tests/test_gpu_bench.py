@@ -1,0 +1,77 @@
+"""The exact commands the driver's scaling run takes, on the one GPU of the box.
+
+* ``bench.main(["--gpus", "2", ...])`` in its default N > 1 mode -- the distributed decomposition
+  solver (rehearsed with two thread ranks over the loopback transport) as the headline, then the star
+  and the tree cascades (BASELINE configs 5 / 4) timed under the same bracket.
+* ``torchrun --nproc-per-node 1 bench.py --gpus 1 --parallel decomp``: the per-process branch (gloo
+  bootstrap, ncclCommInitRank, the RCCL candidate all-gather path, the max over ranks).
+The JSON contract is checked field by field, and the timed steps against the wall clock around them."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_common(out, n_gpus, steps, wall_s):
+    assert out["metric"] == bench.METRIC and out["n_gpus"] == n_gpus and out["steps"] == steps
+    assert out["higher_is_better"] is False and out["unit"] == "s" and out["dtype"] == "fp64"
+    assert out["ms_per_step"] * steps <= wall_s * 1e3
+    assert abs(out["value"] * 1e3 - out["ms_per_step"]) < 1e-3 * out["ms_per_step"] + 1e-3
+    assert out["config"]["global_batch"] == 6000 and out["config"]["seq_len"] == 784
+
+
+def test_bench_default_mode_two_ranks_with_the_cascades(tmp_path):
+    path = tmp_path / "b.json"
+    t0 = time.perf_counter()
+    rc = bench.main(["--gpus", "2", "--transport", "loopback", "--steps", "1", "--warmup", "1", "--rows", "6000",
+                     "--test-rows", "1000", "--baseline-1gpu", "1", "--cascade-steps", "1", "--out", str(path)])
+    wall = time.perf_counter() - t0
+    assert rc == 0
+    out = json.loads(path.read_text())
+    _check_common(out, 2, 1, wall)
+    assert out["config"]["parallelism"] == "distributed-decomp-dp2"
+    assert out["bit_identical_to_1gpu"] is True and out["speedup_vs_1gpu"] > 0 and out["single_gpu_s"] > 0
+    assert out["stop_reason"] == "converged"
+    for topo in ("star", "tree"):
+        c = out[f"cascade_{topo}"]
+        assert out[f"cascade_{topo}_ms"] == c["ms"] > 0
+        assert c["converged"] and c["rounds"] >= 1 and len(c["sv_history"]) >= 1 and c["solver"] == "decomp"
+        assert c["n_sv"] > 0 and c["accuracy"] > 0.95 and c["transport"] == "loopback"
+        assert abs(c["b_minus_headline_b"]) <= 10 * 1e-5
+        assert c["per_round_critical_path"] and c["critical_path_solve_ms"] > 0
+    assert "merged_history" in out["cascade_star"]
+
+
+def test_torchrun_one_process_default_decomp():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "1", "--parallel", "decomp",
+           "--rows", "6000", "--test-rows", "1000", "--steps", "2", "--warmup", "1", "--baseline-1gpu", "1",
+           "--cascade-steps", "1"]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    wall = time.perf_counter() - t0
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    _check_common(out, 1, 2, wall)
+    assert out["launch"].startswith("torchrun") and out["config"]["parallelism"] == "distributed-decomp-dp1"
+    assert out["launch_form"] == "one rank per process"
+    assert out["bit_identical_to_1gpu"] is True and out["speedup_vs_1gpu"] > 0
+    assert out["cascade_star"]["converged"] and out["cascade_tree"]["converged"]
+    assert out["rccl_runtime"].startswith("2.")

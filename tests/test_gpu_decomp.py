@@ -34,7 +34,7 @@ def test_decomp_meets_the_stop_test_with_the_pairwise_svs(n, q):
     from svm355.ops import device as D
 
     tr = synthetic_mnist(n, seed=77).compact()
-    ref = SVC(device="cuda:0").fit(tr.X, tr.y)
+    ref = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
     m = SVC(device="cuda:0", solver="decomp", working_set=q).fit(tr.X, tr.y)
     assert m.stop_reason_ == ref.stop_reason_ == "converged"
     assert m.timings_["solver"] == "decomp" and m.timings_["outer_iterations"] >= 1
@@ -57,7 +57,7 @@ def test_decomp_at_the_headline_shape():
     """60k MNIST-shaped rows (the bench's problem): the same SV set as the pairwise solve and b
     within the stop tolerance, with far fewer device round trips (one per outer iteration)."""
     tr = synthetic_mnist(60000, seed=2024).compact()
-    ref = SVC(device="cuda:0").fit(tr.X, tr.y)
+    ref = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
     m = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
     assert m.stop_reason_ == "converged"
     assert abs(m.b_ - ref.b_) <= 1e-4
@@ -102,13 +102,53 @@ def test_decomp_stop_reasons_of_the_device_loop():
     assert m5.timings_["outer_iterations"] == ref.timings_["outer_iterations"]
 
 
-def test_decomp_refuses_what_it_does_not_cover():
+def test_decomp_refuses_unscaled_rows():
     tr = synthetic_mnist(500, seed=3)
-    rng = np.random.default_rng(5)
-    with pytest.raises(ValueError, match="integer pixel rows"):
-        SVC(device="cuda:0", solver="decomp").fit(tr.X.astype(np.float64) + rng.random(tr.X.shape) * 0.5, tr.y)
     with pytest.raises(ValueError, match="scale=True"):
         SVC(device="cuda:0", solver="decomp", scale=False).fit(tr.compact().X, tr.y)
+    m = SVC(device="cuda:0", scale=False).fit(tr.compact().X, tr.y)  # auto: the pairwise solver then
+    assert m.timings_.get("solver") != "decomp"
+
+
+@pytest.mark.parametrize("n,d", [(3000, 50), (2500, 784)])
+def test_decomp_on_real_valued_rows(n, d):
+    """Rows with no exact-integer plan (real-valued data) are solved on the FP64 rows, every kernel
+    value on FP64 MFMA (gram_mfma.hip): the KKT gap from numpy exp(-gamma d^2) is within 2 tau, and the
+    support vectors are the pairwise FP64 solve's."""
+    rng = np.random.default_rng(n + d)
+    X = rng.random((n, d))
+    w = rng.standard_normal(d)
+    y = np.where(X @ w + 0.3 * rng.standard_normal(n) > np.median(X @ w), 1, -1).astype(np.int32)
+    gamma, C = (0.05, 2.0) if d == 50 else (0.00125, 10.0)
+    m = SVC(device="cuda:0", gamma=gamma, C=C).fit(X, y)
+    assert m.timings_["solver"] == "decomp" and m.timings_["gram_path"] == "fp64"
+    assert m.stop_reason_ == "converged"
+    ref = SVC(device="cuda:0", gamma=gamma, C=C, solver="smo").fit(X, y)
+    assert ref.timings_["gram_path"] == "fp64"
+    Xs = (X - X.min(0)) / np.where(X.max(0) - X.min(0) < 1e-12, 1.0, X.max(0) - X.min(0))
+    sq = np.einsum("ij,ij->i", Xs, Xs)
+    K = np.exp(-gamma * np.maximum(sq[:, None] + sq[None, :] - 2.0 * Xs @ Xs.T, 0.0))
+    np.fill_diagonal(K, 1.0)
+    a, yf, p = m.alpha_, y.astype(np.float64), m.params
+    f = K @ (a * yf) - yf
+    hi = ((yf == 1) & (a < C - p.eps)) | ((yf == -1) & (a > p.eps))
+    lo = ((yf == 1) & (a > p.eps)) | ((yf == -1) & (a < C - p.eps))
+    assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-8
+    np.testing.assert_array_equal(m.support_, ref.support_)
+    assert abs(m.b_ - ref.b_) <= 10 * p.tau
+
+
+def test_decomp_f64_rows_forced_on_pixel_data(monkeypatch):
+    """SVM355_DECOMP_F64=1 takes the FP64-MFMA path on pixel rows too: the kernel values agree with the
+    exact-integer ones to a few ulps, so the model is the same to the stop tolerance."""
+    tr = synthetic_mnist(4000, seed=83)
+    a = SVC(device="cuda:0").fit(tr.X, tr.y)
+    monkeypatch.setenv("SVM355_DECOMP_F64", "1")
+    b = SVC(device="cuda:0").fit(tr.X, tr.y)
+    assert a.timings_["gram_path"] == "int8-exact" and b.timings_["gram_path"] == "fp64"
+    np.testing.assert_array_equal(a.support_, b.support_)
+    assert abs(a.b_ - b.b_) <= 10 * a.params.tau
+    assert np.mean(a.predict(tr.X) == b.predict(tr.X)) >= 0.999
 
 
 def test_decomp_rejects_an_inner_stop_that_cannot_progress(monkeypatch):

@@ -52,7 +52,7 @@ def test_rehearsal_trajectory_equals_single_gpu(D, n, world):
 def test_rehearsal_at_the_headline_shape(D):
     """60k MNIST-shaped rows over 8 teams: the bench's solve (12,793 iterations), same b and SVs."""
     tr = synthetic_mnist(60000, seed=2024).compact()
-    m1 = SVC(device="cuda:0").fit(tr.X, tr.y)
+    m1 = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
     g = DsmoGroup(8, rehearsal=True)
     try:
         m = DistributedSVC(8, rehearsal=True, group=g).fit(tr.X, tr.y)

@@ -246,7 +246,7 @@ def test_headline_shape_60k_default_solver_equals_graph_replay(dev, D, monkeypat
     np.testing.assert_array_equal(t1, t2)
     np.testing.assert_array_equal(a1, a2)
     del K
-    m = SVC(device="cuda:0").fit(tr.X, tr.y)
+    m = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
     assert m.n_iter_ == r1.iterations and m.b_ == r1.b
     assert m.timings_["gram_path"] == "int8-exact" and m.timings_["kcache"] == "full"
     assert m.timings_.get("rows") == "uint8"  # bench.py's byte path (SVC._fit_cuda_u8)
@@ -327,7 +327,7 @@ def test_count_correct_vs_numpy(dev, D, m):
 
 def test_svc_cuda_matches_cpu(dev, mn_data):
     tr, te = mn_data
-    g = SVC(device="cuda").fit(tr.X, tr.y)
+    g = SVC(device="cuda", solver="smo").fit(tr.X, tr.y)
     c = SVC(device="cpu", n_threads=8).fit(tr.X, tr.y)
     assert abs(g.b_ - c.b_) < 1e-6 * max(1, abs(c.b_))
     assert len(set(g.support_.tolist()) ^ set(c.support_.tolist())) <= 2
@@ -411,9 +411,9 @@ def test_near_integer_rows_take_the_fp64_gram(dev, mn_data):
     inner = np.flatnonzero((X[:, col] > X[:, col].min()) & (X[:, col] < X[:, col].max()))
     assert len(inner) > 3
     X[inner[::3], col] += 4e-7  # e.g. 3.0000004; min / max (and so the range plan) stay integers
-    a = SVC(device="cuda:0").fit(X, tr.y[:600])
+    a = SVC(device="cuda:0", solver="smo").fit(X, tr.y[:600])
     assert a.timings_["gram_path"] == "fp64"
-    b = SVC(device="cuda:0").fit(tr.X[:600], tr.y[:600])
+    b = SVC(device="cuda:0", solver="smo").fit(tr.X[:600], tr.y[:600])
     assert b.timings_["gram_path"] == "int8-exact"
 
 
@@ -468,8 +468,8 @@ def test_upload_u8_rows_equal_fp64_upload(dev, D, mn_data):
 
 def test_svc_u8_rows_bit_identical_to_fp64_rows(dev, mn_data):
     tr, te = mn_data
-    a = SVC(device="cuda:0").fit(tr.compact().X, tr.y)
-    b = SVC(device="cuda:0").fit(tr.X, tr.y)
+    a = SVC(device="cuda:0", solver="smo").fit(tr.compact().X, tr.y)
+    b = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
     assert a.b_ == b.b_ and a.n_iter_ == b.n_iter_
     np.testing.assert_array_equal(a.alpha_, b.alpha_)
     np.testing.assert_array_equal(a.decision_function(te.compact().X), b.decision_function(te.X))
@@ -481,10 +481,10 @@ def test_svc_byte_path_equals_fp64_row_path(dev, mn_data, monkeypatch):
     The models -- alphas, b, SV rows and norms, decisions -- must be identical bit for bit."""
     tr, te = mn_data
     Xc = tr.compact().X
-    a = SVC(device="cuda:0").fit(Xc, tr.y)
+    a = SVC(device="cuda:0", solver="smo").fit(Xc, tr.y)
     assert a.timings_.get("rows") == "uint8" and a.timings_["gram_path"] == "int8-exact"
     monkeypatch.setenv("SVM355_U8_TRAIN", "0")
-    b = SVC(device="cuda:0").fit(Xc, tr.y)
+    b = SVC(device="cuda:0", solver="smo").fit(Xc, tr.y)
     assert "rows" not in b.timings_
     assert a.b_ == b.b_ and a.n_iter_ == b.n_iter_
     np.testing.assert_array_equal(a.alpha_, b.alpha_)

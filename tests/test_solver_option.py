@@ -1,5 +1,6 @@
-"""SVC's solver option on the CPU: the decomposition solver (decomp.hip) is GPU-only and says so; an
-unknown solver is refused at construction."""
+"""SVC's solver option on the CPU: the decomposition solver (decomp.hip) is the GPU default ("auto"),
+the pairwise SMO the CPU's (the oracle); an explicit decomp on the CPU says it is GPU-only; an unknown
+solver is refused at construction."""
 import numpy as np
 import pytest
 
@@ -18,9 +19,9 @@ def test_decomp_on_the_cpu_is_refused():
         SVC(device="cpu", solver="decomp").fit(tr.X, tr.y)
 
 
-def test_default_solver_is_the_reference_smo():
+def test_default_solver_on_the_cpu_is_the_reference_smo():
     m = SVC(device="cpu")
-    assert m.solver == "smo" and m.working_set == 1024
+    assert m.solver == "auto" and m.working_set == 1024
     tr = synthetic_mnist(300, seed=2)
     m.fit(tr.X, tr.y)
     assert m.stop_reason_ == "converged" and np.all(m.alpha_ >= 0)
