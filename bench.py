@@ -132,6 +132,7 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
+    cascade_solver = a.solver or "auto"  # the cascade's solves: per solve on GPUs unless --solver is given
     if a.solver is None:  # the decomposition on GPUs (every cascade solve too); the pairwise SMO on the CPU oracle
         a.solver = "smo" if (cpu or a.parallel == "smo") else "decomp"
     if a.solver == "decomp" and (cpu or a.parallel == "smo"):
@@ -293,7 +294,7 @@ def main(argv=None):
             model = cascade_fit(a.topology)
 
     def cascade_fit(topology):
-        c = CascadeSVM(params, topology=topology, comm_timeout_s=a.comm_timeout, solver=a.solver)
+        c = CascadeSVM(params, topology=topology, comm_timeout_s=a.comm_timeout, solver=cascade_solver)
         if multiproc:
             return c.fit_rank(crank, part.X, part.y, np.arange(lo, hi), a.n)
         return c.fit(full.X, full.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)

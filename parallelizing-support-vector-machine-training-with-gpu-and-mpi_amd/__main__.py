@@ -94,8 +94,9 @@ def _cascade(argv) -> int:
     ap.add_argument("--wss", choices=["first", "second"], default="first",
                     help="working-set selection: first order (the reference) or the opt-in second-order choice")
     ap.add_argument("--solver", choices=["auto", "decomp", "smo"], default="auto",
-                    help="every local / merge solve: the warm-started working-set decomposition (decomp; auto on "
-                         "GPUs) or the reference's pairwise SMO (smo; auto on --cpu)")
+                    help="every local / merge solve: the warm-started working-set decomposition (decomp), the "
+                         "reference's pairwise SMO (smo), or auto: on GPUs per solve (the decomposition for cold and "
+                         "small sets, the pairwise SMO for large warm-started ones), on --cpu the pairwise oracle")
     ap.add_argument("--cpu", action="store_true", help="CPU thread-ranks on the native oracle instead of GPUs")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU; thread-ranks of this process)")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
@@ -113,7 +114,7 @@ def _cascade(argv) -> int:
         args = ["--topology", a.topology, "--gpus", str(max(1, a.gpus)), "--transport", a.transport,
                 "--max-rounds", str(a.max_rounds), "--C", str(a.C), "--gamma", str(a.gamma), "--tau", str(a.tau),
                 "--positive-label", str(a.positive_label), "--seed", str(a.seed), "--comm-timeout", str(a.comm_timeout),
-                "--wss", a.wss, "--solver", "smo" if a.solver == "smo" else "decomp"]
+                "--wss", a.wss, "--solver", a.solver]
         if a.synthetic:
             args += ["--synthetic", a.synthetic]
         else:

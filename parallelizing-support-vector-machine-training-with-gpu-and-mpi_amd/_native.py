@@ -178,7 +178,7 @@ class DecompTrace:
         return out
 
 
-SOLVE_COLS = 13  # svm355.h SVM_CASCADE_SOLVE_COLS
+SOLVE_COLS = 14  # svm355.h SVM_CASCADE_SOLVE_COLS
 CASCADE_PHASES = ("upload", "scale", "bcast", "assemble", "solve", "select", "gather", "sendrecv", "checkpoint",
                   "final", "setup")
 

@@ -37,8 +37,8 @@ struct Options {
   bool quiet = false;
   int gram_mode = 0;  // svm_gpu: 0 auto (exact-integer int8 MFMA Gram for pixel data), 1 fp64, 2 int
   int warmup = 0;     // svm_gpu: untimed training runs before the timed one
-  int solver = 1;     // svm_gpu / svm_cascade: 1 working-set decomposition (default), 0 the pairwise SMO (the
-                      // reference's trajectory, --solver smo)
+  int solver = 2;     // 1 working-set decomposition, 0 the pairwise SMO (the reference's trajectory, --solver
+                      // smo), 2 auto (default): svm_gpu the decomposition, svm_cascade per solve (cascade.h)
 };
 
 inline void usage(const char* prog) {
@@ -46,7 +46,7 @@ inline void usage(const char* prog) {
           "usage: %s [--dataset P | --train F --test F | --synthetic N[,M] [--seed S]] [--n-limit N]\n"
           "          [--C 10] [--gamma 0.00125] [--tau 1e-5] [--eps 1e-12] [--sv-tol 1e-8]\n"
           "          [--max-iter 100000] [--positive-label 1] [--threads T] [--model-dir D] [--json F]\n"
-          "          [--gram auto|fp64|int] [--warmup W] [--wss first|second] [--solver smo|decomp]\n",
+          "          [--gram auto|fp64|int] [--warmup W] [--wss first|second] [--solver auto|decomp|smo]\n",
           prog);
 }
 
@@ -90,11 +90,11 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
       o.gram_mode = g == "fp64" ? 1 : g == "int" ? 2 : 0;
     } else if (a == "--solver") {
       const std::string v = next("--solver");
-      if (v != "smo" && v != "decomp") {
-        fprintf(stderr, "--solver must be smo or decomp\n");
+      if (v != "smo" && v != "decomp" && v != "auto") {
+        fprintf(stderr, "--solver must be smo, decomp or auto\n");
         return false;
       }
-      o.solver = v == "decomp" ? 1 : 0;
+      o.solver = v == "decomp" ? 1 : v == "smo" ? 0 : 2;
     } else if (a == "--wss") {
       const std::string w = next("--wss");
       if (w != "first" && w != "second") {

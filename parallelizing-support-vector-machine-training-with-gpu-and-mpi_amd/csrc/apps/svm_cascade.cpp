@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
   cfg.comm_timeout_s = timeout;
   cfg.fail_rank = fail_rank;
   cfg.fail_round = fail_round;
-  cfg.solver = o.solver;  // --solver decomp (default) | smo
+  cfg.solver = o.solver;  // --solver auto (default: per solve) | decomp | smo
   svm_cascade_out* R = svmd_cascade_group_fit(group, tr.X.data(), 0, tr.y.data(), tr.n, tr.d, &cfg);
   if (!R) {
     fprintf(stderr, "[rank 0] error: %s\n", svm_last_error());

@@ -85,7 +85,7 @@ int main(int argc, char** argv) {
     CK(svmd_preprocess(dev.ctx, Xd, n, d, ld, mn, mx, sqn, 0));
     CK(svmd_memcpy_d2h(dev.ctx, mnh.data(), mn, d * 8));
     CK(svmd_memcpy_d2h(dev.ctx, mxh.data(), mx, d * 8));
-    if (o.solver == 1) {  // working-set decomposition (the default; no stored Gram)
+    if (o.solver != 0) {  // working-set decomposition (the default, auto; no stored Gram)
       int32_t used = 0;
       int64_t st[8] = {};
       CK(svmd_train_decomp_rows(dev.ctx, Xd, n, ld, d, mnh.data(), mxh.data(), yd, alpha, &o.p, 1024, &r, &tm, st,
@@ -158,7 +158,7 @@ int main(int argc, char** argv) {
   printf("The elapsed time: %.3f milliseconds\n", train_ms + pred_ms);
   if (!o.quiet)
     fprintf(stderr, "[svm_gpu] %s: gram %.3f ms (%s), smo %.3f ms, iterations %lld\n",
-            o.solver == 1 ? "decomposition" : "pairwise SMO", tm.gram_ms, int_gram ? "int8-exact" : "fp64", tm.smo_ms,
+            o.solver != 0 ? "decomposition" : "pairwise SMO", tm.gram_ms, int_gram ? "int8-exact" : "fp64", tm.smo_ms,
             (long long)r.iterations);
   if (!o.model_dir.empty()) {
     std::vector<int32_t> lab(static_cast<size_t>(nsv));
@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
   }
   char extra[256];
   snprintf(extra, sizeof(extra), "\"gram_ms\": %.3f, \"smo_ms\": %.3f, \"gram_path\": \"%s\", \"solver\": \"%s\"",
-           tm.gram_ms, tm.smo_ms, int_gram ? "int8-exact" : "fp64", o.solver == 1 ? "decomp" : "smo");
+           tm.gram_ms, tm.smo_ms, int_gram ? "int8-exact" : "fp64", o.solver != 0 ? "decomp" : "smo");
   cli::write_json(o.json, "svm_gpu", o, n, d, r, correct, m, train_ms, pred_ms, train_ms + pred_ms, extra);
   return 0;
 }

@@ -84,7 +84,8 @@ class CpuBackend final : public Backend {
   void record_ids(const double* rec, int64_t k, int64_t ld, int64_t* ids) override {
     for (int64_t i = 0; i < k; ++i) ids[i] = int64_t(rec[i * (ld + 3) + ld + 2]);
   }
-  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double*, const double*, int solver) override {
+  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double*, const double*, int solver,
+                   int64_t) override {
     svm_result r{};
     if (solver == 1 && S.k >= 2) {
       // the decomposition oracle (decomp_cpu.cpp) on the set's kernel matrix (the reference's direct
@@ -92,11 +93,13 @@ class CpuBackend final : public Backend {
       std::vector<double> K(size_t(S.k) * size_t(S.k));
       check(svm_rbf_matrix(S.X.as<double>(), S.k, S.X.as<double>(), S.k, d, p.gamma, K.data(), p.n_threads),
             "svm_rbf_matrix");
-      check(svm_decomp_train_gram(K.data(), S.k, S.y.as<int32_t>(), S.k, S.a.as<double>(), 1, &p, 1024, 0.1, 2, &r,
-                                  nullptr, nullptr),
+      int64_t ds[8] = {};
+      check(svm_decomp_train_gram(K.data(), S.k, S.y.as<int32_t>(), S.k, S.a.as<double>(), 1, &p, 1024, 0.1, 2, &r, ds,
+                                  nullptr),
             "svm_decomp_train_gram");
       SolveStats st{r.iterations, r.b, r.stop_reason, 0.0};
       st.solver = 1;
+      st.outer = ds[0];
       return st;
     }
     check(svm_smo_train(S.X.as<double>(), S.y.as<int32_t>(), S.k, d, S.a.as<double>(), 1, &p, &r, nullptr, 0),

@@ -80,7 +80,8 @@ svm_cascade_out* build_cascade_out(const std::vector<const CascadeOutput*>& outs
     for (const SolveLog& s : x->solves)
       solves.insert(solves.end(), {double(s.rank), double(s.round), double(s.layer), double(s.rows),
                                    double(s.iterations), s.ms, s.b, double(s.stop), s.gram_ms,
-                                   s.skipped ? 1.0 : 0.0, s.row_cache ? 1.0 : 0.0, s.solo_ms, double(s.solver)});
+                                   s.skipped ? 1.0 : 0.0, s.row_cache ? 1.0 : 0.0, s.solo_ms, double(s.solver),
+                                   double(s.outer)});
   }
   static_assert(kNumPhases == sizeof(o->phase_ms) / sizeof(double), "svm_cascade_out.phase_ms size");
   std::copy(R.phase_ms, R.phase_ms + kNumPhases, o->phase_ms);

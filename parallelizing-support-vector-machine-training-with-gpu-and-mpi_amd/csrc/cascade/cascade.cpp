@@ -300,7 +300,8 @@ class Rank {
         ++skipped;
         skipped_now = true;
       } else {
-        st = B_.solve(S, d_, cfg_.params, mn_h.data(), mx_h.data(), cfg_.solver);
+        st = B_.solve(S, d_, cfg_.params, mn_h.data(), mx_h.data(), cascade_solver_for(cfg_.solver, S.k, warm_rows),
+                      warm_rows);
       }
     }
     auto tm = timer(kPhSelect);
@@ -312,7 +313,9 @@ class Rank {
     DSet out = assemble({seg});
     log.push_back(
         SolveLog{t_.rank(), rnd, layer, S.k, st.iterations, ms_between(t0, Clock::now()), st.b, st.stop, st.gram_ms,
-                              skipped_now, st.row_cache, B_.take_solo_ms(), skipped_now ? cfg_.solver : st.solver});
+                              skipped_now, st.row_cache, B_.take_solo_ms(),
+                              skipped_now ? cascade_solver_for(cfg_.solver, S.k, warm_rows) : st.solver,
+                              st.outer});
     return {std::move(out), st.b};
   }
 

@@ -135,6 +135,7 @@ struct SolveStats {
   double gram_ms = 0.0;
   bool row_cache = false;  // solved on the HBM row cache (the k x k Gram did not fit)
   int32_t solver = 0;      // the solver that ran: 0 pairwise SMO, 1 working-set decomposition
+  int64_t outer = 0;       // decomposition: outer iterations (working sets solved)
 };
 
 class Backend {
@@ -180,8 +181,9 @@ class Backend {
   // Warm-start solve on S (SMO_train(..., init=false), mpi_svm_main3.cpp:155-290): alphas in S.a are
   // updated in place.  mn_h/mx_h: the global scaling statistics (host, d values).  solver: 0 the
   // pairwise SMO, 1 the working-set decomposition (CascadeConfig::solver; the stats say which ran).
+  // warm_rows: S's leading rows that carry the warm alphas (0: a cold start).
   virtual SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h,
-                           int solver) = 0;
+                           int solver, int64_t warm_rows) = 0;
   // True when the warm start of S (rows [0, nz) carry every nonzero alpha) provably meets the stop
   // test b_low <= b_high + 2 tau already -- i.e. the solve would end at its first selection without
   // an update -- checked from a cross-kernel K(S, S[0:nz]) only, before any Gram work.  The margin
@@ -364,8 +366,16 @@ struct CascadeConfig {
   // with fail_stall_s > 0 stops responding for that long (its peers' exchanges hit the deadline).
   int fail_rank = -1, fail_round = -1;
   double fail_stall_s = 0.0;
-  int solver = 0;  // svm_cascade_cfg.solver: 0 pairwise SMO, 1 working-set decomposition
+  int solver = 0;  // svm_cascade_cfg.solver: 0 pairwise SMO, 1 working-set decomposition, 2 per solve
 };
+
+// svm_cascade_cfg.solver = 2: the solver of one solve.  Measured at 60k (profiles/r4_cascade_decomp_rehearsal.txt):
+// the decomposition is 1.4-2.2x faster on cold and small warm sets (round-0 locals, merges), 4-6x slower on
+// large warm-started sets (later-round locals of P <= 4: hundreds of working sets of ~20-90 pair updates).
+inline int cascade_solver_for(int solver, int64_t k, int64_t warm_rows) {
+  if (solver != 2) return solver;
+  return (warm_rows == 0 || k <= SVM_CASCADE_DECOMP_WARM_ROWS) ? 1 : 0;
+}
 
 // cascade_state.bin layout (little-endian): char magic[8] = "SVM355C2"; int32 topology (0 star,
 // 1 tree); int32 reserved; int64 next_round; double b; int64 d; int64 k; then k records of d + 3
@@ -383,6 +393,7 @@ struct SolveLog {
   bool row_cache = false;  // SolveStats::row_cache
   double solo_ms = -1.0;   // Backend::take_solo_ms (skip check + solve), < 0 = not measured
   int32_t solver = 0;      // SolveStats::solver
+  int64_t outer = 0;       // SolveStats::outer
 };
 
 // Wall time of this rank per driver phase (host clock; with SVM355_CASCADE_PROFILE=1 every phase

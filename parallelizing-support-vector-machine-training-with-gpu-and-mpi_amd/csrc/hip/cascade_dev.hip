@@ -340,8 +340,8 @@ class HipBackend final : public Backend {
     keep->assign(kh, kh + *cnt);
     *keep_dev = static_cast<const int64_t*>(sel_d_);
   }
-  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h,
-                   int solver) override {
+  SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h, int solver,
+                   int64_t) override {
     if (solver == 1) {  // the decomposition solver keeps no Gram: nothing to size or hand back
       SolveStats st;
       if (solo([&] { return solve_decomp(S, d, p, mn_h, mx_h, &st); })) return st;
@@ -404,12 +404,16 @@ class HipBackend final : public Backend {
     double prep = 0.0;
     DecompOpts o;
     o.warm = true;
+    // A/B probe: SVM355_DECOMP_CASCADE_START=cold starts every solve from alpha = 0 (the same local
+    // optimum, another path); the reference warm-starts (mpi_svm_main3.cpp:169-186)
+    if (const char* cs = getenv("SVM355_DECOMP_CASCADE_START")) o.warm = strcmp(cs, "cold") != 0;
     check(decomp_fit_rows(device_ctx(), S.X.as<double>(), S.k, ld(d), d, mn_h, mx_h, S.y.as<int32_t>(),
                           S.a.as<double>(), p, 1024, &r, st, &used, &prep, o),
           "decomposition SMO");
     if (!used) return false;
     *out = SolveStats{r.iterations, r.b, r.stop_reason, prep};
     out->solver = 1;
+    out->outer = st[0];
     return true;
   }
   SolveStats solve_impl(DSet& S, int64_t d, const svm_params& p, const double* mn_h, const double* mx_h) {

@@ -777,7 +777,12 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512
   int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
-  if (inner_nt != 64 && inner_nt != 128 && inner_nt != 512) inner_nt = 256;
+  if (inner_nt != 64 && inner_nt != 128 && inner_nt != 512 && inner_nt != 65) inner_nt = 256;
+  // 65: one wave x 6 points (A/B probe of a one-wave inner solve; needs a working set of <= 384)
+  if (inner_nt == 65 && sh.L > 384) {
+    set_error("decomposition SMO: SVM355_DECOMP_NT=65 needs a working set of <= 384 points");
+    return SVM_ERR_ARG;
+  }
   // inner stop: the working set's own gap <= max(2 tau, 2 tau_frac gap) (SVM355_DECOMP_TAU_FRAC)
   double tau_frac = 0.1;
   if (const char* v = getenv("SVM355_DECOMP_TAU_FRAC")) tau_frac = atof(v);
@@ -953,7 +958,9 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                                   &ctl->m, nullptr, 0);
         if (rc) return rc;
       }
-      if (inner_nt == 64)
+      if (inner_nt == 65)
+        SVM_WS_INNER(64, 6);
+      else if (inner_nt == 64)
         SVM_WS_INNER(64, 16);
       else if (inner_nt == 128)
         SVM_WS_INNER(128, 8);

@@ -173,11 +173,13 @@ typedef struct svm_cascade_cfg {
   int32_t solver;          // every local / merge solve: 0 = the pairwise first-order SMO (the reference's
                            //   trajectory, default), 1 = the warm-started working-set decomposition
                            //   (device backend: decomp.hip; CPU backend: its oracle on the set's kernel
-                           //   matrix; sets without an exact-integer plan on the device fall back to 0)
+                           //   matrix), 2 = per solve: the decomposition for cold or small sets
+                           //   (<= SVM_CASCADE_DECOMP_WARM_ROWS rows), the pairwise SMO for large warm ones
   int32_t reserved;
 } svm_cascade_cfg;
 
-#define SVM_CASCADE_SOLVE_COLS 13
+#define SVM_CASCADE_SOLVE_COLS 14
+#define SVM_CASCADE_DECOMP_WARM_ROWS 4096
 // Result of a cascade fit (allocated by the library, release with svm_cascade_free).
 typedef struct svm_cascade_out {
   int32_t world, rank, rounds, converged;
@@ -201,7 +203,7 @@ typedef struct svm_cascade_out {
                            //   the kernel matrix, skipped (warm start already optimal), row cache
                            //   (solved on kernel rows computed on demand: the Gram did not fit),
                            //   solo ms (device time alone, serial-solve rehearsals; < 0 otherwise),
-                           //   solver (0 pairwise SMO, 1 decomposition)
+                           //   solver (0 pairwise SMO, 1 decomposition), decomposition outer iterations (0 pairwise)
   int64_t n_ranks;
   double* rank_train_ms;   // train_ms of each rank this call drove
   char transport[16];

@@ -60,7 +60,7 @@ class CascadeResult:
                        "iterations": int(s[4]), "ms": float(s[5]), "b": float(s[6]),
                        "stop": N.STOP_NAMES.get(int(s[7]), str(int(s[7]))), "gram_ms": float(s[8]), "skipped": bool(s[9]),
                        "row_cache": bool(s[10]), "solo_ms": float(s[11]),
-                       "solver": SOLVER_NAMES.get(int(s[12]), str(int(s[12])))} for s in sol]
+                       "solver": SOLVER_NAMES.get(int(s[12]), str(int(s[12]))), "outer": int(s[13])} for s in sol]
             phases = dict(zip(N.CASCADE_PHASES, [round(float(v), 3) for v in o.phase_ms]))
             return cls(arr(o.ids, o.n_sv, np.int64), arr(o.y, o.n_sv, np.int32), arr(o.alpha, o.n_sv, np.float64),
                        arr(o.sv_rows, o.n_sv * o.d, np.float64).reshape(o.n_sv, o.d), arr(o.mn, o.d, np.float64),
@@ -81,11 +81,11 @@ class CascadeSVM:
         if topology not in ("star", "tree"):
             raise ValueError("topology must be 'star' (modified two-layer) or 'tree' (classical)")
         if solver not in ("auto", "smo", "decomp"):
-            raise ValueError("solver must be 'auto' (decomp on GPUs, the pairwise oracle on the CPU), 'smo' (the "
-                             "reference's pairwise trajectory) or 'decomp' (warm-started working-set decomposition)")
+            raise ValueError("solver must be 'auto' (GPUs: per solve, the decomposition for cold / small sets and "
+                             "the pairwise SMO for large warm ones; CPU: the pairwise oracle), 'smo' (the reference's "
+                             "pairwise trajectory) or 'decomp' (the warm-started working-set decomposition)")
         # every local / merge solve: the warm-started working-set decomposition (decomp.hip; on the CPU
-        # backend its oracle on the set's kernel matrix) or the reference's pairwise SMO; "auto" resolves
-        # per fit: decomp on GPUs, the pairwise oracle on the CPU
+        # backend its oracle on the set's kernel matrix), the reference's pairwise SMO, or per solve
         self.solver = solver
         self.params = params or SVMParams()
         self.topology = topology
@@ -100,8 +100,10 @@ class CascadeSVM:
         self.device = "cpu"
 
     def _set_solver(self, cpu: bool) -> None:
-        s = self.solver if self.solver != "auto" else ("smo" if cpu else "decomp")
-        self.cfg.solver = int(s == "decomp")
+        # auto on GPUs: per solve (svm_cascade_cfg.solver = 2) -- the decomposition for cold and small
+        # sets, the pairwise SMO for large warm-started ones (cascade.h cascade_solver_for)
+        s = self.solver if self.solver != "auto" else ("smo" if cpu else "per-solve")
+        self.cfg.solver = {"smo": 0, "decomp": 1, "per-solve": 2}[s]
         self.solver_used = s
 
     def _check_world(self, world: int) -> None:

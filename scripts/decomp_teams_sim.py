@@ -147,15 +147,18 @@ def select(f, a, y, NB, per, T):
     return H, L
 
 
-def run(X, y, teams, q, deal, combine, log, shrink=0):
+def run(X, y, teams, q, deal, combine, log, shrink=0, a0=None, tau_frac=0.1, per_outer=None):
     n = len(y)
     K = Kern(X)
     NB0 = max((n + 4095) // 4096, min(64, (n + 63) // 64))
     NB = (NB0 + 7) // 8 * 8
     per = (n + NB - 1) // NB
     T = max(1, q // (2 * NB))  # per team, per block, per side
-    a = np.zeros(n)
+    a = np.zeros(n) if a0 is None else a0.astype(np.float64).copy()
     f = -y.astype(np.float64)
+    if a0 is not None:
+        nz = np.flatnonzero(a != 0)
+        f += K.block(np.arange(n), nz) @ (a[nz] * y[nz])
     outer = crit = total = 0
     lams = []
     sstats = {"rounds": 0, "sizes": []}
@@ -167,7 +170,7 @@ def run(X, y, teams, q, deal, combine, log, shrink=0):
         bl = np.max(np.where(lo, f, -np.inf))
         if bl <= bh + 2 * TAU:
             break
-        tau_in = max(TAU, 0.1 * (bl - bh))
+        tau_in = max(TAU, tau_frac * (bl - bh))
         owner = {}
         # claims in per-block rank order (both sides of rank k before rank k + 1): the blocks' first
         # picks -- among them the global maximal violating pair -- all land in team 0
@@ -192,6 +195,8 @@ def run(X, y, teams, q, deal, combine, log, shrink=0):
             steps.append((W, (an - a[W]) * yf[W]))
             its.append(it)
         outer += 1
+        if per_outer is not None:
+            per_outer.append((bl - bh, [len(W) for W in Ws], its))
         crit += max(its)
         total += sum(its)
         mv = [(W[c != 0], c[c != 0]) for W, c in steps]
@@ -215,6 +220,7 @@ def run(X, y, teams, q, deal, combine, log, shrink=0):
         if total > 100000:
             break
     sv = int(np.sum(a > 1e-8))
+    run.alpha = a
     return outer, crit, total, sv, (bh + bl) / 2, sstats
 
 

@@ -6,11 +6,12 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp SVM355_CASCADE_SERIAL_SOLVES=1
-for solver in decomp smo; do
+for solver in ${SOLVERS:-auto decomp smo}; do
 for topo in star tree; do
   for P in 2 4 8; do
     f=gpurun_out/r4crit_${solver}_${topo}_P$P
-    timeout -k 10 300 python -u bench.py --gpus $P --cascade --solver $solver --topology $topo --transport loopback \
+    sarg="--solver $solver"; [ "$solver" = auto ] && sarg=""
+    timeout -k 10 300 python -u bench.py --gpus $P --cascade $sarg --topology $topo --transport loopback \
       --steps 2 --warmup 1 --baseline-1gpu 0 --out $f.json > $f.log 2>&1 || { tail -20 $f.log; exit 1; }
     python - "$f.json" "$solver $topo P=$P" <<'PY'
 import json, sys

@@ -46,7 +46,7 @@ def test_bench_default_mode_two_ranks_with_the_cascades(tmp_path):
     for topo in ("star", "tree"):
         c = out[f"cascade_{topo}"]
         assert out[f"cascade_{topo}_ms"] == c["ms"] > 0
-        assert c["converged"] and c["rounds"] >= 1 and len(c["sv_history"]) >= 1 and c["solver"] == "decomp"
+        assert c["converged"] and c["rounds"] >= 1 and len(c["sv_history"]) >= 1 and c["solver"] == "per-solve"
         assert c["n_sv"] > 0 and c["accuracy"] > 0.95 and c["transport"] == "loopback"
         assert abs(c["b_minus_headline_b"]) <= 10 * 1e-5
         assert c["per_round_critical_path"] and c["critical_path_solve_ms"] > 0
