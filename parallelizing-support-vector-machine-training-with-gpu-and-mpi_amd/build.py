@@ -32,6 +32,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", "-pthread", "-Wall", "-Wextra",
             "-Wno-unused-parameter", f"-I{CSRC / 'include'}", f"-I{CSRC / 'cascade'}"]
 HIPFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", f"-I{ROCM / 'include'}",
+            f'-DSVM355_RCCL_PATH="{ROCM / "lib" / "librccl.so.1"}"',  # rccl_api.h: the RCCL of these headers
             "-Wall", "-Wno-unused-parameter", "-Wno-unused-result", f"-I{CSRC / 'include'}",
             f"-I{CSRC / 'hip'}", f"-I{CSRC / 'cascade'}"]
 
@@ -105,7 +106,7 @@ def build_hip(force=False, verbose=False) -> Path:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _stale(out, objs):
         _run([cc, "-shared", f"--offload-arch={ARCH}", *objs, f"-L{LIB}", "-lsvm355_core",
-              f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", "-lrccl", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}",
+              f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", "-ldl", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}",
               "-o", out], verbose)
     return out
 

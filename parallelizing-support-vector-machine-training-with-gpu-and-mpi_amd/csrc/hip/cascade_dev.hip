@@ -28,10 +28,13 @@
 #include "cascade_capi.h"
 #include "ctx.h"
 #include "decomp.h"
+#include "rccl_api.h"
 #include "svm355_device.h"
 
 namespace svm355 {
 namespace {
+
+inline const RcclApi& RC() { return rccl_checked(); }  // the explicitly loaded librccl (rccl_api.h)
 
 // ------------------------------------------------------------------------------------- kernels
 // One workgroup per row (grid-stride); rows of stored sets are 16-byte aligned (ld % 16 == 0), record
@@ -572,7 +575,7 @@ class HipBackend final : public Backend {
 #define NCCLT(expr)                                                                                 \
   do {                                                                                              \
     const ncclResult_t r_ = (expr);                                                                 \
-    if (r_ != ncclSuccess) throw TransportError(std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    if (r_ != ncclSuccess) throw TransportError(std::string(#expr) + ": " + RC().GetErrorString(r_)); \
   } while (0)
 #define HIPT(expr)                                                                                    \
   do {                                                                                                \
@@ -585,8 +588,8 @@ class RcclTransport final : public Transport {
   RcclTransport(ncclComm_t comm, int device, hipStream_t stream, WaitPolicy wp)
       : comm_(comm), device_(device), stream_(stream), wp_(std::move(wp)) {
     HIPT(hipSetDevice(device_));
-    NCCLT(ncclCommUserRank(comm_, &rank_));
-    NCCLT(ncclCommCount(comm_, &world_));
+    NCCLT(RC().CommUserRank(comm_, &rank_));
+    NCCLT(RC().CommCount(comm_, &world_));
     HIPT(hipMalloc(&scratch_, size_t(64 + world_) * 8));
     HIPT(hipHostMalloc(&pinned_, size_t(64 + world_) * 8, hipHostMallocDefault));
   }
@@ -612,7 +615,7 @@ class RcclTransport final : public Transport {
     pinned_[0] = v;
     HIPT(hipMemcpyAsync(scratch_, pinned_, 8, hipMemcpyHostToDevice, stream_));
     const auto t1 = std::chrono::steady_clock::now();
-    NCCLT(ncclBroadcast(scratch_, scratch_, 1, ncclInt64, root, comm_, stream_));
+    NCCLT(RC().Broadcast(scratch_, scratch_, 1, ncclInt64, root, comm_, stream_));
     const auto t2 = std::chrono::steady_clock::now();
     HIPT(hipMemcpyAsync(pinned_ + 1, scratch_, 8, hipMemcpyDeviceToHost, stream_));
     wait("ncclBroadcast(i64)");
@@ -626,36 +629,36 @@ class RcclTransport final : public Transport {
   std::vector<int64_t> allgather_i64(int64_t v) override {
     pinned_[0] = v;
     HIPT(hipMemcpyAsync(scratch_, pinned_, 8, hipMemcpyHostToDevice, stream_));
-    NCCLT(ncclAllGather(scratch_, scratch_ + 1, 1, ncclInt64, comm_, stream_));
+    NCCLT(RC().AllGather(scratch_, scratch_ + 1, 1, ncclInt64, comm_, stream_));
     HIPT(hipMemcpyAsync(pinned_ + 1, scratch_ + 1, size_t(world_) * 8, hipMemcpyDeviceToHost, stream_));
     wait("ncclAllGather(i64)");
     return std::vector<int64_t>(pinned_ + 1, pinned_ + 1 + world_);
   }
   void allreduce_min(double* buf, int64_t n) override {
-    NCCLT(ncclAllReduce(buf, buf, size_t(n), ncclFloat64, ncclMin, comm_, stream_));
+    NCCLT(RC().AllReduce(buf, buf, size_t(n), ncclFloat64, ncclMin, comm_, stream_));
     wait("ncclAllReduce(min)");
   }
   void allreduce_max(double* buf, int64_t n) override {
-    NCCLT(ncclAllReduce(buf, buf, size_t(n), ncclFloat64, ncclMax, comm_, stream_));
+    NCCLT(RC().AllReduce(buf, buf, size_t(n), ncclFloat64, ncclMax, comm_, stream_));
     wait("ncclAllReduce(max)");
   }
   void bcast(void* buf, int64_t bytes, int root) override {
     if (bytes <= 0) return;
-    NCCLT(ncclBroadcast(buf, buf, size_t(bytes), ncclUint8, root, comm_, stream_));
+    NCCLT(RC().Broadcast(buf, buf, size_t(bytes), ncclUint8, root, comm_, stream_));
     wait("ncclBroadcast");
   }
   void gather(const void* send, int64_t bytes, void* recv, int root) override {
     if (bytes <= 0) return;
-    NCCLT(ncclGather(send, recv, size_t(bytes), ncclUint8, root, comm_, stream_));
+    NCCLT(RC().Gather(send, recv, size_t(bytes), ncclUint8, root, comm_, stream_));
     wait("ncclGather");
   }
   void allgather(const void* send, int64_t bytes, void* recv) override {
     if (bytes <= 0) return;
-    NCCLT(ncclAllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
+    NCCLT(RC().AllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
     wait("ncclAllGather");
   }
   void allgather_async(const void* send, int64_t bytes, void* recv) override {
-    if (bytes > 0) NCCLT(ncclAllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
+    if (bytes > 0) NCCLT(RC().AllGather(send, recv, size_t(bytes), ncclUint8, comm_, stream_));
   }
   bool stream_wait(const char* what) override {
     wait(what);
@@ -668,33 +671,33 @@ class RcclTransport final : public Transport {
   void send_i64(int64_t v, int peer) override {
     pinned_[2] = v;
     HIPT(hipMemcpyAsync(scratch_ + 2, pinned_ + 2, 8, hipMemcpyHostToDevice, stream_));
-    NCCLT(ncclSend(scratch_ + 2, 1, ncclInt64, peer, comm_, stream_));
+    NCCLT(RC().Send(scratch_ + 2, 1, ncclInt64, peer, comm_, stream_));
     wait("ncclSend(i64)");
   }
   int64_t recv_i64(int peer) override {
-    NCCLT(ncclRecv(scratch_ + 3, 1, ncclInt64, peer, comm_, stream_));
+    NCCLT(RC().Recv(scratch_ + 3, 1, ncclInt64, peer, comm_, stream_));
     HIPT(hipMemcpyAsync(pinned_ + 3, scratch_ + 3, 8, hipMemcpyDeviceToHost, stream_));
     wait("ncclRecv(i64)");
     return pinned_[3];
   }
   void send(const void* buf, int64_t bytes, int peer) override {
     if (bytes <= 0) return;
-    NCCLT(ncclSend(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
+    NCCLT(RC().Send(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
     wait("ncclSend");
   }
   void recv(void* buf, int64_t bytes, int peer) override {
     if (bytes <= 0) return;
-    NCCLT(ncclRecv(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
+    NCCLT(RC().Recv(buf, size_t(bytes), ncclUint8, peer, comm_, stream_));
     wait("ncclRecv");
   }
   void barrier() override {
-    NCCLT(ncclAllReduce(scratch_ + 4, scratch_ + 4, 1, ncclInt64, ncclSum, comm_, stream_));
+    NCCLT(RC().AllReduce(scratch_ + 4, scratch_ + 4, 1, ncclInt64, ncclSum, comm_, stream_));
     wait("ncclAllReduce(barrier)");
   }
   void abort() override {
     if (aborted_ || !comm_) return;
     aborted_ = true;
-    (void)ncclCommAbort(comm_);  // frees the communicator; in-flight kernels are torn down
+    (void)RC().CommAbort(comm_);  // frees the communicator; in-flight kernels are torn down
   }
 
  private:
@@ -706,8 +709,8 @@ class RcclTransport final : public Transport {
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) throw TransportError(std::string(what) + ": " + hipGetErrorString(e));
       ncclResult_t ae = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
-        throw TransportError(std::string(what) + ": " + ncclGetErrorString(ae));
+      if (RC().CommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        throw TransportError(std::string(what) + ": " + RC().GetErrorString(ae));
       wp_.check(t0, what);
       if (spin < 2000)
         std::this_thread::yield();
@@ -726,13 +729,12 @@ class RcclTransport final : public Transport {
 
 double timeout_or_default(double s) { return s > 0 ? s : 600.0; }
 
-// ---- RCCL runtime identity.  Inside a PyTorch process the librccl this library resolves is the one
-// torch already loaded (its bundled copy), not necessarily the /opt/rocm one the header came from.
-// Every entry point called here (CommInitAll / InitRank / Abort / Destroy / GetAsyncError / UserRank /
-// Count, Broadcast, AllReduce, AllGather, Gather, Send, Recv, GetUniqueId, GetErrorString) has kept
-// its signature since RCCL 2.12, and ncclUniqueId its 128 bytes, so a runtime of the header's major
-// version and at least kMinRcclCode is accepted; an older minor than the header's is recorded as a
-// skew, and the preflight (exercise.cpp) checks every op on the live communicators anyway.
+// ---- RCCL runtime identity.  The entry points come from the librccl loaded explicitly by
+// rccl_api.h (the one the headers belong to; inside a PyTorch process a -lrccl link would bind to
+// torch's bundled, older copy instead).  The version check stays as a guard for SVM355_RCCL_LIB
+// overrides: a runtime of the header's major version and at least kMinRcclCode is accepted, an older
+// minor than the header's is reported as a skew, and the preflight (exercise.cpp) checks every op on
+// the live communicators anyway.
 constexpr int kMinRcclCode = 21200;
 struct RcclInfo {
   int header = NCCL_VERSION_CODE;
@@ -742,9 +744,9 @@ struct RcclInfo {
 const RcclInfo& rccl_info() {
   static const RcclInfo info = [] {
     RcclInfo r;
-    if (ncclGetVersion(&r.runtime) != ncclSuccess) r.runtime = 0;
-    Dl_info di{};
-    if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname) r.path = di.dli_fname;
+    const RcclApi& a = rccl();
+    if (!a.ok() || a.GetVersion(&r.runtime) != ncclSuccess) r.runtime = 0;
+    r.path = a.ok() ? a.path : a.error;
     return r;
   }();
   return info;
@@ -945,8 +947,8 @@ SVM_API void* svmd_cascade_group_create(int32_t world, const char* transport, do
     }
     if (g->rccl) {
       g->comms.resize(size_t(world));
-      const ncclResult_t rc = ncclCommInitAll(g->comms.data(), world, g->devices.data());
-      if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitAll: ") + ncclGetErrorString(rc));
+      const ncclResult_t rc = RC().CommInitAll(g->comms.data(), world, g->devices.data());
+      if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitAll: ") + RC().GetErrorString(rc));
       for (int r = 0; r < world; ++r)
         g->rtr.push_back(std::make_unique<RcclTransport>(g->comms[size_t(r)], g->devices[size_t(r)],
                                                          g->be[size_t(r)]->stream(), WaitPolicy{}));
@@ -976,7 +978,7 @@ SVM_API void svmd_cascade_group_destroy(void* h) {
   g->pool.reset();
   g->rtr.clear();
   if (!g->broken)
-    for (auto c : g->comms) (void)ncclCommDestroy(c);
+    for (auto c : g->comms) (void)RC().CommDestroy(c);
   g->be.clear();
   delete g;
 }
@@ -1171,9 +1173,9 @@ SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap) {
     return SVM_ERR_ARG;
   }
   ncclUniqueId id;
-  const ncclResult_t rc = ncclGetUniqueId(&id);
+  const ncclResult_t rc = RC().GetUniqueId(&id);
   if (rc != ncclSuccess) {
-    set_error("ncclGetUniqueId: %s", ncclGetErrorString(rc));
+    set_error("ncclGetUniqueId: %s", RC().GetErrorString(rc));
     return SVM_ERR_DEVICE;
   }
   std::memcpy(out, &id, sizeof(id));
@@ -1193,8 +1195,8 @@ SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32
     p->be = std::make_unique<HipBackend>(device);
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
-    const ncclResult_t rc = ncclCommInitRank(&p->comm, world, id, rank);
-    if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
+    const ncclResult_t rc = RC().CommInitRank(&p->comm, world, id, rank);
+    if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitRank: ") + RC().GetErrorString(rc));
     p->tr = std::make_unique<RcclTransport>(p->comm, device, p->be->stream(), WaitPolicy{nullptr, p->timeout_s});
     require_rccl_runtime();
     if (preflight_enabled()) {
@@ -1223,7 +1225,7 @@ SVM_API void svmd_cascade_rank_destroy(void* h) {
   (void)hipSetDevice(p->device);
   const bool aborted = p->broken;
   p->tr.reset();
-  if (p->comm && !aborted) (void)ncclCommDestroy(p->comm);
+  if (p->comm && !aborted) (void)RC().CommDestroy(p->comm);
   p->be.reset();
   delete p;
 }

@@ -19,8 +19,8 @@ from .. import _native as N
 
 
 def rccl_info() -> dict:
-    """RCCL the device library was built against and the one it runs on (with the library path:
-    inside PyTorch usually torch's bundled librccl)."""
+    """RCCL the device library was built against and the one it runs on, with the library path: the
+    librccl of those headers, loaded explicitly (csrc/hip/rccl_api.h), not the copy PyTorch bundles."""
     h, r = ctypes.c_int32(0), ctypes.c_int32(0)
     path = ctypes.create_string_buffer(512)
     N.hip().svmd_rccl_info(ctypes.byref(h), ctypes.byref(r), path, 512)
@@ -29,7 +29,7 @@ def rccl_info() -> dict:
         return f"{c // 10000}.{c // 100 % 100}.{c % 100}" if c else "unknown"
 
     return {"rccl_header": ver(h.value), "rccl_runtime": ver(r.value), "rccl_path": path.value.decode(),
-            "rccl_skew": h.value // 100 != r.value // 100}
+            "rccl_skew": h.value != r.value}
 
 
 class DeviceGroup:

@@ -71,3 +71,4 @@ def test_dsmo_rank_agrees_on_a_bad_input_before_any_solve():
             DsmoRank.fit(r, X.astype(np.float64) + 0.5, y)
     finally:
         dist.destroy_process_group()
+
