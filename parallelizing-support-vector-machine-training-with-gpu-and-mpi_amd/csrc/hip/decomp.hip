@@ -24,6 +24,7 @@
 // sequence of pair updates differs, so iteration counts and b differ in the last digits.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +38,8 @@
 
 namespace svm355 {
 namespace {
+
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 struct DecompHost {  // pinned: the PROF build's phase totals (the loop state is DecompCtl, on the device)
   int64_t prof[12];  // clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall ticks;
@@ -625,6 +628,138 @@ __global__ __launch_bounds__(256) void ws_rowsum_f64_kernel(const double* __rest
   if (lane == 0) f[row] += acc;
 }
 
+// Column cache bookkeeping of one f update (one 1024-thread workgroup): the moved columns cols[0..*count)
+// the cache lacks get slots -- persistent ones in moved order while the cache has room (slot_of keeps
+// them for the rest of the fit), then scratch slots cap + position -- and are listed for the column
+// store (miss_ids / miss_slots, state[1] of them); rd_slot[k] = every moved column's slot.  state[0] =
+// the next free persistent slot; state[2] = 1 when the narrow column store takes the misses (at most
+// 64: the tiled store's gate).
+__global__ __launch_bounds__(1024) void ws_cache_plan_kernel(const int32_t* __restrict__ cols,
+                                                             const int32_t* __restrict__ count,
+                                                             int32_t* __restrict__ slot_of, int32_t cap,
+                                                             int32_t* __restrict__ state, int32_t* __restrict__ rd_slot,
+                                                             int32_t* __restrict__ miss_ids,
+                                                             int32_t* __restrict__ miss_slots) {
+  constexpr int NW = 1024 / 64;
+  __shared__ int32_t wsum[NW];
+  const int k = threadIdx.x, lane = k & 63, w = k >> 6;
+  const int cnt = *count;
+  const bool valid = k < cnt;
+  const int32_t id = valid ? cols[k] : -1;
+  int32_t sl = valid ? slot_of[id] : 0;
+  const bool miss = valid && sl < 0;
+  const unsigned long long bal = __ballot(miss);
+  if (lane == 0) wsum[w] = __popcll(bal);
+  __syncthreads();
+  int r = __popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+  for (int q = 0; q < NW; ++q) {
+    if (q < w) r += wsum[q];
+    tot += wsum[q];
+  }
+  const int32_t next = state[0];
+  if (miss) {
+    if (next + r < cap) {
+      sl = next + r;
+      slot_of[id] = sl;
+    } else {
+      sl = cap + k;  // cache full: a scratch slot for this update only
+    }
+    miss_ids[r] = id;
+    miss_slots[r] = sl;
+  }
+  if (valid) rd_slot[k] = sl;
+  __syncthreads();  // every thread has read state[0]
+  if (k == 0) {
+    state[0] = min(cap, next + tot);
+    state[1] = tot;
+    state[2] = tot <= 64 ? 1 : 0;
+  }
+}
+
+// f[i] += sum_k coef[k] K(i, cols[k]) from the column cache, in the GEMV + half-sum order, bit for bit
+// (igram GEMV epilogue + ws_fsum_count_kernel): per 64-column half, lane l's two terms (columns l and
+// 32 + l) summed from 0, the 32-lane xor butterfly (16, 8, 4, 2, 1) as seen by lane 0 -- a binary tree
+// whose leaves in evaluation order are the 5-bit bit-reversed lanes, so a 6-deep stack of completed
+// subtrees replaces the 32 lane values --, the halves added in index order, then one add into f.
+// A thread per RPT rows (16-byte loads: ldc is a multiple of 4); the 32 leaves of a half run as 4
+// rolled groups of 8 (8 column pairs of loads in flight per group; unrolled, the compiler hoisted all
+// 64 and ran at 3 waves / SIMD: 4.3 against 5.9 TB/s), the level of a group's last leaf depending on g.
+template <int RPT>
+__global__ __launch_bounds__(256) void ws_cache_fsum_kernel(const double* __restrict__ cache, int64_t ldc,
+                                                             const int32_t* __restrict__ rd_slot,
+                                                             const double* __restrict__ coef,
+                                                             const int32_t* __restrict__ count, double* __restrict__ f,
+                                                             int64_t nloc) {
+  const int64_t i = RPT * (int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+  const int cnt = *count;
+  if (i >= nloc || cnt <= 0) return;
+  const int halves = (cnt + 63) / 64;
+  const double* base = cache + i;
+  double s[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) s[r] = 0.0;
+  for (int c = 0; c < halves; ++c) {
+    double st[6][RPT];
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 8 * g + jj;
+        const int l = ((j & 1) << 4) | ((j & 2) << 2) | (j & 4) | ((j & 8) >> 2) | ((j & 16) >> 4);
+        const int k0 = c * 64 + l, k1 = k0 + 32;
+        double x[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) x[r] = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int k = kk ? k1 : k0;
+          if (k < cnt) {
+            const double cf = coef[k];
+            const f64x2* src = reinterpret_cast<const f64x2*>(base + int64_t(rd_slot[k]) * ldc);
+#pragma unroll
+            for (int r2 = 0; r2 < RPT / 2; ++r2) {
+              const f64x2 v = src[r2];
+              x[2 * r2] += cf * v[0];
+              x[2 * r2 + 1] += cf * v[1];
+            }
+          }
+        }
+        int lev = 0;
+#pragma unroll
+        for (int t = jj; t & 1; t >>= 1, ++lev)
+#pragma unroll
+          for (int r = 0; r < RPT; ++r) x[r] = st[lev][r] + x[r];
+        if (jj == 7) {  // lev == 3: continue up through the trailing ones of g
+          if (g & 1) {
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) x[r] = st[3][r] + x[r];
+            if (g & 2) {
+#pragma unroll
+              for (int r = 0; r < RPT; ++r) x[r] = st[4][r] + x[r];
+#pragma unroll
+              for (int r = 0; r < RPT; ++r) st[5][r] = x[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < RPT; ++r) st[4][r] = x[r];
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) st[3][r] = x[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < RPT; ++r) st[lev][r] = x[r];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) s[r] += st[5][r];
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+    if (i + r < nloc) f[i + r] += s[r];
+}
+
 // f[i] += the first ceil(*mcount / 64) column halves of part (the ones the GEMV wrote).
 __global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __restrict__ part, int64_t ldp,
                                                             const int32_t* __restrict__ mcount,
@@ -806,6 +941,43 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     off += al(bytes);
     return o;
   };
+  // Column cache (exact-integer rows): the f update's kernel columns K(this GPU's rows, j) stay in HBM
+  // per point for the rest of the fit, so a column moved again is a read, not an int8-MFMA
+  // recomputation (64 / 75 / 85 % of the column uses at 60k / 250k / 1M repeat an earlier one,
+  // profiles/r4_decomp_column_cache.txt); bit-identical to the GEMV path (ws_cache_fsum_kernel).
+  // SVM355_DECOMP_CCACHE = 0 off, 1 on; default on once this GPU's int8 rows (nloc x kq bytes, read by
+  // every recomputation) outgrow the 256 MB last-level cache: the recomputation then streams them from
+  // HBM (192 MiB: 60k MNIST rows, 46 MB, are 4 % faster without the cache, 250k rows 2 % with it).
+  bool use_cache = false;
+  int32_t cache_cap = 0;
+  int64_t ldc_cache = 0;
+  double* cache = nullptr;
+  if (!f64 && nloc > 0) {
+    const char* cc = getenv("SVM355_DECOMP_CCACHE");
+    use_cache = cc ? atoi(cc) != 0 : nloc * int64_t(P.kq) > (int64_t(192) << 20);
+  }
+  if (use_cache) {
+    // slots: twice the distinct columns measured per fit (~1,686 (n / 60k)^0.46), within half the free
+    // HBM, plus kMaxWS scratch slots (moved columns beyond a full cache, this update only)
+    int64_t cap = int64_t(2.0 * 1686.0 * std::pow(double(n) / 60000.0, 0.46));
+    cap = std::min<int64_t>(std::max<int64_t>(cap, 1024), n);
+    size_t free_b = 0, total_b = 0;
+    SVMD_CHECK(hipMemGetInfo(&free_b, &total_b));
+    ldc_cache = (nloc + 3) & ~int64_t(3);  // a multiple of 4: 16-byte row pairs (or quads) in the reader
+    const size_t slot_b = size_t(ldc_cache) * 8;
+    cap = std::min<int64_t>(cap, int64_t((free_b + ctx->rc_cache_bytes) / 2 / slot_b) - kMaxWS);
+    int64_t min_cap = 256;
+    if (const char* v = getenv("SVM355_DECOMP_CCACHE_SLOTS")) {  // tests: a small cache (its scratch path)
+      cap = std::min<int64_t>(cap, atoll(v));
+      min_cap = 1;
+    }
+    if (cap >= min_cap && cap < int64_t(INT32_MAX) - kMaxWS) {
+      cache = ctx->ensure_rc_cache(size_t(cap + kMaxWS) * slot_b);
+      cache_cap = int32_t(cap);
+    }
+    use_cache = cache != nullptr;
+    if (!use_cache) (void)hipGetLastError();  // a failed allocation is not sticky: the GEMV path runs
+  }
   const size_t nl1 = size_t(std::max<int64_t>(nloc, 1));
   const size_t o_f = take(nl1 * 8), o_own = take(size_t(Lr) * sizeof(CandRec)),
                o_all = take(size_t(sh.L) * sizeof(CandRec)), o_W = take(kMaxWS * 4), o_Wf = take(kMaxWS * 8),
@@ -818,6 +990,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                o_Xw = f64 ? take(size_t(kMaxWS) * R.ld * 8) : 0, o_nw = f64 ? take(kMaxWS * 8) : 0,
                o_Xc = f64 ? take(size_t(kMaxWS) * R.ld * 8) : 0, o_nc = f64 ? take(kMaxWS * 8) : 0,
                o_Kc = f64 ? take(nl1 * kMaxWS * 8) : 0;
+  // column cache state: slot per point (-1 = none), the update's slots, its misses, {next free, misses}
+  const size_t o_cslot = use_cache ? take(size_t(n) * 4) : 0, o_crd = use_cache ? take(kMaxWS * 4) : 0,
+               o_cmid = use_cache ? take(kMaxWS * 4) : 0, o_cmsl = use_cache ? take(kMaxWS * 4) : 0,
+               o_cst = use_cache ? take(64) : 0;
   // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
   const int64_t nchunks = (n + kMaxWS - 1) / kMaxWS;
   const size_t o_wcols = o.warm ? take(size_t(n) * 4) : 0, o_wcoef = o.warm ? take(size_t(n) * 8) : 0,
@@ -845,11 +1021,28 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   auto* Xc = reinterpret_cast<double*>(ws + o_Xc);
   auto* nc = reinterpret_cast<double*>(ws + o_nc);
   auto* Kc = reinterpret_cast<double*>(ws + o_Kc);
+  auto* cslot = reinterpret_cast<int32_t*>(ws + o_cslot);
+  auto* crd = reinterpret_cast<int32_t*>(ws + o_crd);
+  auto* cmid = reinterpret_cast<int32_t*>(ws + o_cmid);
+  auto* cmsl = reinterpret_cast<int32_t*>(ws + o_cmsl);
+  auto* cst = reinterpret_cast<int32_t*>(ws + o_cst);
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
   // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
   // order) or, for FP64 rows, the moved columns' rows gathered, their block on FP64 MFMA and a row sum
   auto f_update = [&](const int32_t* cl, const double* cf, const int32_t* cnt) -> int {
     if (nloc <= 0) return SVM_OK;
+    if (use_cache) {  // plan the slots, compute and store the missing columns, sum every column from the cache
+      hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cl, cnt, cslot, cache_cap, cst, crd, cmid,
+                         cmsl);
+      SVMD_LAUNCH_CHECK();
+      const int rc2 = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid,
+                                            cmsl, cst + 1, kMaxWS, P, p.gamma, cache, ldc_cache, cst + 2);
+      if (rc2) return rc2;
+      hipLaunchKernelGGL((ws_cache_fsum_kernel<2>), dim3(unsigned((nloc + 511) / 512)), dim3(256), 0, s, cache,
+                         ldc_cache, crd, cf, cnt, f, nloc);
+      SVMD_LAUNCH_CHECK();
+      return SVM_OK;
+    }
     if (!f64) {
       const int rc2 = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cl, cf,
                                         cnt, kMaxWS, P, p.gamma, part, ldp);
@@ -875,6 +1068,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   std::memset(hs, 0, sizeof(DecompHost));
   SVMD_CHECK(hipMemsetAsync(ctl, 0, sizeof(DecompCtl), s));  // stop = SVM_STOP_RUNNING, counters 0
   if (f64) SVMD_CHECK(hipMemsetAsync(Xw, 0, size_t(kMaxWS) * R.ld * 8, s));  // rows beyond m stay finite
+  if (use_cache) {  // a fresh cache per fit: no point has a slot, the first free slot is 0
+    SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
+    SVMD_CHECK(hipMemsetAsync(cst, 0, 64, s));
+  }
   hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n,
                      int(o.warm));
   SVMD_LAUNCH_CHECK();
@@ -1385,12 +1582,52 @@ SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t
   SVMD_CHECK(hipMemcpyAsync(coef, coef_h, size_t(m) * 8, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemcpyAsync(cnt, &m, 4, hipMemcpyHostToDevice, s));
   SVMD_CHECK(hipMemsetAsync(f, 0, size_t(nloc) * 8, s));
-  rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, cnt, kMaxWS,
-                         P, gamma, part, ldp);
-  if (rc) return rc;
-  hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f,
-                     nloc);
-  SVMD_LAUNCH_CHECK();
+  const char* vc = getenv("SVM355_GEMV_VIA_CACHE");
+  if (vc && atoi(vc) != 0) {
+    // the column-cache form of the same update (tests / timing): a fresh cache of m persistent slots
+    // (every column a miss: the narrow store up to 64 columns, the tiled one beyond), then the reader
+    const int64_t ldc = (nloc + 3) & ~int64_t(3);
+    double* cache = ctx->ensure_rc_cache(size_t(m + kMaxWS) * ldc * 8);
+    if (!cache) {
+      set_error("svmd_decomp_gemv_u8: no memory for the column cache");
+      return SVM_ERR_DEVICE;
+    }
+    const size_t o_cs = need, o_rd = o_cs + al(size_t(n) * 4), o_mid = o_rd + al(kMaxWS * 4),
+                 o_msl = o_mid + al(kMaxWS * 4), o_st = o_msl + al(kMaxWS * 4), need2 = o_st + 256;
+    rc = ctx->ensure_ws(need2);
+    if (rc) return rc;
+    ws = static_cast<char*>(ctx->ws);  // (re)allocated: every pointer again
+    cols = reinterpret_cast<int32_t*>(ws + o_cols);
+    coef = reinterpret_cast<double*>(ws + o_coef);
+    cnt = reinterpret_cast<int32_t*>(ws + o_cnt);
+    f = reinterpret_cast<double*>(ws + o_f);
+    auto* cslot = reinterpret_cast<int32_t*>(ws + o_cs);
+    auto* crd = reinterpret_cast<int32_t*>(ws + o_rd);
+    auto* cmid = reinterpret_cast<int32_t*>(ws + o_mid);
+    auto* cmsl = reinterpret_cast<int32_t*>(ws + o_msl);
+    auto* cst = reinterpret_cast<int32_t*>(ws + o_st);
+    SVMD_CHECK(hipMemcpyAsync(cols, cols_h, size_t(m) * 4, hipMemcpyHostToDevice, s));
+    SVMD_CHECK(hipMemcpyAsync(coef, coef_h, size_t(m) * 8, hipMemcpyHostToDevice, s));
+    SVMD_CHECK(hipMemcpyAsync(cnt, &m, 4, hipMemcpyHostToDevice, s));
+    SVMD_CHECK(hipMemsetAsync(f, 0, size_t(nloc) * 8, s));
+    SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
+    SVMD_CHECK(hipMemsetAsync(cst, 0, 256, s));
+    hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cols, cnt, cslot, m, cst, crd, cmid, cmsl);
+    SVMD_LAUNCH_CHECK();
+    rc = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid, cmsl,
+                               cst + 1, kMaxWS, P, gamma, cache, ldc, cst + 2);
+    if (rc) return rc;
+    hipLaunchKernelGGL((ws_cache_fsum_kernel<2>), dim3(unsigned((nloc + 511) / 512)), dim3(256), 0, s, cache, ldc, crd,
+                       coef, cnt, f, nloc);
+    SVMD_LAUNCH_CHECK();
+  } else {
+    rc = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cols, coef, cnt,
+                           kMaxWS, P, gamma, part, ldp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f,
+                       nloc);
+    SVMD_LAUNCH_CHECK();
+  }
   SVMD_CHECK(hipMemcpyAsync(f_out, f, size_t(nloc) * 8, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipStreamSynchronize(s));
   if (used_out) *used_out = 1;

@@ -296,7 +296,9 @@ __global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict
 // workgroup's 64 columns of coef[j] * K(row, colid[j]) to K[row * ldk + (column-half index)] (a
 // fixed-order butterfly: the caller adds the halves in index order, so the f update is
 // deterministic).
-template <bool EXTRA, int BK, bool RECT = false, bool GEMV = false>
+// CST (with GEMV, decomposition column cache): the same columns and kernel values, stored instead of
+// reduced: K(row, colid[j]) to K[slot[j] * ldk + row] (column j's cache slot, rows contiguous).
+template <bool EXTRA, int BK, bool RECT = false, bool GEMV = false, bool CST = false>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
@@ -304,8 +306,9 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
     const int32_t* __restrict__ ncount = nullptr, const int8_t* __restrict__ Qc = nullptr,
     const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0,
-    const int32_t* __restrict__ gate = nullptr, int64_t cstride = 0) {
+    const int32_t* __restrict__ gate = nullptr, int64_t cstride = 0, const int32_t* __restrict__ slot = nullptr) {
   static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
+  static_assert(!CST || GEMV, "the column store is the GEMV's operands with a store epilogue");
   if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch (decomp.hip)
   using Cfg = IgramCfg<BK>;
   constexpr int QLS = Cfg::LS;
@@ -451,6 +454,47 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   }
 
   __syncthreads();  // staging tiles fully consumed: the union becomes the transpose images
+  if constexpr (CST) {
+    // ---- column-store epilogue: the GEMV's kernel values (the same arithmetic, bit for bit) to the
+    // columns' cache slots; a lane's four consecutive rows are 32 contiguous bytes of one slot
+    const int64_t row0 = bm + w * 32 + 4 * h;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+      const int cl = bj * 32 + l32;
+      const int64_t gj = bn + cl;
+      const bool colok = gj < ncol;
+      const int64_t gid = colok ? int64_t(colid[gj]) : -1;
+      double* dst = K + (colok ? int64_t(slot[gj]) * ldk : 0);
+      const int32_t nbj = n0_c[cl];
+      const double wbj = EXTRA ? wn_c[cl] : 0.0;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        double ex[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = 8 * half + q;
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int32_t D0 = n0_r[w * 32 + rl] + nbj - 2 * acc[bj][r];
+          double dist = w0 * double(D0);
+          if (EXTRA) dist += (wn_r[w * 32 + rl] + wbj) - 2.0 * xacc[bj][r];
+          dist = dist > 0.0 ? dist : 0.0;
+          ex[q] = neg_gamma * dist;
+        }
+        exp_batch<8>(ex);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = 8 * half + q;
+          const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
+          const double kv = gi + row_off == gid ? 1.0 : ex[q];
+          if (colok && gi < n) dst[gi] = kv;
+        }
+      }
+    }
+    if (cstride <= 0) return;
+    bn += cstride;
+    __syncthreads();  // the next half rewrites the column tables the epilogue has just read
+    continue;
+  }
   if constexpr (GEMV) {
     // ---- GEMV epilogue: rowsum[r] = sum over this workgroup's 64 columns of coef * K (the same kernel
     // values as the stored path), lane-local over its two columns, then a 32-lane butterfly per row.
@@ -578,6 +622,144 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
   }
   return;
   }  // for (GEMV column halves)
+}
+
+// Narrow column store (decomposition column cache, <= kNarrowCols missing columns per f update): the
+// columns are the B operand resident in LDS, 32 at a time, and every wave streams 32-row tiles of Q
+// straight from HBM into its MFMA A fragments (four k-steps in flight), so an update that misses a
+// handful of columns reads Q once at streaming rate instead of paying the 128 x 64 tiled pass.  The
+// (lane, byte) -> k map, the extra groups' FP64 flushes in k-step order, the exact integer D0 and the
+// epilogue arithmetic are igram_tri_kernel's, so every stored value equals the GEMV's bit for bit.
+constexpr int kNarrowCols = 64;
+constexpr int kNarrowMaxKq = 1536;  // 32 x (kq + 16) bytes of B in LDS
+template <bool EXTRA>
+__global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
+    const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
+    const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
+    const int8_t* __restrict__ Qc, const int32_t* __restrict__ N0c, const double* __restrict__ WNc,
+    const int32_t* __restrict__ ids, const int32_t* __restrict__ slots, const int32_t* __restrict__ count,
+    int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused) {
+  __shared__ double sw[kMaxSteps];
+  __shared__ double wn_c[32];
+  __shared__ int32_t n0_c[32], id_c[32], sl_c[32];
+  extern __shared__ __attribute__((aligned(16))) char nsm[];
+  const int cnt = *count;
+  if (cnt <= 0 || cnt > kNarrowCols) return;  // nothing missing, or the tiled column store's update
+  const int LS = kq + 16;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, l32 = lane & 31, h = lane >> 5;
+  const int nsteps = kq / 32, main_step0 = main0 / 32;
+  if (EXTRA)
+    for (int k = t; k < main_step0; k += 256) sw[k] = step_w[k];
+  const int64_t tiles = (n + 31) / 32;
+  const int64_t wave0 = int64_t(blockIdx.x) * 4 + w, nwaves = int64_t(gridDim.x) * 4;
+  const i32x4 zero4 = {0, 0, 0, 0};
+  const i32x16 zero16 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int g0 = 0; g0 < cnt; g0 += 32) {
+    const int gc = min(32, cnt - g0);
+    __syncthreads();  // the previous group's columns are consumed
+    if (t < 32) {
+      const bool ok = t < gc;
+      const int32_t id = ok ? ids[g0 + t] : -1;
+      id_c[t] = id;
+      sl_c[t] = ok ? slots[g0 + t] : 0;
+      n0_c[t] = ok ? N0c[id] : 0;
+      if (EXTRA) wn_c[t] = ok ? WNc[id] : 0.0;
+    }
+    const int cpr = kq / 16;
+    for (int c = t; c < 32 * cpr; c += 256) {
+      const int col = c / cpr, ch = c - col * cpr;
+      const i32x4 v = col < gc ? *reinterpret_cast<const i32x4*>(Qc + int64_t(ids[g0 + col]) * kq + ch * 16) : zero4;
+      *reinterpret_cast<i32x4*>(nsm + col * LS + ch * 16) = v;
+    }
+    __syncthreads();
+    const int32_t nbj = n0_c[l32];
+    const double wbj = EXTRA ? wn_c[l32] : 0.0;
+    const int64_t gid = id_c[l32];
+    const bool colok = l32 < gc;
+    double* dst = cache + int64_t(sl_c[l32]) * ldc;
+    const char* bcol = nsm + l32 * LS + 16 * h;
+    // the wave's (tile, chunk of 4 k-steps) positions as one stream, loads one chunk ahead (across tile
+    // boundaries: the next tile's first chunk is in flight during this tile's epilogue; two ahead
+    // measured the same)
+    // only the k-steps holding columns (kused: the trailing pad of kq is zero in every row, so its
+    // MFMAs would add 0); a partial last chunk loads zeros for the steps beyond
+    const int nsu = kused / 32, nch = (nsu + 3) / 4;  // nch * 4 <= nsteps: kq is a multiple of 128
+    int64_t lt = wave0;
+    int lc = 0;
+    auto ld = [&](i32x4(&dst)[4]) {
+      const int64_t arow = lt * 32 + l32;
+      const bool ok = lt < tiles && arow < n;
+      const int8_t* ap = Q + (ok ? arow : 0) * int64_t(kq) + 16 * h + lc * 128;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dst[u] = ok && 4 * lc + u < nsu ? *reinterpret_cast<const i32x4*>(ap + u * 32) : zero4;
+      if (++lc == nch) {
+        lc = 0;
+        lt += nwaves;
+      }
+    };
+    i32x4 p0[4];
+    ld(p0);
+    for (int64_t tile = wave0; tile < tiles; tile += nwaves) {
+      // the tile's row norms, loaded now (lane l32: row l32) and shuffled to the accumulator layout in
+      // the epilogue, so their latency hides behind the k-loop
+      const int64_t nr = tile * 32 + l32 < n ? tile * 32 + l32 : 0;
+      const int32_t n0_mine = N0[nr];
+      const double wn_mine = EXTRA ? WN[nr] : 0.0;
+      i32x16 acc = zero16;
+      double xacc[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xacc[r] = 0.0;
+      bool fresh = false;
+      for (int c = 0; c < nch; ++c) {
+        i32x4 cur[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = p0[u];
+        ld(p0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int step = 4 * c + u;
+          const i32x4 b = *reinterpret_cast<const i32x4*>(bcol + step * 32);
+          if (EXTRA && fresh) {
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur[u], b, zero16, 0, 0, 0);
+            fresh = false;
+          } else {
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur[u], b, acc, 0, 0, 0);
+          }
+          if (EXTRA && step < main_step0) {
+            const double wgt = sw[step];
+            if (wgt != 0.0) {  // last k-step of an extra group: flush its exact cross term
+#pragma unroll
+              for (int r = 0; r < 16; ++r) xacc[r] += wgt * double(acc[r]);
+              fresh = true;
+            }
+          }
+        }
+      }
+      const int64_t row0 = tile * 32 + 4 * h;
+#pragma unroll
+      for (int qtr = 0; qtr < 4; ++qtr) {  // exp_batch is elementwise: quarters keep the registers low
+        double ex[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * qtr + q;
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;  // the row's lane (row0 - tile * 32 = 4 h)
+          const int32_t D0 = __shfl(n0_mine, rl, 64) + nbj - 2 * acc[r];
+          double dist = w0 * double(D0);
+          if (EXTRA) dist += (__shfl(wn_mine, rl, 64) + wbj) - 2.0 * xacc[r];
+          dist = dist > 0.0 ? dist : 0.0;
+          ex[q] = neg_gamma * dist;
+        }
+        exp_batch<4>(ex);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * qtr + q;
+          const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
+          const double kv = gi + row_off == gid ? 1.0 : ex[q];
+          if (colok && gi < n) dst[gi] = kv;
+        }
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -963,6 +1145,68 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
     if (bk == 128) SVM_IGRAM_GEMV(false, 128); else SVM_IGRAM_GEMV(false, 64);
   }
 #undef SVM_IGRAM_GEMV
+  SVMD_LAUNCH_CHECK();
+  return SVM_OK;
+}
+
+// Decomposition column cache (decomp.hip): cache[slots[k] * ldc + i] = K(row_off + i, ids[k]) for the
+// rows i < n of (Q, N0, WN) and k < *count (device; <= m, the grid's bound) -- the GEMV's operands,
+// grid and kernel values (bit for bit), stored per column instead of reduced.
+int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
+                          int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
+                          const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,
+                          const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate) {
+  if (n <= 0 || m <= 0) return SVM_OK;
+  if (gate && P.kq <= kNarrowMaxKq) {  // <= kNarrowCols columns: the streaming kernel (the tiled one exits)
+    const int64_t tiles = (n + 31) / 32;
+    const size_t lds = size_t(32) * (P.kq + 16);
+    int kused = 0;  // int8 columns up to the last real one, rounded up to a k-step
+    for (int k = int(P.perm.size()) - 1; k >= 0; --k)
+      if (P.perm[k] >= 0) {
+        kused = k + 1;
+        break;
+      }
+    kused = std::min(P.kq, (std::max(kused, 1) + 31) / 32 * 32);
+    // one resident wave of workgroups (each loads its columns once and walks ~tiles / waves tiles): a
+    // 2048-workgroup grid ran 2.7 rounds at 3 workgroups per CU
+    int dev = 0, cus = 256, per_cu = 3;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (P.main0 > 0)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, igram_colstore_narrow_kernel<true>, 256, lds);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, igram_colstore_narrow_kernel<false>, 256, lds);
+    const unsigned nwg = unsigned(std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, int64_t(cus) * std::max(per_cu, 1))));
+    if (P.main0 > 0)
+      hipLaunchKernelGGL(igram_colstore_narrow_kernel<true>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
+                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused);
+    else
+      hipLaunchKernelGGL(igram_colstore_narrow_kernel<false>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
+                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused);
+    SVMD_LAUNCH_CHECK();
+  }
+  const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
+  int64_t gc = tiles >= 256 ? -1 : 0;  // the GEMV's grid rule (launch_igram_gemv)
+  if (const char* v = getenv("SVM355_GEMV_GC")) gc = atoi(v);
+  const bool walk_all = gc < 0;
+  if (!walk_all && (gc == 0 || gc > ctiles)) gc = ctiles;
+  const int64_t cstride = walk_all ? QBN : gc < ctiles ? gc * QBM : 0;
+  if (walk_all) gc = 1;
+  const int64_t nwg = walk_all ? tiles : 2 * tiles * gc;
+  if (ldc < n || nwg > 0x7FFFFFFF) {
+    set_error("igram colstore: bad slot stride or problem too large");
+    return SVM_ERR_ARG;
+  }
+  const int bk = P.kq % 128 == 0 ? 128 : 64;
+#define SVM_IGRAM_CST(EX, B)                                                                                        \
+  hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,  \
+                     P.main0, N0, WN, stw, P.w0, -gamma, cache, ldc, tiles, gc * QBM, int64_t(0), ids, nullptr, count,  \
+                     Qc, N0c, WNc, row_off, P.kq <= kNarrowMaxKq ? gate : nullptr, cstride, slots)
+  if (P.main0 > 0) {
+    if (bk == 128) SVM_IGRAM_CST(true, 128); else SVM_IGRAM_CST(true, 64);
+  } else {
+    if (bk == 128) SVM_IGRAM_CST(false, 128); else SVM_IGRAM_CST(false, 64);
+  }
+#undef SVM_IGRAM_CST
   SVMD_LAUNCH_CHECK();
   return SVM_OK;
 }

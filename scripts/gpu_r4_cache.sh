@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: the decomposition column cache -- oracle / bit-identity GPU tests, timings off vs on at
+# 60k / 250k / 1M, and a kernel-stats profile of the 1M fit with the cache.
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONPATH=.
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_decomp_oracle.py \
+  > gpurun_out/r4cache_pytest.txt 2>&1 || { tail -30 gpurun_out/r4cache_pytest.txt; exit 1; }
+timeout -k 10 400 python -u scripts/decomp_cache_timing.py 60000 250000 1000000 > gpurun_out/r4cache_time.txt 2>&1 \
+  || { tail -20 gpurun_out/r4cache_time.txt; exit 1; }
+CACHES=1 bash scripts/gpu_r4_cache_prof.sh 1000000 && CACHES=1 bash scripts/gpu_r4_cache_prof.sh 250000 || exit 1
+cat gpurun_out/r4cache_time.txt
+tail -3 gpurun_out/r4cache_pytest.txt

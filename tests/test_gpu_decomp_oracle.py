@@ -43,8 +43,12 @@ def _exact_gram_host(Xu, mn, mx, n, cols=None):
     return np.ascontiguousarray(out)
 
 
+@pytest.mark.parametrize("via", ["gemv", "cache"])
 @pytest.mark.parametrize("n", [20000, 60000])
-def test_gemv_against_numpy_and_its_summation_order(n):
+def test_gemv_against_numpy_and_its_summation_order(n, via, monkeypatch):
+    """via="cache": the column-cache form of the update (every column stored -- the narrow store up to
+    64 columns, the tiled one beyond -- then read back in the GEMV order) gives the same bits."""
+    monkeypatch.setenv("SVM355_GEMV_VIA_CACHE", "1" if via == "cache" else "0")
     tr = synthetic_mnist(n, seed=31).compact()
     Xu, mn, mx = _dev_rows(tr)
     rng = np.random.default_rng(n)
@@ -130,3 +134,47 @@ def test_warm_start_equals_the_oracle_and_meets_the_stop_test():
     np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), cold.support_)
     warm = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y, alpha0=a0)  # the estimator's warm start
     np.testing.assert_array_equal(warm.alpha_, a)
+
+
+@pytest.mark.parametrize("slots", [None, "300"])
+def test_column_cache_trajectory_equals_the_oracle(monkeypatch, slots):
+    """The f update served from the column cache (forced on at 6k; with 300 slots the cache fills and
+    later misses take scratch slots) keeps the oracle's trajectory bit for bit, cold and warm."""
+    monkeypatch.setenv("SVM355_DECOMP_CCACHE", "1")
+    if slots:
+        monkeypatch.setenv("SVM355_DECOMP_CCACHE_SLOTS", slots)
+    n = 6000
+    tr = synthetic_mnist(n, seed=61).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    K = _exact_gram_host(Xu, mn, mx, n)
+    yd = torch.from_numpy(tr.y).to(DEV)
+    half = tr.subset(0, n // 2)
+    a_half = SVC(device="cuda:0", solver="decomp").fit(half.X, half.y).alpha_
+    for warm in (False, True):
+        a0 = np.concatenate([a_half, np.zeros(n - n // 2)]) if warm else np.zeros(n)
+        alpha = torch.from_numpy(a0.copy()).to(DEV)
+        dt = N.DecompTrace(400, n)
+        res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx, warm=warm, trace=dt)
+        a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), alpha=a0 if warm else None,
+                                                 trace_cap=400, snapshots=True)
+        _compare(dt, ot)
+        a = alpha.cpu().numpy()
+        np.testing.assert_array_equal(a, a_o)
+        assert res.stop_reason == r_o.stop_reason == "converged" and res.b == r_o.b
+
+
+@pytest.mark.parametrize("n", [60000, 250000])
+def test_column_cache_is_bit_identical_at_large_n(monkeypatch, n):
+    """The cache (SVM355_DECOMP_CCACHE=1; the default from ~200k rows) against the GEMV path
+    (SVM355_DECOMP_CCACHE=0): the same alpha, b and iteration counts."""
+    tr = synthetic_mnist(n, seed=2024).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    yd = torch.from_numpy(tr.y).to(DEV)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SVM355_DECOMP_CCACHE", flag)
+        alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+        res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx)
+        out[flag] = (alpha.cpu().numpy(), res.b, res.iterations, tm["outer_iterations"], res.stop_reason)
+    np.testing.assert_array_equal(out["0"][0], out["1"][0])
+    assert out["0"][1:] == out["1"][1:] and out["1"][4] == "converged"
