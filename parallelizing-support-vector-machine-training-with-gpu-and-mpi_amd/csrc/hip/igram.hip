@@ -625,13 +625,18 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 }
 
 // Narrow column store (decomposition column cache, <= kNarrowCols missing columns per f update): the
-// columns are the B operand resident in LDS, 32 at a time, and every wave streams 32-row tiles of Q
-// straight from HBM into its MFMA A fragments (four k-steps in flight), so an update that misses a
-// handful of columns reads Q once at streaming rate instead of paying the 128 x 64 tiled pass.  The
-// (lane, byte) -> k map, the extra groups' FP64 flushes in k-step order, the exact integer D0 and the
-// epilogue arithmetic are igram_tri_kernel's, so every stored value equals the GEMV's bit for bit.
+// columns are resident in LDS, 32 at a time, and every wave streams 32-row tiles of Q straight from
+// HBM into its MFMA fragments, so an update that misses a handful of columns reads Q once at streaming
+// rate instead of paying the 128 x 64 tiled pass.  The MFMA takes the COLUMNS as its A operand and the
+// rows as B: the accumulator is K^T, lane l32 holds row l32 of the tile and register r column
+// (r & 3) + 8 (r >> 2) + 4 h, so a store of register r writes two 256-byte runs of consecutive rows
+// of two columns (the igram layout wrote 32 B pieces of 32 columns per store: 1.7 TB/s), the row
+// norms are the lane's own, and whole quarters of registers whose columns lie beyond the group are
+// skipped.  The integer products are exact and every (row, column) entry sees the same extra-group
+// FP64 flushes in k-step order and the same epilogue arithmetic as igram_tri_kernel, so every stored
+// value equals the GEMV's bit for bit.
 constexpr int kNarrowCols = 64;
-constexpr int kNarrowMaxKq = 1536;  // 32 x (kq + 16) bytes of B in LDS
+constexpr int kNarrowMaxKq = 1536;  // 32 x (kq + 16) bytes of columns in LDS
 template <bool EXTRA>
 __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
@@ -641,19 +646,23 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused) {
   __shared__ double sw[kMaxSteps];
   __shared__ double wn_c[32];
-  __shared__ int32_t n0_c[32], id_c[32], sl_c[32];
+  __shared__ int64_t off_c[32];
+  __shared__ int32_t n0_c[32], id_c[32];
   extern __shared__ __attribute__((aligned(16))) char nsm[];
   const int cnt = *count;
   if (cnt <= 0 || cnt > kNarrowCols) return;  // nothing missing, or the tiled column store's update
   const int LS = kq + 16;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, l32 = lane & 31, h = lane >> 5;
-  const int nsteps = kq / 32, main_step0 = main0 / 32;
+  const int main_step0 = main0 / 32;
   if (EXTRA)
     for (int k = t; k < main_step0; k += 256) sw[k] = step_w[k];
   const int64_t tiles = (n + 31) / 32;
   const int64_t wave0 = int64_t(blockIdx.x) * 4 + w, nwaves = int64_t(gridDim.x) * 4;
   const i32x4 zero4 = {0, 0, 0, 0};
   const i32x16 zero16 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // only the k-steps holding columns (kused: the trailing pad of kq is zero in every row, so its
+  // MFMAs would add 0); a partial last chunk of 4 steps loads zeros for the steps beyond
+  const int nsu = kused / 32, nch = (nsu + 3) / 4;  // nch * 4 <= kq / 32: kq is a multiple of 128
   for (int g0 = 0; g0 < cnt; g0 += 32) {
     const int gc = min(32, cnt - g0);
     __syncthreads();  // the previous group's columns are consumed
@@ -661,7 +670,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
       const bool ok = t < gc;
       const int32_t id = ok ? ids[g0 + t] : -1;
       id_c[t] = id;
-      sl_c[t] = ok ? slots[g0 + t] : 0;
+      off_c[t] = ok ? int64_t(slots[g0 + t]) * ldc : 0;
       n0_c[t] = ok ? N0c[id] : 0;
       if (EXTRA) wn_c[t] = ok ? WNc[id] : 0.0;
     }
@@ -672,18 +681,10 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
       *reinterpret_cast<i32x4*>(nsm + col * LS + ch * 16) = v;
     }
     __syncthreads();
-    const int32_t nbj = n0_c[l32];
-    const double wbj = EXTRA ? wn_c[l32] : 0.0;
-    const int64_t gid = id_c[l32];
-    const bool colok = l32 < gc;
-    double* dst = cache + int64_t(sl_c[l32]) * ldc;
-    const char* bcol = nsm + l32 * LS + 16 * h;
+    const char* bcol = nsm + l32 * LS + 16 * h;  // column l32's fragment (the A operand)
     // the wave's (tile, chunk of 4 k-steps) positions as one stream, loads one chunk ahead (across tile
     // boundaries: the next tile's first chunk is in flight during this tile's epilogue; two ahead
     // measured the same)
-    // only the k-steps holding columns (kused: the trailing pad of kq is zero in every row, so its
-    // MFMAs would add 0); a partial last chunk loads zeros for the steps beyond
-    const int nsu = kused / 32, nch = (nsu + 3) / 4;  // nch * 4 <= nsteps: kq is a multiple of 128
     int64_t lt = wave0;
     int lc = 0;
     auto ld = [&](i32x4(&dst)[4]) {
@@ -700,11 +701,11 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     i32x4 p0[4];
     ld(p0);
     for (int64_t tile = wave0; tile < tiles; tile += nwaves) {
-      // the tile's row norms, loaded now (lane l32: row l32) and shuffled to the accumulator layout in
-      // the epilogue, so their latency hides behind the k-loop
-      const int64_t nr = tile * 32 + l32 < n ? tile * 32 + l32 : 0;
-      const int32_t n0_mine = N0[nr];
-      const double wn_mine = EXTRA ? WN[nr] : 0.0;
+      // the lane's row norms, loaded now so their latency hides behind the k-loop
+      const int64_t gi = tile * 32 + l32;
+      const bool rowok = gi < n;
+      const int32_t n0_row = N0[rowok ? gi : 0];
+      const double wn_row = EXTRA ? WN[rowok ? gi : 0] : 0.0;
       i32x16 acc = zero16;
       double xacc[16];
 #pragma unroll
@@ -720,42 +721,41 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
           const int step = 4 * c + u;
           const i32x4 b = *reinterpret_cast<const i32x4*>(bcol + step * 32);
           if (EXTRA && fresh) {
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur[u], b, zero16, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, cur[u], zero16, 0, 0, 0);
             fresh = false;
           } else {
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur[u], b, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, cur[u], acc, 0, 0, 0);
           }
           if (EXTRA && step < main_step0) {
             const double wgt = sw[step];
             if (wgt != 0.0) {  // last k-step of an extra group: flush its exact cross term
 #pragma unroll
-              for (int r = 0; r < 16; ++r) xacc[r] += wgt * double(acc[r]);
+              for (int r = 0; r < 16; ++r)
+                if (2 * (r & ~3) < gc) xacc[r] += wgt * double(acc[r]);  // quarters of real columns only
               fresh = true;
             }
           }
         }
       }
-      const int64_t row0 = tile * 32 + 4 * h;
 #pragma unroll
-      for (int qtr = 0; qtr < 4; ++qtr) {  // exp_batch is elementwise: quarters keep the registers low
+      for (int qtr = 0; qtr < 4; ++qtr) {  // registers 4 qtr .. 4 qtr + 3: columns 8 qtr + 4 h + (0..3)
+        if (8 * qtr >= gc) break;
         double ex[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int r = 4 * qtr + q;
-          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;  // the row's lane (row0 - tile * 32 = 4 h)
-          const int32_t D0 = __shfl(n0_mine, rl, 64) + nbj - 2 * acc[r];
+          const int r = 4 * qtr + q, cc = q + 8 * qtr + 4 * h;
+          const int32_t D0 = n0_row + n0_c[cc] - 2 * acc[r];
           double dist = w0 * double(D0);
-          if (EXTRA) dist += (__shfl(wn_mine, rl, 64) + wbj) - 2.0 * xacc[r];
+          if (EXTRA) dist += (wn_row + wn_c[cc]) - 2.0 * xacc[r];
           dist = dist > 0.0 ? dist : 0.0;
           ex[q] = neg_gamma * dist;
         }
         exp_batch<4>(ex);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int r = 4 * qtr + q;
-          const int64_t gi = row0 + (r & 3) + 8 * (r >> 2);
-          const double kv = gi + row_off == gid ? 1.0 : ex[q];
-          if (colok && gi < n) dst[gi] = kv;
+          const int cc = q + 8 * qtr + 4 * h;
+          const double kv = gi + row_off == int64_t(id_c[cc]) ? 1.0 : ex[q];
+          if (cc < gc && rowok) cache[off_c[cc] + gi] = kv;
         }
       }
     }

@@ -30,6 +30,7 @@ import numpy as np
 
 from ..utils.config import SVMParams, default_threads
 from ..utils.data import MinMaxScaler
+from ..utils.trace import trace_range
 
 
 class OneVsRestSVC:
@@ -145,7 +146,8 @@ class OneVsRestSVC:
             mm = torch.cat([mn, mx]).cpu().numpy()
             mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
             t1 = time.perf_counter()
-            K = D.rbf_gram_u8(Xu, self.params.gamma, mn_h, mx_h, out=D.gram_buffer(X.shape[0], device))
+            with trace_range("svm355.ovr.gram"):
+                K = D.rbf_gram_u8(Xu, self.params.gamma, mn_h, mx_h, out=D.gram_buffer(X.shape[0], device))
             path = "int8-exact"
         if K is None:
             Xu = None
@@ -176,27 +178,28 @@ class OneVsRestSVC:
         mine = [k for k in range(len(ys)) if self._mine(k)]
         results = {}
         self.batched_ = False
-        if self.solver in ("auto", "batched") and mine:
-            # One launch: an XCD-local team per XCD, classes pulled from a queue (smo_multi_kernel).
-            Yb = torch.stack([ys_d[k] for k in mine]).contiguous()
-            Ab = torch.zeros((len(mine), n), dtype=torch.float64, device=device)
-            rs, self.batched_ = D.smo_multi(K, Yb, Ab, self.params, n=n)
-            alphas[mine] = Ab
-            results = dict(zip(mine, rs))
-        workers = max(1, min(self.concurrent_solves, len(mine)))
-        if results:
-            pass
-        elif workers > 1:
-            from concurrent.futures import ThreadPoolExecutor
+        with trace_range(f"svm355.ovr.solve classes={len(mine)}"):
+            if self.solver in ("auto", "batched") and mine:
+                # One launch: an XCD-local team per XCD, classes pulled from a queue (smo_multi_kernel).
+                Yb = torch.stack([ys_d[k] for k in mine]).contiguous()
+                Ab = torch.zeros((len(mine), n), dtype=torch.float64, device=device)
+                rs, self.batched_ = D.smo_multi(K, Yb, Ab, self.params, n=n)
+                alphas[mine] = Ab
+                results = dict(zip(mine, rs))
+            workers = max(1, min(self.concurrent_solves, len(mine)))
+            if results:
+                pass
+            elif workers > 1:
+                from concurrent.futures import ThreadPoolExecutor
 
-            with ThreadPoolExecutor(max_workers=workers) as ex:  # the native calls release the GIL
-                results = dict(zip(mine, ex.map(solve, mine)))
-        else:
-            results = {k: solve(k) for k in mine}
-        bs = [results[k].b if k in results else 0.0 for k in range(len(ys))]
-        iters = [results[k].iterations if k in results else 0 for k in range(len(ys))]
-        stops = [results[k].stop_reason if k in results else "" for k in range(len(ys))]
-        torch.cuda.synchronize(device)
+                with ThreadPoolExecutor(max_workers=workers) as ex:  # the native calls release the GIL
+                    results = dict(zip(mine, ex.map(solve, mine)))
+            else:
+                results = {k: solve(k) for k in mine}
+            bs = [results[k].b if k in results else 0.0 for k in range(len(ys))]
+            iters = [results[k].iterations if k in results else 0 for k in range(len(ys))]
+            stops = [results[k].stop_reason if k in results else "" for k in range(len(ys))]
+            torch.cuda.synchronize(device)
         alphas, bs, iters, stops = self._combine(alphas, bs, iters, stops)
         t3 = time.perf_counter()
         del K

@@ -19,6 +19,7 @@ import numpy as np
 
 from .. import _native as N
 from ..utils.config import SVMParams
+from ..utils.trace import trace_range
 
 LAYER_NAMES = {0: "local", -1: "merge"}
 SOLVER_NAMES = {0: "smo", 1: "decomp"}
@@ -123,8 +124,9 @@ class CascadeSVM:
 
             X = np.ascontiguousarray(X, dtype=np.uint8 if X.dtype == np.uint8 else np.float64)
             g = group or DeviceGroup.shared(world, transport)
-            p = N.hip().svmd_cascade_group_fit(g.handle, N.ptr(X), int(X.dtype == np.uint8), N.ptr(y), X.shape[0],
-                                               X.shape[1], ctypes.byref(self.cfg))
+            with trace_range(f"svm355.cascade.{self.topology} world={world} solver={self.solver_used}"):
+                p = N.hip().svmd_cascade_group_fit(g.handle, N.ptr(X), int(X.dtype == np.uint8), N.ptr(y),
+                                                   X.shape[0], X.shape[1], ctypes.byref(self.cfg))
             if not p:
                 err = N.last_error()
                 if group is None and g.broken:  # aborted communicators: the next fit builds a new group

@@ -32,6 +32,7 @@ import numpy as np
 
 from .. import _native as N
 from ..utils.config import SVMParams
+from ..utils.trace import trace_range
 
 
 def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: int, world: int) -> dict:
@@ -47,8 +48,9 @@ def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: 
     ms = np.zeros(max(world, 1), dtype=np.float64)
     p = params.to_struct()
     t0 = time.perf_counter()
-    N.check(fn(handle, N.ptr(X), N.ptr(y), n, d, ctypes.byref(p), int(q), N.ptr(alpha), ctypes.byref(r), st,
-               N.ptr(ms), N.ptr(mm)), fn.__name__)
+    with trace_range(f"svm355.decomp.solve world={world} n={n}"):
+        N.check(fn(handle, N.ptr(X), N.ptr(y), n, d, ctypes.byref(p), int(q), N.ptr(alpha), ctypes.byref(r), st,
+                   N.ptr(ms), N.ptr(mm)), fn.__name__)
     wall = (time.perf_counter() - t0) * 1e3
     return {"alpha": alpha, "b": float(r.b), "b_high": float(r.b_high), "b_low": float(r.b_low),
             "iterations": int(r.iterations), "stop_reason": N.STOP_NAMES.get(int(r.stop_reason), str(r.stop_reason)),
@@ -107,11 +109,12 @@ class DistributedDecompSVC:
         m.b_, m.intercept_ = out["b"], -out["b"]
         m.n_iter_, m.stop_reason_ = out["iterations"], out["stop_reason"]
         X = np.asarray(X)
-        if X.dtype == np.uint8:
-            m._device_model_from_u8(X[sup], dev)
-        else:  # pixel values held as FP64 (validated integers): widened on the host
-            m.support_vectors_ = m.scaler_.transform(X[sup])
-            m._upload_model(dev)
+        with trace_range("svm355.decomp.model"):
+            if X.dtype == np.uint8:
+                m._device_model_from_u8(X[sup], dev)
+            else:  # pixel values held as FP64 (validated integers): widened on the host
+                m.support_vectors_ = m.scaler_.transform(X[sup])
+                m._upload_model(dev)
         self.model_ = m
         self.alpha_, self.support_, self.b_ = a, sup, out["b"]
         self.n_iter_, self.stop_reason_ = out["iterations"], out["stop_reason"]
