@@ -9,8 +9,8 @@ export TMPDIR=/tmp SVM355_CASCADE_SERIAL_SOLVES=1
 for solver in ${SOLVERS:-auto decomp smo}; do
 for topo in star tree; do
   for P in 2 4 8; do
-    f=gpurun_out/r4crit_${solver}_${topo}_P$P
-    sarg="--solver $solver"; [ "$solver" = auto ] && sarg=""
+    f=gpurun_out/r4crit_${solver}${WSS:+_$WSS}_${topo}_P$P
+    sarg="--solver $solver"; [ "$solver" = auto ] && sarg=""; [ -n "$WSS" ] && sarg="$sarg --wss $WSS"
     timeout -k 10 300 python -u bench.py --gpus $P --cascade $sarg --topology $topo --transport loopback \
       --steps 2 --warmup 1 --baseline-1gpu 0 --out $f.json > $f.log 2>&1 || { tail -20 $f.log; exit 1; }
     python - "$f.json" "$solver $topo P=$P" <<'PY'
