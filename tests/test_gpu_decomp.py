@@ -162,12 +162,20 @@ def test_decomp_rejects_an_inner_stop_that_cannot_progress(monkeypatch):
     assert m.stop_reason_ == "converged" and len(m.support_) > 0
 
 
-@pytest.mark.parametrize("n,world", [(6000, 2), (6000, 8), (20000, 4)])
-def test_distributed_rehearsal_equals_one_gpu(n, world):
+@pytest.mark.parametrize("n,world,ccache", [(6000, 2, None), (6000, 8, None), (20000, 4, None), (6000, 2, "1"),
+                                             (20000, 4, "300")])
+def test_distributed_rehearsal_equals_one_gpu(n, world, ccache, monkeypatch):
     """P ranks rehearsed on the one GPU (loopback transport, thread ranks): the global block partition
-    makes every working set, alpha, b and iteration count the one-GPU decomposition solver's."""
+    makes every working set, alpha, b and iteration count the one-GPU decomposition solver's.  ccache:
+    the column cache forced on (each rank caches its own rows' slice: row offsets in the store and the
+    diagonal), "300": with 300 slots per rank (full caches, scratch slots)."""
     from svm355.parallel.decomp import DistributedDecompSVC
     from svm355.parallel.rccl import DeviceGroup
+
+    if ccache:
+        monkeypatch.setenv("SVM355_DECOMP_CCACHE", "1")
+        if ccache != "1":
+            monkeypatch.setenv("SVM355_DECOMP_CCACHE_SLOTS", ccache)
 
     tr = synthetic_mnist(n, seed=91).compact()
     one = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
