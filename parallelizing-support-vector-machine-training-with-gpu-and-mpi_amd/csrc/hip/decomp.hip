@@ -142,17 +142,21 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
 }
 
 // One workgroup over the L gathered candidates (Lr per GPU, GPU-major; the first Lh of each GPU's
-// are I_high picks, the rest I_low): b_high = min f over the I_high candidates, b_low = max f over
-// the I_low ones (the global extremes: every block's first pick is its own extreme), the stop test,
-// and the working set = the candidates' ids sorted, without duplicates (a free SV may be in both
-// lists), with their f (Wf).  Independent of the order the candidates arrive in.
-__global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restrict__ cand, int L, int Lr, int Lh,
+// are I_high picks, T per selection block, the rest I_low): b_high = min f over the I_high
+// candidates, b_low = max f over the I_low ones (the global extremes: every block's first pick is its
+// own extreme), the stop test, and the working set = the candidates' ids sorted, without duplicates (a
+// free SV may be in both lists), with their f (Wf).  No sort: selection blocks are disjoint id ranges
+// in candidate order (GPU-major, block-major), so a candidate's place in W is its block's offset (a
+// scan of the blocks' distinct counts) plus the number of distinct ids of its own block (2T picks)
+// below it -- four barriers instead of a 55-stage bitonic network.
+__global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restrict__ cand, int L, int Lr, int Lh, int T,
                                                           double tau, double tau_frac, int64_t max_iter,
                                                           int32_t* __restrict__ W, double* __restrict__ Wf,
                                                           DecompCtl* __restrict__ ctl, int32_t* __restrict__ mcount) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   __shared__ int32_t s[kMaxWS];
-  __shared__ double sf[kMaxWS];
+  __shared__ int8_t kf[kMaxWS];
+  __shared__ int32_t bcnt[kMaxWS / 2];
   __shared__ int32_t wsum[kMaxWS / 64];
   __shared__ double red[2][kMaxWS / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -172,38 +176,41 @@ __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restr
     red[0][w] = vh;
     red[1][w] = vl;
   }
-  s[t] = c.id >= 0 ? c.id : INT_MAX;
-  sf[t] = c.f;
-  __syncthreads();
-  // bitonic sort of the 1024 candidate ids (ascending; INT_MAX = empty), f riding along
-  for (int k = 2; k <= kMaxWS; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int p = t ^ j;
-      if (p > t) {
-        const int32_t x = s[t], y = s[p];
-        const bool up = (t & k) == 0;
-        if ((x > y) == up) {
-          const double fx = sf[t];
-          s[t] = y;
-          s[p] = x;
-          sf[t] = sf[p];
-          sf[p] = fx;
-        }
-      }
-      __syncthreads();
-    }
+  // this candidate's selection block: its T high picks start at hb, its T low picks at hb + Lh
+  const int nb = L / (2 * T), nbr = Lh / T;
+  int blk = 0, hb = 0;
+  if (t < L) {
+    const int r = t / Lr, o = t - r * Lr, lb = (o < Lh ? o : o - Lh) / T;
+    blk = r * nbr + lb;
+    hb = r * Lr + lb * T;
   }
-  const int32_t v = s[t];
-  const bool keep = v != INT_MAX && (t == 0 || s[t - 1] != v);
-  const unsigned long long bal = __ballot(keep);
-  if (lane == 0) wsum[w] = __popcll(bal);
+  s[t] = c.id;
+  if (t < kMaxWS / 2) bcnt[t] = 0;
   __syncthreads();
-  int off = 0;
-  for (int q = 0; q < w; ++q) off += wsum[q];
+  // the block's first occurrence of an id is the one kept
+  bool keep = c.id >= 0;
+  if (keep)
+    for (int half = 0; half < 2; ++half)
+      for (int j = hb + half * Lh, je = j + T; j < je; ++j)
+        if (j < t && s[j] == c.id) keep = false;
+  kf[t] = keep;
+  if (keep) atomicAdd(&bcnt[blk], 1);
+  __syncthreads();
+  // exclusive scan of the blocks' distinct counts (nb <= 512 blocks)
+  const int bv = t < nb ? bcnt[t] : 0;
+  const int incl = wave_incl_scan(bv);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int wpre = 0;
+  for (int q = 0; q < w; ++q) wpre += wsum[q];
+  if (t < nb) bcnt[t] = wpre + incl - bv;
+  __syncthreads();
   if (keep) {
-    const int j = off + __popcll(bal & ((1ull << lane) - 1ull));
-    W[j] = v;
-    Wf[j] = sf[t];  // duplicates of an id carry the same f
+    int j = bcnt[blk];
+    for (int half = 0; half < 2; ++half)
+      for (int i = hb + half * Lh, ie = i + T; i < ie; ++i) j += (kf[i] != 0 && s[i] < c.id) ? 1 : 0;
+    W[j] = c.id;
+    Wf[j] = c.f;  // duplicates of an id carry the same f
   }
   if (t == 0) {
     int m = 0;
@@ -1136,8 +1143,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                            T, p.C, p.eps, cown, cown + NBr * T, ctl);
       SVMD_LAUNCH_CHECK();
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
-      hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), p.tau,
-                         tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount);
+      hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), int(T),
+                         p.tau, tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount);
       SVMD_LAUNCH_CHECK();
       if (!f64) {
         hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, Q, N0, WN, P.kq, W, ctl, Qw, N0w,
