@@ -61,6 +61,13 @@ struct DecompCtl {
 };
 constexpr int32_t kStopInternal = -100;
 
+// The control block's host copy, written by the kernel that last changes it in an outer iteration (the
+// inner solve, or the build when it stops the solve) with plain vector stores into pinned host memory:
+// visible to the host once the batch's event has completed, with no copy in the stream.
+__device__ __forceinline__ void publish_ctl(const DecompCtl& c, DecompCtl* __restrict__ pub) {
+  if (pub) *pub = c;
+}
+
 constexpr int kSelNT = 256, kSelE = 16;  // per-block selection: up to 4096 points per block
 constexpr int kMaxWS = 1024;             // working-set capacity (one 1024-thread inner workgroup)
 
@@ -152,7 +159,8 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
 __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restrict__ cand, int L, int Lr, int Lh, int T,
                                                           double tau, double tau_frac, int64_t max_iter,
                                                           int32_t* __restrict__ W, double* __restrict__ Wf,
-                                                          DecompCtl* __restrict__ ctl, int32_t* __restrict__ mcount) {
+                                                          DecompCtl* __restrict__ ctl, int32_t* __restrict__ mcount,
+                                                          DecompCtl* __restrict__ pub) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   __shared__ int32_t s[kMaxWS];
   __shared__ int8_t kf[kMaxWS];
@@ -236,6 +244,7 @@ __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restr
     if (st != SVM_STOP_RUNNING) {
       ctl->stop = st;
       *mcount = 0;  // the rest of the batch's f updates are no-ops
+      publish_ctl(*ctl, pub);
     } else {
       ctl->m = m;
       ctl->tau_in = fmax(tau, tau_frac * (bl - bh));
@@ -284,7 +293,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
                                                       const double* __restrict__ Wf, double C, double eps,
                                                       int32_t* __restrict__ cols, double* __restrict__ coef,
-                                                      int32_t* __restrict__ mcount, DecompHost* __restrict__ hs) {
+                                                      int32_t* __restrict__ mcount, DecompHost* __restrict__ hs,
+                                                      DecompCtl* __restrict__ pub) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   const int m = ctl->m;
   const double tau_in = ctl->tau_in;
@@ -599,6 +609,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     ctl->changed_total += base;
     ctl->last_inner_it = it;
     ctl->last_inner_reason = reason;
+    publish_ctl(*ctl, pub);
   }
 }
 
@@ -1125,7 +1136,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
   hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha, Wf,   \
-                     p.C, p.eps, cols, coef, mcount, hs)
+                     p.C, p.eps, cols, coef, mcount, hs, pub)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
     SVM_WS_INNER_(NT, PER, true, true);      \
@@ -1136,7 +1147,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
   const DecompCtl* fin = nullptr;  // the readback that saw the stop
+  DecompCtl* ctl_pub = nullptr;  // ctl_h as the device addresses it
+  SVMD_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctl_pub), ctl_h, 0));
   for (int64_t bt = 0;; ++bt) {
+    DecompCtl* pub = tr ? nullptr : ctl_pub + (bt & 1);  // the trace path copies the block itself
     for (int bi = 0; bi < batch; ++bi) {
       if (NBr > 0)
         hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
@@ -1144,7 +1158,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       SVMD_LAUNCH_CHECK();
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
       hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), int(T),
-                         p.tau, tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount);
+                         p.tau, tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount, pub);
       SVMD_LAUNCH_CHECK();
       if (!f64) {
         hipLaunchKernelGGL(ws_gather_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, Q, N0, WN, P.kq, W, ctl, Qw, N0w,
@@ -1219,8 +1233,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       }
       continue;
     }
-    SVMD_CHECK(hipMemcpyAsync(ctl_h + (bt & 1), ctl, sizeof(DecompCtl), hipMemcpyDeviceToHost, s));
-    SVMD_CHECK(hipEventRecord(ctx->ev_ctl[bt & 1], s));
+    SVMD_CHECK(hipEventRecord(ctx->ev_ctl[bt & 1], s));  // the batch's kernels published into ctl_h[bt & 1]
     if (bt == 0) continue;  // keep one batch queued ahead of the wait
     const int64_t pb = bt - 1;
     hipEvent_t ev = ctx->ev_ctl[pb & 1];
