@@ -1012,6 +1012,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const size_t o_cslot = use_cache ? take(size_t(n) * 4) : 0, o_crd = use_cache ? take(kMaxWS * 4) : 0,
                o_cmid = use_cache ? take(kMaxWS * 4) : 0, o_cmsl = use_cache ? take(kMaxWS * 4) : 0,
                o_cst = use_cache ? take(64) : 0;
+  // K(W, W) through the narrow column store: the identity ids 0 .. kMaxWS - 1 and the column count
+  const size_t o_wid = f64 ? 0 : take(kMaxWS * 4 + 64);
   // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
   const int64_t nchunks = (n + kMaxWS - 1) / kMaxWS;
   const size_t o_wcols = o.warm ? take(size_t(n) * 4) : 0, o_wcoef = o.warm ? take(size_t(n) * 8) : 0,
@@ -1044,6 +1046,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   auto* cmid = reinterpret_cast<int32_t*>(ws + o_cmid);
   auto* cmsl = reinterpret_cast<int32_t*>(ws + o_cmsl);
   auto* cst = reinterpret_cast<int32_t*>(ws + o_cst);
+  auto* wid = reinterpret_cast<int32_t*>(ws + o_wid);  // [kMaxWS] identity, then the count kMaxWS
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
   // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
   // order) or, for FP64 rows, the moved columns' rows gathered, their block on FP64 MFMA and a row sum
@@ -1086,6 +1089,17 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   std::memset(hs, 0, sizeof(DecompHost));
   SVMD_CHECK(hipMemsetAsync(ctl, 0, sizeof(DecompCtl), s));  // stop = SVM_STOP_RUNNING, counters 0
   if (f64) SVMD_CHECK(hipMemsetAsync(Xw, 0, size_t(kMaxWS) * R.ld * 8, s));  // rows beyond m stay finite
+  const char* kww = getenv("SVM355_DECOMP_KWW");  // "sym": the triangular Gram launch (A/B)
+  const bool kww_narrow = !f64 && !(kww && std::strcmp(kww, "sym") == 0) && P.kq <= 1536;
+  if (kww_narrow) {
+    static const std::vector<int32_t> ident = [] {
+      std::vector<int32_t> v(kMaxWS + 1);
+      for (int k = 0; k < kMaxWS; ++k) v[k] = k;
+      v[kMaxWS] = kMaxWS;
+      return v;
+    }();
+    SVMD_CHECK(hipMemcpyAsync(wid, ident.data(), ident.size() * 4, hipMemcpyHostToDevice, s));
+  }
   if (use_cache) {  // a fresh cache per fit: no point has a slot, the first free slot is 0
     SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
     SVMD_CHECK(hipMemsetAsync(cst, 0, 64, s));
@@ -1165,8 +1179,11 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                            WNw);
         SVMD_LAUNCH_CHECK();
         // K(W, W) over the full capacity (rows beyond m are never read); skipped once stopped
-        rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
-        if (rc) return rc;
+        if (!(kww_narrow && launch_igram_ww(s, Qw, N0w, WNw, stw, kMaxWS, wid, wid + kMaxWS, P, p.gamma, Kw, ldw,
+                                            gate))) {
+          rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
+          if (rc) return rc;
+        }
       } else {
         hipLaunchKernelGGL(ws_gather_f64_kernel, dim3(unsigned(kMaxWS)), dim3(64), 0, s, R.X, R.nrm, R.ld, W, &ctl->m,
                            gate, Xw, nw);

@@ -643,14 +643,17 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     const double* __restrict__ WN, const double* __restrict__ step_w, double w0, double neg_gamma,
     const int8_t* __restrict__ Qc, const int32_t* __restrict__ N0c, const double* __restrict__ WNc,
     const int32_t* __restrict__ ids, const int32_t* __restrict__ slots, const int32_t* __restrict__ count,
-    int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused) {
+    int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused, const int32_t* __restrict__ gate = nullptr,
+    bool gsplit = false) {
   __shared__ double sw[kMaxSteps];
   __shared__ double wn_c[32];
   __shared__ int64_t off_c[32];
   __shared__ int32_t n0_c[32], id_c[32];
   extern __shared__ __attribute__((aligned(16))) char nsm[];
+  if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch
   const int cnt = *count;
-  if (cnt <= 0 || cnt > kNarrowCols) return;  // nothing missing, or the tiled column store's update
+  // gsplit (a working set's K(W, W)): workgroup row blockIdx.y takes column group blockIdx.y only, any count
+  if (cnt <= 0 || (!gsplit && cnt > kNarrowCols)) return;  // nothing missing, or the tiled store's update
   const int LS = kq + 16;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, l32 = lane & 31, h = lane >> 5;
   const int main_step0 = main0 / 32;
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
   // only the k-steps holding columns (kused: the trailing pad of kq is zero in every row, so its
   // MFMAs would add 0); a partial last chunk of 4 steps loads zeros for the steps beyond
   const int nsu = kused / 32, nch = (nsu + 3) / 4;  // nch * 4 <= kq / 32: kq is a multiple of 128
-  for (int g0 = 0; g0 < cnt; g0 += 32) {
+  for (int g0 = gsplit ? int(blockIdx.y) * 32 : 0; g0 < cnt; g0 += gsplit ? cnt : 32) {
     const int gc = min(32, cnt - g0);
     __syncthreads();  // the previous group's columns are consumed
     if (t < 32) {
@@ -1209,6 +1212,34 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
 #undef SVM_IGRAM_CST
   SVMD_LAUNCH_CHECK();
   return SVM_OK;
+}
+
+// K(W, W) of a decomposition working set (decomp.hip): the gathered quantised rows (Qw, N0w, WNw; n of
+// them, rows beyond the set's size are stale but valid) against themselves through the narrow column
+// store -- column group g of 32 in workgroup row g, row tiles over the workgroup columns: 32 x 8
+// workgroups for 1,024 rows where the triangular Gram launch has 72, and the same kernel values bit
+// for bit.  ids: the identity 0 .. n-1 on the device (columns k at K + k * ldk; K(W, W) is symmetric,
+// so that is also its row k); the diagonal is 1 (local row == column).  false when kq is too wide.
+bool launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
+                     int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
+                     int64_t ldk, const int32_t* gate) {
+  if (P.kq > kNarrowMaxKq || n <= 0 || n > 32 * 65535) return false;
+  int kused = 0;
+  for (int k = int(P.perm.size()) - 1; k >= 0; --k)
+    if (P.perm[k] >= 0) {
+      kused = k + 1;
+      break;
+    }
+  kused = std::min(P.kq, (std::max(kused, 1) + 31) / 32 * 32);
+  const size_t lds = size_t(32) * (P.kq + 16);
+  const dim3 grid(unsigned((n + 127) / 128), unsigned((n + 31) / 32));
+  if (P.main0 > 0)
+    hipLaunchKernelGGL(igram_colstore_narrow_kernel<true>, grid, dim3(256), lds, s, Qw, n, P.kq, P.main0, N0w, WNw, stw,
+                       P.w0, -gamma, Qw, N0w, WNw, ids, ids, count, int64_t(0), K, ldk, kused, gate, true);
+  else
+    hipLaunchKernelGGL(igram_colstore_narrow_kernel<false>, grid, dim3(256), lds, s, Qw, n, P.kq, P.main0, N0w, WNw,
+                       stw, P.w0, -gamma, Qw, N0w, WNw, ids, ids, count, int64_t(0), K, ldk, kused, gate, true);
+  return hipGetLastError() == hipSuccess;
 }
 
 // K(rows [0, n), rows [col0, col0 + ncols)) of already quantised rows (Q, N0, WN; step weights
