@@ -677,11 +677,22 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
       n0_c[t] = ok ? N0c[id] : 0;
       if (EXTRA) wn_c[t] = ok ? WNc[id] : 0.0;
     }
+    // the group's columns into LDS, eight 16-byte loads in flight per thread (one at a time, the 9
+    // dependent round trips of a 1,152-byte column set were most of a K(W, W) workgroup's time)
     const int cpr = kq / 16;
-    for (int c = t; c < 32 * cpr; c += 256) {
-      const int col = c / cpr, ch = c - col * cpr;
-      const i32x4 v = col < gc ? *reinterpret_cast<const i32x4*>(Qc + int64_t(ids[g0 + col]) * kq + ch * 16) : zero4;
-      *reinterpret_cast<i32x4*>(nsm + col * LS + ch * 16) = v;
+    for (int c0 = 0; c0 < 32 * cpr; c0 += 256 * 8) {
+      i32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + t + 256 * u, col = c / cpr, ch = c - col * cpr;
+        v[u] = c < 32 * cpr && col < gc ? *reinterpret_cast<const i32x4*>(Qc + int64_t(ids[g0 + col]) * kq + ch * 16)
+                                        : zero4;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + t + 256 * u, col = c / cpr, ch = c - col * cpr;
+        if (c < 32 * cpr) *reinterpret_cast<i32x4*>(nsm + col * LS + ch * 16) = v[u];
+      }
     }
     __syncthreads();
     const char* bcol = nsm + l32 * LS + 16 * h;  // column l32's fragment (the A operand)
