@@ -16,5 +16,3 @@ import json
 a = json.load(open("gpurun_out/r4full_bench1.json"))
 print("1 GPU", a["value"], a["iterations"], a["b"], a["n_sv"], a["accuracy"], a.get("f64_input_fit_ms"), a["pairwise_solver"]["fit_ms"])
 PY
-SOLVERS=auto WSS=second bash scripts/gpu_r4_cascade_crit.sh > gpurun_out/r4crit_auto_second.txt 2>&1 || { tail -5 gpurun_out/r4crit_auto_second.txt; exit 1; }
-grep -v "per round" gpurun_out/r4crit_auto_second.txt
