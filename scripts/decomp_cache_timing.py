@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Decomposition fit time with the column cache off / on (SVM355_DECOMP_CCACHE, read per fit) at the
 sizes of argv: best of 3 fits after a warm-up, the alpha of both compared bit for bit
-(SVM355_DECOMP_CCACHE_FIXED=0|1: that setting only, for a profile).
+(SVM355_DECOMP_CCACHE_FIXED=0|1: that setting only, for a profile; SVM355_TIMING_VAR: the variable
+toggled instead of SVM355_DECOMP_CCACHE, e.g. SVM355_DECOMP_WCOLS).
 
     python scripts/decomp_cache_timing.py 60000 250000 1000000
 """
@@ -27,7 +28,7 @@ for n in [int(a) for a in sys.argv[1:]]:
     res = {}
     flags = (os.environ["SVM355_DECOMP_CCACHE_FIXED"],) if "SVM355_DECOMP_CCACHE_FIXED" in os.environ else ("0", "1")
     for flag in flags:
-        os.environ["SVM355_DECOMP_CCACHE"] = flag
+        os.environ[os.environ.get("SVM355_TIMING_VAR", "SVM355_DECOMP_CCACHE")] = flag
         best = 1e30
         for rep in range(4):
             alpha = torch.empty(n, dtype=torch.float64, device=dev)
