@@ -178,3 +178,32 @@ def test_column_cache_is_bit_identical_at_large_n(monkeypatch, n):
         out[flag] = (alpha.cpu().numpy(), res.b, res.iterations, tm["outer_iterations"], res.stop_reason)
     np.testing.assert_array_equal(out["0"][0], out["1"][0])
     assert out["0"][1:] == out["1"][1:] and out["1"][4] == "converged"
+
+
+@pytest.mark.parametrize("d,kww", [(784, "sym"), (1800, None)])
+def test_kww_paths_equal_the_oracle(monkeypatch, d, kww):
+    """K(W, W) from the triangular Gram launch (SVM355_DECOMP_KWW=sym; and, automatically, for rows
+    wider than the narrow store's 1,536 int8 columns) instead of the narrow column store: the same
+    trajectory as the CPU oracle, bit for bit."""
+    if kww:
+        monkeypatch.setenv("SVM355_DECOMP_KWW", kww)
+    n = 3000
+    rng = np.random.default_rng(d)
+    X = rng.integers(0, 256, size=(n, d)).astype(np.uint8)
+    X[:, : d // 3] = np.minimum(X[:, : d // 3], 12)  # an extra column group (12 does not divide 255)
+    y = np.where(X[:, :64].astype(np.int64).sum(1) > np.median(X[:, :64].astype(np.int64).sum(1)), 1, -1).astype(np.int32)
+    Xu = D.upload_u8(X, DEV)
+    mmd = torch.empty(2 * d, dtype=torch.float64, device=DEV)
+    D.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    mn, mx = mm[:d].copy(), mm[d:].copy()
+    K = _exact_gram_host(Xu, mn, mx, n)
+    yd = torch.from_numpy(y).to(DEV)
+    alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+    dt = N.DecompTrace(400, n)
+    res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx, trace=dt)
+    assert tm["gram_path"] == "int8-exact"
+    a_o, r_o, st_o, ot = C.decomp_train_gram(K, y, SVMParams(n_threads=8), trace_cap=400, snapshots=True)
+    _compare(dt, ot)
+    np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
+    assert res.b == r_o.b and res.stop_reason == r_o.stop_reason
