@@ -176,7 +176,8 @@ bool launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const 
 int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                           int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                           const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,
-                          const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate);
+                          const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate,
+                          bool tiled = true);
 int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
                  const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used);
 size_t igram_u8_workspace(int64_t n, const QuantPlan& P);

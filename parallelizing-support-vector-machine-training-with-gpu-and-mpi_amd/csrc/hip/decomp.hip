@@ -1050,14 +1050,17 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
   // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
   // order) or, for FP64 rows, the moved columns' rows gathered, their block on FP64 MFMA and a row sum
-  auto f_update = [&](const int32_t* cl, const double* cf, const int32_t* cnt) -> int {
+  // tiled: also launch the tiled column store for updates of more than 64 misses (it exits at once
+  // otherwise, but a launch over every row tile costs ~5-8 us); off after the first outer iterations,
+  // where the narrow store takes any count itself (only the cold start misses hundreds of columns)
+  auto f_update = [&](const int32_t* cl, const double* cf, const int32_t* cnt, bool tiled = true) -> int {
     if (nloc <= 0) return SVM_OK;
     if (use_cache) {  // plan the slots, compute and store the missing columns, sum every column from the cache
       hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cl, cnt, cslot, cache_cap, cst, crd, cmid,
                          cmsl);
       SVMD_LAUNCH_CHECK();
       const int rc2 = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid,
-                                            cmsl, cst + 1, kMaxWS, P, p.gamma, cache, ldc_cache, cst + 2);
+                                            cmsl, cst + 1, kMaxWS, P, p.gamma, cache, ldc_cache, cst + 2, tiled);
       if (rc2) return rc2;
       hipLaunchKernelGGL((ws_cache_fsum_kernel<2>), dim3(unsigned((nloc + 511) / 512)), dim3(256), 0, s, cache,
                          ldc_cache, crd, cf, cnt, f, nloc);
@@ -1204,7 +1207,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       else
         SVM_WS_INNER(512, 2);
       SVMD_LAUNCH_CHECK();
-      rc = f_update(cols, coef, mcount);
+      rc = f_update(cols, coef, mcount, bt * batch + bi < 4);
       if (rc) return rc;
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_

@@ -644,7 +644,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     const int8_t* __restrict__ Qc, const int32_t* __restrict__ N0c, const double* __restrict__ WNc,
     const int32_t* __restrict__ ids, const int32_t* __restrict__ slots, const int32_t* __restrict__ count,
     int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused, const int32_t* __restrict__ gate = nullptr,
-    bool gsplit = false) {
+    bool gsplit = false, bool all = false) {
   __shared__ double sw[kMaxSteps];
   __shared__ double wn_c[32];
   __shared__ int64_t off_c[32];
@@ -653,7 +653,8 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
   if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch
   const int cnt = *count;
   // gsplit (a working set's K(W, W)): workgroup row blockIdx.y takes column group blockIdx.y only, any count
-  if (cnt <= 0 || (!gsplit && cnt > kNarrowCols)) return;  // nothing missing, or the tiled store's update
+  // all: no tiled store was launched for this update, so every count is this kernel's (32 columns a pass)
+  if (cnt <= 0 || (!gsplit && !all && cnt > kNarrowCols)) return;  // nothing missing, or the tiled store's
   const int LS = kq + 16;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, l32 = lane & 31, h = lane >> 5;
   const int main_step0 = main0 / 32;
@@ -1169,8 +1170,10 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
 int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                           int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                           const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,
-                          const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate) {
+                          const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate,
+                          bool tiled) {
   if (n <= 0 || m <= 0) return SVM_OK;
+  const bool narrow_all = !tiled && gate && P.kq <= kNarrowMaxKq;  // the narrow store alone, any count
   if (gate && P.kq <= kNarrowMaxKq) {  // <= kNarrowCols columns: the streaming kernel (the tiled one exits)
     const int64_t tiles = (n + 31) / 32;
     const size_t lds = size_t(32) * (P.kq + 16);
@@ -1192,11 +1195,14 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
     const unsigned nwg = unsigned(std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, int64_t(cus) * std::max(per_cu, 1))));
     if (P.main0 > 0)
       hipLaunchKernelGGL(igram_colstore_narrow_kernel<true>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
-                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused);
+                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused, nullptr,
+                         false, narrow_all);
     else
       hipLaunchKernelGGL(igram_colstore_narrow_kernel<false>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
-                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused);
+                         WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused, nullptr,
+                         false, narrow_all);
     SVMD_LAUNCH_CHECK();
+    if (narrow_all) return SVM_OK;
   }
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
   int64_t gc = tiles >= 256 ? -1 : 0;  // the GEMV's grid rule (launch_igram_gemv)
