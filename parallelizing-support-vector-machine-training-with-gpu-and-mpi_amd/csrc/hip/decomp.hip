@@ -80,8 +80,9 @@ struct CandRec {
 
 // Per block b of `per` points of this GPU's slice (local rows [b per, (b + 1) per), global ids lo +
 // local): the T most violating points of I_high (smallest f) and of I_low (largest f) in wave_arg's
-// order (value, then lowest index): T rounds of a block arg-reduction, the winner masked out by its
-// owner after each round.  f is the slice's (local index); alpha and y are global.
+// order (value, then lowest index): every wave's own T best by T wave arg-reductions (the winner
+// masked out by its owner after each), then a 4-way merge of the sorted wave lists.  f is the slice's
+// (local index); alpha and y are global.
 __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restrict__ f,
                                                            const double* __restrict__ alpha,
                                                            const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
@@ -90,8 +91,6 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
                                                            const DecompCtl* __restrict__ ctl) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   constexpr int NW = kSelNT / 64;
-  __shared__ double sv[2][NW];
-  __shared__ uint32_t si[2][NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t b0 = int64_t(blockIdx.x) * per, b1 = std::min<int64_t>(nloc, b0 + per);
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
@@ -108,6 +107,12 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
       if ((yi == 1 && a > c_lo) || (yi == -1 && a < c_hi)) fl[e] = fi;
     }
   }
+  // Every wave takes its own T best of each side with wave reductions only (no barrier per pick), then
+  // the block's T best are the first T of the merge of the four sorted wave lists: the same picks in
+  // the same order as T rounds of a block arg-reduction (the keys (value, index) are distinct).
+  constexpr int kTMax = 64;  // T <= q / (2 * 8 blocks)
+  __shared__ double lv[2][NW][kTMax];
+  __shared__ uint32_t li[2][NW][kTMax];
   for (int k = 0; k < T; ++k) {
     VI mn{inf, kSentinel}, mx{-inf, kSentinel};
 #pragma unroll
@@ -120,30 +125,40 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
     VIL a, b;
     wave_arg_pair(mn, mx, a, b);
     if (lane == 0) {
-      sv[0][w] = a.v;
-      si[0][w] = a.i;
-      sv[1][w] = b.v;
-      si[1][w] = b.i;
-    }
-    __syncthreads();
-    VI gm{sv[0][0], si[0][0]}, gx{sv[1][0], si[1][0]};
-#pragma unroll
-    for (int q = 1; q < NW; ++q) {
-      const VI cm{sv[0][q], si[0][q]}, cx{sv[1][q], si[1][q]};
-      if (beats<true>(cm, gm)) gm = cm;
-      if (beats<false>(cx, gx)) gx = cx;
-    }
-    __syncthreads();  // the LDS slots are rewritten next round
-    if (t == 0) {
-      const bool hok = gm.i != kSentinel && gm.v < inf, lok = gx.i != kSentinel && gx.v > -inf;
-      cand_h[int64_t(blockIdx.x) * T + k] = CandRec{hok ? gm.v : 0.0, hok ? int32_t(gm.i) : -1, 0};
-      cand_l[int64_t(blockIdx.x) * T + k] = CandRec{lok ? gx.v : 0.0, lok ? int32_t(gx.i) : -1, 0};
+      lv[0][w][k] = a.v;
+      li[0][w][k] = a.i;
+      lv[1][w][k] = b.v;
+      li[1][w][k] = b.i;
     }
 #pragma unroll
     for (int e = 0; e < kSelE; ++e) {
       const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
-      if (i == gm.i) fh[e] = inf;
-      if (i == gx.i) fl[e] = -inf;
+      if (i == a.i) fh[e] = inf;
+      if (i == b.i) fl[e] = -inf;
+    }
+  }
+  __syncthreads();
+  if (t == 0 || t == 64) {  // wave 0 merges I_high, wave 1 I_low
+    const int sd = t == 0 ? 0 : 1;
+    int ptr[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) ptr[q] = 0;
+    CandRec* out = (sd == 0 ? cand_h : cand_l) + int64_t(blockIdx.x) * T;
+    for (int k = 0; k < T; ++k) {
+      int bq = 0;
+      VI best{lv[sd][0][ptr[0]], li[sd][0][ptr[0]]};
+#pragma unroll
+      for (int q = 1; q < NW; ++q) {
+        const VI c{lv[sd][q][ptr[q]], li[sd][q][ptr[q]]};
+        const bool take = sd == 0 ? beats<true>(c, best) : beats<false>(c, best);
+        if (take) {
+          best = c;
+          bq = q;
+        }
+      }
+      ++ptr[bq];  // a wave's list holds T entries: no list runs out before T picks
+      const bool ok = best.i != kSentinel && (sd == 0 ? best.v < inf : best.v > -inf);
+      out[k] = CandRec{ok ? best.v : 0.0, ok ? int32_t(best.i) : -1, 0};
     }
   }
 }
