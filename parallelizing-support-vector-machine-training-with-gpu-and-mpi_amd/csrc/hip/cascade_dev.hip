@@ -877,6 +877,10 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   bool used = false;
   double prep = 0.0;
   svm_result res{};
+  // fault injection (tests): this rank fails while the others wait in the solve's first candidate
+  // all-gather; the group's abort must end every rank with an error, not a hang
+  if (const char* fr = getenv("SVM355_DECOMP_FAIL_RANK"); fr && world > 1 && atoi(fr) == rank)
+    throw CascadeError("injected failure before the solve");
   check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, o),
         "decomposition SMO");
   if (!used) throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan)");

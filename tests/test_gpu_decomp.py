@@ -3,6 +3,8 @@ reference's pairwise solve (``solver="smo"``) on the same rows.  The two reach t
 all n points by different pair sequences, so the checks are the optimality conditions themselves
 (recomputed on the host from the final alphas and an independent Gram), the support-vector set and
 b within the stop tolerance -- not a bit-identical trajectory."""
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -205,4 +207,29 @@ def test_distributed_process_rank_world1_equals_one_gpu():
     finally:
         rk.close()
     assert m.n_iter_ == one.n_iter_ and m.b_ == one.b_
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
+
+
+def test_distributed_rank_failure_ends_every_rank(monkeypatch):
+    """A rank that fails (SVM355_DECOMP_FAIL_RANK) while the others wait in the solve's candidate
+    all-gather: the group's abort ends every rank with the error instead of a hang, and the loopback
+    group stays usable for the next fit."""
+    from svm355._native import NativeError
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.rccl import DeviceGroup
+
+    tr = synthetic_mnist(4000, seed=95).compact()
+    g = DeviceGroup(2, "loopback")
+    try:
+        monkeypatch.setenv("SVM355_DECOMP_FAIL_RANK", "1")
+        t0 = time.perf_counter()
+        with pytest.raises(NativeError, match="injected failure"):
+            DistributedDecompSVC(2, group=g).fit(tr.X, tr.y)
+        assert time.perf_counter() - t0 < 60
+        monkeypatch.delenv("SVM355_DECOMP_FAIL_RANK")
+        m = DistributedDecompSVC(2, group=g).fit(tr.X, tr.y)
+    finally:
+        g.close()
+    one = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    assert m.stop_reason_ == "converged" and m.b_ == one.b_
     np.testing.assert_array_equal(m.alpha_, one.alpha_)
