@@ -30,6 +30,7 @@ namespace {
 
 constexpr int kMaxWS = SVM_DECOMP_MAX_WS;
 constexpr int64_t kSelPts = 256 * 16;  // points per selection block at most (ws_select_kernel)
+constexpr int kInnerNT = 256;           // the device's inner workgroup (ws_inner_kernel<256, 4>)
 
 struct Shape {
   bool ok = false;
@@ -252,6 +253,20 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
         reason = SVM_STOP_MAX_ITER;
         break;
       }
+      // inner_wss 3: the second pair from the same selection (ws_inner_kernel DP): i2 = the best I_high
+      // point outside i_high's wave of the 256-thread inner workgroup (position k lies in wave
+      // (k mod 512) / 128), j2 = the first-order j
+      int i2 = -1;
+      const int j2 = il;
+      if (inner_wss == 3) {
+        const int wih = (ih % (2 * kInnerNT)) / 128;
+        double v2 = inf;
+        for (int k = 0; k < m; ++k)
+          if ((k % (2 * kInnerNT)) / 128 != wih && in_high(yw[size_t(k)], a[size_t(k)]) && ft[size_t(k)] < v2) {
+            v2 = ft[size_t(k)];
+            i2 = k;
+          }
+      }
       const double* Ki = K + int64_t(W[size_t(ih)]) * ldk;
       for (int k = 0; k < m; ++k) kh[size_t(k)] = Ki[W[size_t(k)]];
       double bl_upd = lv;
@@ -309,6 +324,35 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
       a[size_t(ih)] = ah_new;
       a[size_t(il)] = al_new;
       ++it;
+      if (i2 >= 0 && j2 != ih && i2 != j2 && il != j2 && il != i2 && it < max_inner) {
+        const double fi2 = ft[size_t(i2)], fj2 = ft[size_t(j2)];  // after the first update
+        const double a2h = a[size_t(i2)], a2l = a[size_t(j2)];
+        const int32_t yh2 = yw[size_t(i2)], yl2 = yw[size_t(j2)];
+        const int s2 = yh2 * yl2;
+        const double eta2 = 1.0 + 1.0 - 2.0 * K[int64_t(W[size_t(i2)]) * ldk + W[size_t(j2)]];
+        double U2, V2;
+        if (s2 == -1) {
+          U2 = std::fmax(0.0, a2l - a2h);
+          V2 = std::fmin(C, C + a2l - a2h);
+        } else {
+          U2 = std::fmax(0.0, a2l + a2h - C);
+          V2 = std::fmin(C, a2l + a2h);
+        }
+        if (fj2 > fi2 + 2.0 * tau_in && U2 <= V2 + 1e-12 && !(eta2 <= eps)) {
+          double al2 = a2l + double(yl2) * (fi2 - fj2) / eta2;
+          if (al2 > V2) al2 = V2;
+          if (al2 < U2) al2 = U2;
+          const double ah2 = a2h + double(s2) * (a2l - al2);
+          const double ch2 = (ah2 - a2h) * double(yh2);
+          const double cl2 = (al2 - a2l) * double(yl2);
+          const double* Ki2 = K + int64_t(W[size_t(i2)]) * ldk;
+          const double* Kj2 = K + int64_t(W[size_t(j2)]) * ldk;
+          for (int k = 0; k < m; ++k) ft[size_t(k)] += ch2 * Ki2[W[size_t(k)]] + cl2 * Kj2[W[size_t(k)]];
+          a[size_t(i2)] = ah2;
+          a[size_t(j2)] = al2;
+          ++it;
+        }
+      }
     }
     // ---- moved columns (ascending position = ascending id), alpha written back
     cols.clear();

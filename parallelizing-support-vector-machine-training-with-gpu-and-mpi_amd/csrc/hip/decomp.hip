@@ -302,7 +302,12 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // Stops at W's own gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points
 // whose alpha changed are compacted in position order: cols[j] = their global ids, coef[j] =
 // (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
-template <int NT, int PER, bool PROF = false, bool W2 = false>
+//   DP (second order only): a second pair per iteration from the same selection -- i2 = the best
+//            I_high candidate of the waves other than i_high's, j2 = the first-order j (max f over
+//            I_low) -- whose rows load beside row i_high; after the first pair's update it is applied
+//            if it is still a violating pair (f_j2 > f_i2 + 2 tau_in) and feasible.  32 % fewer
+//            iterations of the chain at 60k for ~10 % more work per iteration.
+template <int NT, int PER, bool PROF = false, bool W2 = false, bool DP = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, DecompCtl* __restrict__ ctl,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
@@ -442,6 +447,33 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     int ih = int(uih), il = int(uil);
     double K12, bl_upd = bl, al;  // the second index's f in the update (first order: b_low)
     double kh[PER], kl[PER];
+    // DP: the second pair (i2, j2) and what its update needs, from the same selection
+    int i2 = -1;
+    double f2h = 0.0, a2h = 0.0, f2l = bl, a2l = 0.0;
+    double k2h[PER], k2l[PER];
+    double Kh_i2 = 0.0, Kh_j2 = 0.0, Kl_i2 = 0.0, Kl_j2 = 0.0, K2_12 = 0.0;
+    bool dp_ok = false;
+    if constexpr (DP) {
+      const int wih = fw[0][0];
+      double bv = inf;
+      uint32_t bi = kSentinel;
+      int bq = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const double v = pv[par][0][q];
+        const uint32_t ix = pi[par][0][q];
+        const bool take = (q != wih) & ((v < bv) | ((v == bv) & (ix < bi)));
+        bv = take ? v : bv;
+        bi = take ? ix : bi;
+        bq = take ? q : bq;
+      }
+      i2 = bi != kSentinel ? int(bi) : -1;
+      f2h = bv;
+      a2h = pa[par][0][bq];
+      a2l = pa[par][1][fw[1][0]];
+      dp_ok = i2 >= 0 && il != ih && i2 != il;  // here il is still the first-order j (= j2)
+    }
+    const int j2 = il;
     double2 rj[PER / 2];  // second order: row j's raw pieces, consumed only after the clip arithmetic
     if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
@@ -455,6 +487,15 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
       // and fold, then row j
       row(ih, kh);  // unconditional loads (no exec-mask branch per load)
+      if constexpr (DP) {
+        if (dp_ok) {  // wave-uniform
+          row(i2, k2h);
+          row(j2, k2l);
+          Kh_i2 = Kw[int64_t(ih) * ldw + i2];
+          Kh_j2 = Kw[int64_t(ih) * ldw + j2];
+          K2_12 = Kw[int64_t(i2) * ldw + j2];
+        }
+      }
       if constexpr (PROF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(8);
@@ -525,6 +566,13 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
 #pragma unroll
         for (int h = 0; h < PER / 2; ++h) rj[h] = src[NT * h];
       }
+      if constexpr (DP) {
+        dp_ok = dp_ok && il != j2 && il != i2;  // the second-order j must leave the second pair alone
+        if (dp_ok) {
+          Kl_i2 = Kw[int64_t(il) * ldw + i2];
+          Kl_j2 = Kw[int64_t(il) * ldw + j2];
+        }
+      }
       al = qa[par][cw[0]];
       bl_upd = qf[par][cw[0]];
       K12 = qk[par][cw[0]];
@@ -577,6 +625,39 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       a[e] = k == ih ? ah_new : k == il ? al_new : a[e];
     }
     ++it;
+    if constexpr (DP) {
+      if (dp_ok && it < max_inner) {
+        // the second pair's f after the first update, as its owner thread computed it just now
+        const double fi2 = f2h + (ch * Kh_i2 + cl * Kl_i2);
+        const double fj2 = f2l + (ch * Kh_j2 + cl * Kl_j2);
+        const int32_t yh2 = sy[i2], yl2 = sy[j2];
+        const int s2 = yh2 * yl2;
+        const double eta2 = K11 + K22 - 2.0 * K2_12;
+        double U2, V2;
+        if (s2 == -1) {
+          U2 = fmax(0.0, a2l - a2h);
+          V2 = fmin(C, C + a2l - a2h);
+        } else {
+          U2 = fmax(0.0, a2l + a2h - C);
+          V2 = fmin(C, a2l + a2h);
+        }
+        if (fj2 > fi2 + 2.0 * tau_in && U2 <= V2 + 1e-12 && !(eta2 <= eps)) {  // still violating, feasible
+          double al2 = a2l + double(yl2) * (fi2 - fj2) / eta2;
+          if (al2 > V2) al2 = V2;
+          if (al2 < U2) al2 = U2;
+          const double ah2 = a2h + double(s2) * (a2l - al2);
+          const double ch2 = (ah2 - a2h) * double(yh2);
+          const double cl2 = (al2 - a2l) * double(yl2);
+#pragma unroll
+          for (int e = 0; e < PER; ++e) {
+            const int k = pos(e);
+            ft[e] += ch2 * k2h[e] + cl2 * k2l[e];
+            a[e] = k == i2 ? ah2 : k == j2 ? al2 : a[e];
+          }
+          ++it;
+        }
+      }
+    }
     stamp(4);
   }
   // compaction in position order: pair h, then wave, then lane, then e & 1
@@ -965,6 +1046,11 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
   // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
   const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
+  // SVM355_DECOMP_WSS = 3: second order plus the second pair per iteration (DP); 2: one pair.  Default:
+  // DP below 200k points (60k: 20.8 -> 19.8 ms; 250k: 84.9 -> 86.1 ms, 1M: 299 -> 299 ms, where the
+  // outer iterations do not fall and the extra pair updates cost what the shorter chain saves)
+  const char* wss_env = getenv("SVM355_DECOMP_WSS");
+  const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) == 3 : n < 200000);
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1166,9 +1252,15 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   if (tr) batch = 1;  // the trace reads every outer iteration back
   int32_t* gate = &ctl->stop;
   const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
-#define SVM_WS_INNER_(NT, PER, PR, S2)                                                                           \
-  hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha, Wf,   \
-                     p.C, p.eps, cols, coef, mcount, hs, pub)
+#define SVM_WS_INNER_(NT, PER, PR, S2)                                                                            \
+  do {                                                                                                             \
+    if (inner_dp && S2)                                                                                            \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,      \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha,   \
+                         Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                             \
+  } while (0)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
     SVM_WS_INNER_(NT, PER, true, true);      \

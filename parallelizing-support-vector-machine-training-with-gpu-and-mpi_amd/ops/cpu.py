@@ -62,7 +62,7 @@ def smo_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optio
 
 
 def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[np.ndarray] = None,
-                      q: int = 1024, tau_frac: float = 0.1, inner_wss: int = 2, trace_cap: int = 0,
+                      q: int = 1024, tau_frac: float = 0.1, inner_wss: int = 3, trace_cap: int = 0,
                       snapshots: bool = False):
     """CPU oracle of the device decomposition solver (csrc/core/decomp_cpu.cpp) on a kernel matrix K.
     alpha given = warm start.  Returns (alpha, SMOResult, stats dict, N.DecompTrace or None)."""

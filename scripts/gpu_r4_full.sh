@@ -16,3 +16,5 @@ import json
 a = json.load(open("gpurun_out/r4full_bench1.json"))
 print("1 GPU", a["value"], a["iterations"], a["b"], a["n_sv"], a["accuracy"], a.get("f64_input_fit_ms"), a["pairwise_solver"]["fit_ms"])
 PY
+SOLVERS=auto bash scripts/gpu_r4_cascade_crit.sh > gpurun_out/r4crit3.txt 2>&1 || { tail -5 gpurun_out/r4crit3.txt; exit 1; }
+grep -v "per round" gpurun_out/r4crit3.txt
