@@ -366,6 +366,13 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       out[2 * h + 1] = pos(2 * h + 1) < m ? v.y : 0.0;
     }
   };
+  // a wave-uniform element of K(W, W) through a VECTOR load (in order with the row loads on vmcnt): a
+  // scalar load would share lgkmcnt with the folds' LDS reads, which would then wait for it
+  auto kval = [&](int r, int c) {
+    int64_t off = int64_t(r) * ldw + c;
+    asm volatile("" : "+v"(off));
+    return Kw[off];
+  };
   auto stamp = [&](int k) {
     if constexpr (PROF) {
       const int64_t now = int64_t(clock64());
@@ -450,7 +457,7 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     // DP: the second pair (i2, j2) and what its update needs, from the same selection
     int i2 = -1;
     double f2h = 0.0, a2h = 0.0, f2l = bl, a2l = 0.0;
-    double k2h[PER], k2l[PER];
+    double2 r2h[PER / 2], r2l[PER / 2];  // DP: rows i2 and j2, raw, consumed by the second pair only
     double Kh_i2 = 0.0, Kh_j2 = 0.0, Kl_i2 = 0.0, Kl_j2 = 0.0, K2_12 = 0.0;
     bool dp_ok = false;
     if constexpr (DP) {
@@ -488,12 +495,18 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       // and fold, then row j
       row(ih, kh);  // unconditional loads (no exec-mask branch per load)
       if constexpr (DP) {
-        if (dp_ok) {  // wave-uniform
-          row(i2, k2h);
-          row(j2, k2l);
-          Kh_i2 = Kw[int64_t(ih) * ldw + i2];
-          Kh_j2 = Kw[int64_t(ih) * ldw + j2];
-          K2_12 = Kw[int64_t(i2) * ldw + j2];
+        {  // issued after row i (unconditionally -- row i again when there is no second pair: no branch
+           // around loads, whose merge made the compiler wait for all of them before the gains)
+          const int ri = dp_ok ? i2 : ih, rj2 = dp_ok ? j2 : ih;
+          const double2* s2h = reinterpret_cast<const double2*>(Kw + int64_t(ri) * ldw + pbase);
+          const double2* s2l = reinterpret_cast<const double2*>(Kw + int64_t(rj2) * ldw + pbase);
+#pragma unroll
+          for (int h = 0; h < PER / 2; ++h) r2h[h] = s2h[NT * h];
+#pragma unroll
+          for (int h = 0; h < PER / 2; ++h) r2l[h] = s2l[NT * h];
+          Kh_i2 = kval(ih, ri);
+          Kh_j2 = kval(ih, rj2);
+          K2_12 = kval(ri, rj2);
         }
       }
       if constexpr (PROF) {
@@ -568,10 +581,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       }
       if constexpr (DP) {
         dp_ok = dp_ok && il != j2 && il != i2;  // the second-order j must leave the second pair alone
-        if (dp_ok) {
-          Kl_i2 = Kw[int64_t(il) * ldw + i2];
-          Kl_j2 = Kw[int64_t(il) * ldw + j2];
-        }
+        Kl_i2 = kval(il, dp_ok ? i2 : il);
+        Kl_j2 = kval(il, dp_ok ? j2 : il);
       }
       al = qa[par][cw[0]];
       bl_upd = qf[par][cw[0]];
@@ -648,6 +659,16 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
           const double ah2 = a2h + double(s2) * (a2l - al2);
           const double ch2 = (ah2 - a2h) * double(yh2);
           const double cl2 = (al2 - a2l) * double(yl2);
+          double k2h[PER], k2l[PER];
+#pragma unroll
+          for (int h = 0; h < PER / 2; ++h) {
+            double x = r2h[h].x, z = r2h[h].y, u = r2l[h].x, v = r2l[h].y;
+            asm volatile("" : "+v"(x), "+v"(z), "+v"(u), "+v"(v) : "v"(cl2));  // consumed here, not at the load
+            k2h[2 * h] = pos(2 * h) < m ? x : 0.0;
+            k2h[2 * h + 1] = pos(2 * h + 1) < m ? z : 0.0;
+            k2l[2 * h] = pos(2 * h) < m ? u : 0.0;
+            k2l[2 * h + 1] = pos(2 * h + 1) < m ? v : 0.0;
+          }
 #pragma unroll
           for (int e = 0; e < PER; ++e) {
             const int k = pos(e);
@@ -1046,11 +1067,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // inner pair selection: second order for j (default; fewer, longer iterations: 8,206 vs 14,334 at
   // 60k, 12% faster) or first order (SVM355_DECOMP_WSS=1)
   const bool inner_wss2 = !(getenv("SVM355_DECOMP_WSS") && atoi(getenv("SVM355_DECOMP_WSS")) == 1);
-  // SVM355_DECOMP_WSS = 3: second order plus the second pair per iteration (DP); 2: one pair.  Default:
-  // DP below 200k points (60k: 20.8 -> 19.8 ms; 250k: 84.9 -> 86.1 ms, 1M: 299 -> 299 ms, where the
-  // outer iterations do not fall and the extra pair updates cost what the shorter chain saves)
+  // SVM355_DECOMP_WSS = 3 (the default): second order plus the second pair per iteration (DP); 2: one
+  // pair (40k 17.0 -> 15.5 ms, 60k 20.8 -> 19.2, 120k 43.9 -> 42.7, 250k 84.9 -> 83.1, 1M 296 -> 289)
   const char* wss_env = getenv("SVM355_DECOMP_WSS");
-  const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) == 3 : n < 200000);
+  const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) == 3 : true);
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
