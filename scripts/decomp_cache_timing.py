@@ -2,7 +2,8 @@
 """Decomposition fit time with the column cache off / on (SVM355_DECOMP_CCACHE, read per fit) at the
 sizes of argv: best of 3 fits after a warm-up, the alpha of both compared bit for bit
 (SVM355_DECOMP_CCACHE_FIXED=0|1: that setting only, for a profile; SVM355_TIMING_VAR: the variable
-toggled instead of SVM355_DECOMP_CCACHE, e.g. SVM355_DECOMP_WCOLS).
+toggled instead of SVM355_DECOMP_CCACHE, e.g. SVM355_DECOMP_WCOLS; SVM355_TIMING_VALUES: its values,
+comma-separated, instead of 0 and 1).
 
     python scripts/decomp_cache_timing.py 60000 250000 1000000
 """
@@ -27,6 +28,8 @@ for n in [int(a) for a in sys.argv[1:]]:
     yd = torch.from_numpy(tr.y).to(dev)
     res = {}
     flags = (os.environ["SVM355_DECOMP_CCACHE_FIXED"],) if "SVM355_DECOMP_CCACHE_FIXED" in os.environ else ("0", "1")
+    if "SVM355_TIMING_VALUES" in os.environ:
+        flags = tuple(os.environ["SVM355_TIMING_VALUES"].split(","))
     for flag in flags:
         os.environ[os.environ.get("SVM355_TIMING_VAR", "SVM355_DECOMP_CCACHE")] = flag
         best = 1e30
@@ -42,7 +45,7 @@ for n in [int(a) for a in sys.argv[1:]]:
         res[flag] = (alpha.cpu().numpy(), r.b, r.iterations, tm["outer_iterations"], best)
         print(f"n={n} cache={flag}: fit {best * 1e3:.1f} ms outer {tm['outer_iterations']} pair updates "
               f"{r.iterations} b {r.b:.12f} stop {r.stop_reason}", flush=True)
-    if len(res) < 2:
+    if set(res) != {"0", "1"}:
         continue
     same = np.array_equal(res["0"][0], res["1"][0]) and res["0"][1:4] == res["1"][1:4]
     print(f"n={n}: speedup {res['0'][4] / res['1'][4]:.2f}x, alpha bit-identical {same}", flush=True)

@@ -21,8 +21,16 @@ first_j = []  # per pair update: the second-order j is the first-order (maximal 
 _inner = S.inner
 
 
+ranks = []  # per outer iteration: W positions by violation at the start of the inner solve
+
+
 def inner(Kw, y, a, f, tau_in, max_inner):
     rec = []
+    hi0, lo0 = S.sets(a, y)
+    bh0 = np.min(np.where(hi0, f, np.inf))
+    bl0 = np.max(np.where(lo0, f, -np.inf))
+    score = np.maximum(np.where(hi0, bl0 - f, -np.inf), np.where(lo0, f - bh0, -np.inf))
+    ranks.append(np.argsort(-score, kind="stable"))
     a = a.copy()
     f = f.copy()
     it = 0
@@ -69,7 +77,7 @@ X = MinMaxScaler().fit_transform(tr.X)
 outer, crit, total, sv, b, _ = S.run(X, tr.y, 1, 1024, "rank", "qp", False)
 print(f"n={n}: outer {outer} pair updates {total} b {b:.7f}; second-order j = first-order j in "
       f"{np.mean(first_j):.3f} of the pair updates")
-for R in (4, 8, 12, 16, 18, 24, 32):
+for R in tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (4, 8, 12, 16, 18, 24, 32):
     hits = acc = hi_i = hi_j = 0
     for rec in pairs:  # the cache starts empty per outer iteration (a new K(W, W))
         lru = OrderedDict()
@@ -87,3 +95,16 @@ for R in (4, 8, 12, 16, 18, 24, 32):
                         lru.popitem(last=False)
     print(f"R={R:3d} rows: hit rate {hits / acc:.3f} (row i {2 * hi_i / acc:.3f}, row j {2 * hi_j / acc:.3f})",
           flush=True)
+
+# L2 warming design input: the rows an inner solve touches at all, and how many of them are among the
+# P most violating W positions at its start (rows a kernel could load into the inner CU's L2 before it)
+used = [len({r for p in rec for r in p}) for rec in pairs]
+print(f"distinct rows per inner solve: mean {np.mean(used):.0f}, max {max(used)}; row loads per inner solve "
+      f"{np.mean([2 * len(rec) for rec in pairs]):.0f}")
+for P in (128, 192, 256, 320, 384, 512):
+    cov = tot = 0
+    for rec, rk in zip(pairs, ranks):
+        u = {r for p in rec for r in p}
+        cov += len(u & set(rk[:P].tolist()))
+        tot += len(u)
+    print(f"P={P:3d} most violating rows warmed: {cov / tot:.3f} of the first touches covered", flush=True)
