@@ -255,10 +255,11 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
       }
       // inner_wss 3: the second pair from the same selection (ws_inner_kernel DP): i2 = the best I_high
       // point outside i_high's wave of the 256-thread inner workgroup (position k lies in wave
-      // (k mod 512) / 128), j2 = the first-order j
+      // (k mod 512) / 128), j2 = the first-order j.  inner_wss 4 (ws_inner_kernel J2S): j2 by the
+      // second-order gain of row i2 over I_low points above f(i2), from the same snapshot
       int i2 = -1;
-      const int j2 = il;
-      if (inner_wss == 3) {
+      int j2 = il;
+      if (inner_wss >= 3) {
         const int wih = (ih % (2 * kInnerNT)) / 128;
         double v2 = inf;
         for (int k = 0; k < m; ++k)
@@ -266,6 +267,25 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
             v2 = ft[size_t(k)];
             i2 = k;
           }
+      }
+      if (inner_wss == 4) {
+        j2 = -1;
+        if (i2 >= 0) {
+          const double* K2 = K + int64_t(W[size_t(i2)]) * ldk;
+          const double h2 = ft[size_t(i2)];
+          double gv2 = inf;
+          for (int k = 0; k < m; ++k) {
+            if (!in_low(yw[size_t(k)], a[size_t(k)]) || !(ft[size_t(k)] > h2)) continue;
+            const double bb = ft[size_t(k)] - h2;
+            double at = 2.0 - 2.0 * K2[W[size_t(k)]];
+            at = at <= 0.0 ? eps : at;
+            const double gain = -(bb * bb) / at;
+            if (gain < gv2) {
+              gv2 = gain;
+              j2 = k;
+            }
+          }
+        }
       }
       const double* Ki = K + int64_t(W[size_t(ih)]) * ldk;
       for (int k = 0; k < m; ++k) kh[size_t(k)] = Ki[W[size_t(k)]];
@@ -324,7 +344,7 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
       a[size_t(ih)] = ah_new;
       a[size_t(il)] = al_new;
       ++it;
-      if (i2 >= 0 && j2 != ih && i2 != j2 && il != j2 && il != i2 && it < max_inner) {
+      if (i2 >= 0 && j2 >= 0 && j2 != ih && i2 != j2 && il != j2 && il != i2 && it < max_inner) {
         const double fi2 = ft[size_t(i2)], fj2 = ft[size_t(j2)];  // after the first update
         const double a2h = a[size_t(i2)], a2l = a[size_t(j2)];
         const int32_t yh2 = yw[size_t(i2)], yl2 = yw[size_t(j2)];

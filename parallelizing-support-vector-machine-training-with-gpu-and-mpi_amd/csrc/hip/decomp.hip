@@ -307,7 +307,9 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 //            I_low) -- whose rows load beside row i_high; after the first pair's update it is applied
 //            if it is still a violating pair (f_j2 > f_i2 + 2 tau_in) and feasible.  32 % fewer
 //            iterations of the chain at 60k for ~10 % more work per iteration.
-template <int NT, int PER, bool PROF = false, bool W2 = false, bool DP = false>
+//   J2S (with DP): j2 by the second-order gain of row i2 instead of the first-order j (row i2 loads
+//            beside row i before the gains; both gains reduce in the same wave / barrier / fold).
+template <int NT, int PER, bool PROF = false, bool W2 = false, bool DP = false, bool J2S = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, DecompCtl* __restrict__ ctl,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
@@ -325,6 +327,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   __shared__ uint32_t pi[2][2][NW];
   __shared__ double qv[2][NW], qa[2][NW], qf[2][NW], qk[2][NW];  // W2: the second index's candidates
   __shared__ uint32_t qi[2][NW];
+  __shared__ double rv[2][NW], ra[2][NW], rf[2][NW], rk[2][NW];  // J2S: the second pair's j candidates
+  __shared__ uint32_t ri2[2][NW];
   __shared__ int8_t sy[NT * PER];
   __shared__ int32_t wcnt[PER][NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -478,9 +482,9 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       f2h = bv;
       a2h = pa[par][0][bq];
       a2l = pa[par][1][fw[1][0]];
-      dp_ok = i2 >= 0 && il != ih && i2 != il;  // here il is still the first-order j (= j2)
+      dp_ok = J2S ? i2 >= 0 : i2 >= 0 && il != ih && i2 != il;  // (not J2S) il is still the first-order j = j2
     }
-    const int j2 = il;
+    int j2 = il;
     double2 rj[PER / 2];  // second order: row j's raw pieces, consumed only after the clip arithmetic
     if constexpr (!W2) {
       // one memory round trip: K12 and this thread's entries of the two rows; the labels from LDS
@@ -494,7 +498,13 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       // floored at eps; reciprocal approximation: only the choice depends on it), a second barrier
       // and fold, then row j
       row(ih, kh);  // unconditional loads (no exec-mask branch per load)
-      if constexpr (DP) {
+      if constexpr (J2S) {  // row i2 now (its gains need it); row j2 and the K values after the fold
+        const int ri = dp_ok ? i2 : ih;
+        const double2* s2h = reinterpret_cast<const double2*>(Kw + int64_t(ri) * ldw + pbase);
+#pragma unroll
+        for (int h = 0; h < PER / 2; ++h) r2h[h] = s2h[NT * h];
+        Kh_i2 = kval(ih, ri);
+      } else if constexpr (DP) {
         {  // issued after row i (unconditionally -- row i again when there is no second pair: no branch
            // around loads, whose merge made the compiler wait for all of them before the gains)
           const int ri = dp_ok ? i2 : ih, rj2 = dp_ok ? j2 : ih;
@@ -530,7 +540,26 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         ge = c ? e : ge;
       }
       const uint32_t gi = gv < inf ? uint32_t(pos(ge)) : kSentinel;
+      double gv2 = inf;
+      int ge2 = 0;
+      if constexpr (J2S) {  // the same gain over I_low points above f(i2), on row i2 (f2h = inf: none)
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          const bool below = a[e] < c_hi, above = a[e] > c_lo;
+          const bool in_low = (yp[e] && above) || (yn[e] && below);
+          const double bb = ft[e] - f2h;
+          const double k2 = pos(e) < m ? ((e & 1) ? r2h[e >> 1].y : r2h[e >> 1].x) : 0.0;
+          double at = 2.0 - 2.0 * k2;
+          at = at <= 0.0 ? eps : at;
+          const double gain = -(bb * bb) / at;
+          const bool c = in_low && ft[e] > f2h && gain < gv2;
+          gv2 = c ? gain : gv2;
+          ge2 = c ? e : ge2;
+        }
+      }
+      const uint32_t gi2 = gv2 < inf ? uint32_t(pos(ge2)) : kSentinel;
       const int lc = wave_arg_lane<true>(VI{gv, gi});
+      const int lc2 = J2S ? wave_arg_lane<true>(VI{gv2, gi2}) : -1;
       stamp(9);
       if (lane == lc) {
         double ga = a[0], gf = ft[0], gk = kh[0];
@@ -545,6 +574,20 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
         qa[par][w] = ga;
         qf[par][w] = gf;
         qk[par][w] = gk;
+      }
+      if (J2S && lane == lc2) {
+        double ga = a[0], gf = ft[0], gk = r2h[0].x;
+#pragma unroll
+        for (int e = 1; e < PER; ++e) {
+          ga = ge2 == e ? a[e] : ga;
+          gf = ge2 == e ? ft[e] : gf;
+          gk = ge2 == e ? ((e & 1) ? r2h[e >> 1].y : r2h[e >> 1].x) : gk;
+        }
+        rv[par][w] = gv2;
+        ri2[par][w] = gi2;
+        ra[par][w] = ga;
+        rf[par][w] = gf;
+        rk[par][w] = gk;
       }
       __syncthreads();
       stamp(10);
@@ -579,7 +622,39 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
 #pragma unroll
         for (int h = 0; h < PER / 2; ++h) rj[h] = src[NT * h];
       }
-      if constexpr (DP) {
+      if constexpr (J2S) {  // the second pair's j: the same fold over the second gains
+        double dv[NW];
+        uint32_t dj[NW];
+        int dw[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          dv[q] = rv[par][q];
+          dj[q] = ri2[par][q];
+          dw[q] = q;
+        }
+#pragma unroll
+        for (int st = 1; st < NW; st <<= 1)
+#pragma unroll
+          for (int q = 0; q + st < NW; q += 2 * st) {
+            const bool tk = (dv[q + st] < dv[q]) | ((dv[q + st] == dv[q]) & (dj[q + st] < dj[q]));
+            dv[q] = tk ? dv[q + st] : dv[q];
+            dj[q] = tk ? dj[q + st] : dj[q];
+            dw[q] = tk ? dw[q + st] : dw[q];
+          }
+        const bool jok = dj[0] != kSentinel;
+        j2 = jok ? int(dj[0]) : ih;
+        dp_ok = dp_ok && jok && j2 != ih && il != j2 && il != i2;
+        f2l = rf[par][dw[0]];
+        a2l = ra[par][dw[0]];
+        K2_12 = rk[par][dw[0]];
+        const int rj2 = dp_ok ? j2 : ih;
+        const double2* s2l = reinterpret_cast<const double2*>(Kw + int64_t(rj2) * ldw + pbase);
+#pragma unroll
+        for (int h = 0; h < PER / 2; ++h) r2l[h] = s2l[NT * h];
+        Kh_j2 = kval(ih, rj2);
+        Kl_i2 = kval(il, dp_ok ? i2 : il);
+        Kl_j2 = kval(il, rj2);
+      } else if constexpr (DP) {
         dp_ok = dp_ok && il != j2 && il != i2;  // the second-order j must leave the second pair alone
         Kl_i2 = kval(il, dp_ok ? i2 : il);
         Kl_j2 = kval(il, dp_ok ? j2 : il);
@@ -1070,7 +1145,9 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // SVM355_DECOMP_WSS = 3 (the default): second order plus the second pair per iteration (DP); 2: one
   // pair (40k 17.0 -> 15.5 ms, 60k 20.8 -> 19.2, 120k 43.9 -> 42.7, 250k 84.9 -> 83.1, 1M 296 -> 289)
   const char* wss_env = getenv("SVM355_DECOMP_WSS");
-  const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) == 3 : true);
+  const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) >= 3 : true);
+  // SVM355_DECOMP_WSS = 4: the second pair's j by the second-order gain of row i2 (opt-in)
+  const bool inner_j2s = inner_dp && wss_env && atoi(wss_env) == 4;
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1274,7 +1351,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                            \
   do {                                                                                                             \
-    if (inner_dp && S2)                                                                                            \
+    if (inner_j2s && S2)                                                                                           \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,  \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
+    else if (inner_dp && S2)                                                                                       \
       hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,      \
                          alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
     else                                                                                                           \

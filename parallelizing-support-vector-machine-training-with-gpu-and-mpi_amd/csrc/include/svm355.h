@@ -131,7 +131,8 @@ typedef struct svm_decomp_trace {
 // block selection, working-set build and stop test, the inner solve's arithmetic and tie rules, and
 // the f update in the device GEMV's summation order.  q: working-set size (<= 1024); tau_frac: inner
 // stop fraction (device default 0.1); inner_wss: 3 = second-order second index plus a second pair per
-// iteration (device default), 2 = second order alone, 1 = first order.  warm = 1: alpha holds the start and f = K (alpha y) - y over its nonzero entries in
+// iteration (device default), 4 = the same with the second pair's j by the second-order gain of
+// row i2 (SVM355_DECOMP_WSS=4), 2 = second order alone, 1 = first order.  warm = 1: alpha holds the start and f = K (alpha y) - y over its nonzero entries in
 // chunks of 1024 columns (the device's warm start).  stats (8 int64, may be NULL) as the device's:
 // outer, inner iterations, working-set capacity, microseconds, moved columns, 0, 0, warm-start columns.
 SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha,

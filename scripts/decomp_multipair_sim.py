@@ -20,6 +20,7 @@ import decomp_teams_sim as S  # noqa: E402
 from svm355.utils.data import MinMaxScaler, synthetic_mnist  # noqa: E402
 
 NPAIR = 1
+J2_SECOND = False  # SIM_J2=second: the second pair's j by i2's second-order gain (not the first-order j)
 stats = {"chain": 0, "pairs": 0}
 
 
@@ -77,6 +78,11 @@ def inner(Kw, y, a, f, tau_in, max_inner):
         j_first = int(np.argmax(fl))
         # candidates of the later pairs come from the same selection (before any update)
         i2 = wave_best(f, hi, waves, {waves[ih]}, True) if NPAIR >= 2 else -1
+        if J2_SECOND and i2 >= 0:  # j2 by the second-order gain of i2's row (same snapshot of f)
+            at2 = 2.0 - 2.0 * Kw[i2]
+            at2 = np.where(at2 <= 0, S.EPS, at2)
+            g2 = np.where(lo & (f > f[i2]), -((f - f[i2]) ** 2) / at2, np.inf)
+            j_first = int(np.argmin(g2)) if np.isfinite(g2).any() else j_first
         i3 = wave_best(f, hi, waves, {waves[ih]} | ({waves[i2]} if i2 >= 0 else set()), True) if NPAIR >= 3 else -1
         j3 = wave_best(f, lo, waves, {waves[j_first]}, False) if NPAIR >= 3 else -1
         r = pair_update(Kw, y, a, f, ih, il, tau_in, False)
@@ -97,6 +103,7 @@ def inner(Kw, y, a, f, tau_in, max_inner):
 
 
 S.inner = inner
+J2_SECOND = __import__("os").environ.get("SIM_J2") == "second"
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 60000
 tr = synthetic_mnist(n, seed=2024)
 X = MinMaxScaler().fit_transform(tr.X)

@@ -33,7 +33,7 @@ def prob2k():
     return _problem(2000, 11)
 
 
-@pytest.mark.parametrize("q,inner_wss", [(1024, 3), (1024, 2), (256, 3), (1024, 1)])
+@pytest.mark.parametrize("q,inner_wss", [(1024, 3), (1024, 4), (1024, 2), (256, 3), (1024, 1)])
 def test_oracle_meets_the_stop_test_with_the_pairwise_svs(prob2k, q, inner_wss):
     K, y = prob2k
     p = SVMParams(n_threads=4)

@@ -86,8 +86,11 @@ def _compare(dt, ot):
         np.testing.assert_array_equal(a["f"], b["f"], err_msg=f"outer {o}: f")
 
 
-@pytest.mark.parametrize("n,q", [(2000, 1024), (2000, 64), (6000, 512), (6000, 1024)])
-def test_device_trajectory_equals_the_cpu_oracle(n, q):
+@pytest.mark.parametrize("n,q,wss", [(2000, 1024, 3), (2000, 64, 3), (6000, 512, 3), (6000, 1024, 3),
+                                     (2000, 1024, 4), (6000, 1024, 4)])
+def test_device_trajectory_equals_the_cpu_oracle(n, q, wss, monkeypatch):
+    # wss 4: the second pair's j by the second-order gain of row i2 (SVM355_DECOMP_WSS=4, oracle inner_wss 4)
+    monkeypatch.setenv("SVM355_DECOMP_WSS", str(wss))
     tr = synthetic_mnist(n, seed=41 + q).compact()
     Xu, mn, mx = _dev_rows(tr)
     K = _exact_gram_host(Xu, mn, mx, n)
@@ -96,7 +99,8 @@ def test_device_trajectory_equals_the_cpu_oracle(n, q):
     alpha = torch.empty(n, dtype=torch.float64, device=DEV)
     dt = N.DecompTrace(400, n)
     res, tm = D.train_decomp(Xu, yd, alpha, p, mn, mx, working_set=q, trace=dt)
-    a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), q=q, trace_cap=400, snapshots=True)
+    a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), q=q, inner_wss=wss, trace_cap=400,
+                                             snapshots=True)
     _compare(dt, ot)
     assert res.stop_reason == r_o.stop_reason == "converged"
     assert res.iterations == r_o.iterations and res.b == r_o.b
