@@ -87,9 +87,12 @@ def main(argv=None):
                          "smo or the cascade, whichever fit is measured faster (auto), or the opt-in distributed "
                          "working-set decomposition solver (decomp; compared with the one-GPU decomposition solver)")
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
-    ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
+    ap.add_argument("--transport", choices=["auto", "rccl", "loopback", "hostcomm"], default="auto",
                     help="direct launch, N > 1: one GPU per rank (auto / rccl), or loopback = a rehearsal of N ranks "
-                         "on the visible GPU (cascade: host-staged exchanges; smo: N teams in one launch)")
+                         "on the visible GPU (cascade: host-staged exchanges; smo: N teams in one launch); under "
+                         "torchrun: RCCL (auto / rccl) or hostcomm = the same per-process ranks exchanging over the "
+                         "gloo group with host-staged device buffers, so N processes may share one GPU (the "
+                         "per-process N-GPU path rehearsed on one device; decomp and cascade)")
     ap.add_argument("--input", choices=["u8", "f64"], default="u8",
                     help="host row format: uint8 pixels (default) or FP64 as in the reference")
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
@@ -132,27 +135,34 @@ def main(argv=None):
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
     cpu = a.device == "cpu"
+    hostcomm = a.transport == "hostcomm"
+    if hostcomm and not multiproc:
+        print("bench.py: --transport hostcomm is a per-process transport (launch under torchrun)", file=sys.stderr)
+        return 2
     cascade_solver = a.solver or "auto"  # the cascade's solves: per solve on GPUs unless --solver is given
+    # the CPU oracle runs the pairwise SMO, except --parallel decomp: the decomposition's CPU twin
+    cpu_smo = cpu and a.parallel != "decomp"
     if a.solver is None:  # the decomposition on GPUs (every cascade solve too); the pairwise SMO on the CPU oracle
-        a.solver = "smo" if (cpu or a.parallel == "smo") else "decomp"
-    if a.solver == "decomp" and (cpu or a.parallel == "smo"):
-        print("bench.py: --solver decomp runs on GPUs; the CPU oracle and the distributed pairwise SMO "
-              "(--parallel smo) are --solver smo", file=sys.stderr)
+        a.solver = "smo" if (cpu_smo or a.parallel == "smo") else "decomp"
+    if a.solver == "decomp" and (cpu_smo or a.parallel == "smo"):
+        print("bench.py: --solver decomp runs on GPUs (on the CPU only as --parallel decomp); the CPU oracle and the "
+              "distributed pairwise SMO (--parallel smo) are --solver smo", file=sys.stderr)
         return 2
     ndev = torch.cuda.device_count() if not cpu else 1 << 30  # does not initialise the GPU on this image
     if not multiproc and a.gpus > 1 and a.transport != "loopback" and ndev < a.gpus:
         print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, {ndev} visible "
               "(use --transport loopback for a one-GPU rehearsal)", file=sys.stderr)
         return 2
-    if multiproc and ndev <= local_rank:
-        print(f"bench.py: LOCAL_RANK {local_rank} but {ndev} visible GPUs", file=sys.stderr)
+    if multiproc and ndev <= local_rank and not hostcomm:
+        print(f"bench.py: LOCAL_RANK {local_rank} but {ndev} visible GPUs (--transport hostcomm lets processes share "
+              "a GPU)", file=sys.stderr)
         return 2
 
     from svm355 import SVC, SVMParams
     from svm355.parallel.cascade import CascadeSVM, critical_path, partition_bounds
     from svm355.utils.data import synthetic_mnist
 
-    dev_index = local_rank if multiproc else 0
+    dev_index = (local_rank % max(1, ndev) if hostcomm else local_rank) if multiproc else 0
     if not cpu:
         torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index) if not cpu else torch.device("cpu")
@@ -196,8 +206,11 @@ def main(argv=None):
         if mode == "cascade":
             fallback_reason = ("not pixel rows" if not pixel else "cpu device" if cpu else "second-order selection"
                                if a.wss != "first" else "cascade requested" if a.cascade else "more than 8 GPUs")
-    elif mode in ("smo", "decomp") and (cpu or not pixel):
+    elif mode == "smo" and (cpu or not pixel) or mode == "decomp" and not cpu and not pixel:
         print(f"bench.py: --parallel {mode} needs uint8 pixel rows on GPUs", file=sys.stderr)
+        return 2
+    if hostcomm and mode not in ("decomp", "cascade"):
+        print("bench.py: --transport hostcomm runs the per-process decomposition and cascade ranks", file=sys.stderr)
         return 2
 
     def agree(ok: bool) -> bool:
@@ -245,13 +258,27 @@ def main(argv=None):
                     h.close()
             dgroup = drank = None
 
+    def proc_rank():
+        """This process's rank: gloo on the CPU oracle, host-staged gloo on the GPU, or RCCL."""
+        if cpu:
+            from svm355.parallel.hostcomm import HostCommRank
+
+            return HostCommRank(comm_timeout_s=a.comm_timeout)
+        if hostcomm:
+            from svm355.parallel.hostcomm import HostCommDeviceRank
+
+            return HostCommDeviceRank(dev_index, comm_timeout_s=a.comm_timeout)
+        from svm355.parallel.rccl import RcclRank
+
+        return RcclRank.from_torch_dist(dev_index, a.comm_timeout)
+
     if mode == "decomp":
         from svm355.parallel.decomp import DistributedDecompSVC
 
         if multiproc:
-            from svm355.parallel.rccl import RcclRank
-
-            crank = RcclRank.from_torch_dist(dev_index, a.comm_timeout)
+            crank = proc_rank()
+        elif cpu:
+            pass  # thread ranks on the CPU oracle (DistributedDecompSVC(transport="cpu"))
         else:
             from svm355.parallel.rccl import DeviceGroup
 
@@ -259,14 +286,8 @@ def main(argv=None):
 
     # auto with both applicable: the cascade is set up too and the faster measured fit runs (below)
     if mode == "cascade" or (auto and mode == "smo"):
-        if multiproc and cpu:
-            from svm355.parallel.hostcomm import HostCommRank
-
-            crank = HostCommRank(comm_timeout_s=a.comm_timeout)
-        elif multiproc:
-            from svm355.parallel.rccl import RcclRank
-
-            crank = RcclRank.from_torch_dist(dev_index, a.comm_timeout)
+        if multiproc:
+            crank = proc_rank()
         elif not cpu:
             from svm355.parallel.rccl import DeviceGroup
 
@@ -289,7 +310,8 @@ def main(argv=None):
         elif mode == "smo":
             model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
         elif mode == "decomp":
-            model = DistributedDecompSVC(a.gpus, group=group, rank=crank).fit(full.X, full.y)
+            model = DistributedDecompSVC(a.gpus, group=group, rank=crank,
+                                         transport="cpu" if cpu else "auto").fit(full.X, full.y)
         else:
             model = cascade_fit(a.topology)
 
@@ -492,7 +514,11 @@ def main(argv=None):
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
                  "stop_reason": model.stop_reason_, "decomp_stats": model.stats_, "rank_ms": model.rank_ms_,
                  "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
-                 "launch_form": ("one rank per process" if multiproc else "thread ranks, one GPU each")
+                 "launch_form": ("one rank per process" + (" (CPU oracle over gloo)" if cpu else
+                                                           f" over gloo, host-staged ({a.gpus} processes on "
+                                                           f"{min(ndev, a.gpus)} GPU(s))" if hostcomm else " (RCCL)")
+                                 if multiproc else "thread ranks on the CPU oracle (loopback)" if cpu
+                                 else "thread ranks, one GPU each")
                  if a.transport != "loopback" else f"rehearsal: {a.gpus} ranks on one GPU",
                  "note": "working-set decomposition solver over all GPUs: every GPU holds all rows and an "
                          "alpha replica, owns 1/N of the selection blocks and of f, and all-gathers its candidate "
@@ -549,12 +575,18 @@ def main(argv=None):
             dist.barrier()
         if rank == 0:
             one_solver = a.solver if mode in ("decomp", "cascade") else "smo"
-            one = SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)  # warm
+
+            def one_fit():
+                if cpu and mode == "decomp":  # the one-rank CPU oracle of the decomposition
+                    return DistributedDecompSVC(1, transport="cpu").fit(full.X, full.y)
+                return SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)
+
+            one = one_fit()  # warm
             ts = []
             for _ in range(a.baseline_1gpu):
                 sync()
                 tb = time.perf_counter()
-                one = SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)
+                one = one_fit()
                 sync()
                 ts.append(time.perf_counter() - tb)
             t1 = float(np.median(ts))

@@ -205,6 +205,11 @@ _CORE_SIGS = {
     "svm_decomp_train_gram": (c_int32, [_P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32, c_double,
                                         c_int32, POINTER(SvmResult), POINTER(c_int64), POINTER(SvmDecompTrace)]),
     "svm_decomp_gemv_ref": (c_int32, [_P, c_int64, c_int64, _P, _P, c_int64, _P]),
+    "svm_decomp_rank_train_gram": (c_int32, [_P, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32,
+                                             c_double, c_int32, POINTER(SvmResult), POINTER(c_int64)]),
+    "svm_decomp_group_train_gram": (c_int32, [c_int32, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
+                                              c_int32, c_double, c_int32, POINTER(SvmResult), POINTER(c_int64),
+                                              c_double]),
     "svm_decision": (c_int32, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_double, c_double, _P,
                                c_int32]),
     "svm_sv_indices": (c_int64, [_P, c_int64, c_double, _P]),
@@ -287,6 +292,7 @@ _HIP_SIGS = {
     "svmd_nccl_unique_id_bytes": (c_int64, []),
     "svmd_nccl_unique_id": (c_int32, [_P, c_int64]),
     "svmd_cascade_rank_create": (c_void_p, [c_int32, _P, c_int32, c_int32, c_double]),
+    "svmd_cascade_rank_create_hostcomm": (c_void_p, [_P, c_int32, c_double]),
     "svmd_cascade_rank_fit": (POINTER(SvmCascadeOut), [c_void_p, _P, c_int32, _P, _P, c_int64, c_int64, c_int64,
                                                        POINTER(SvmCascadeCfg)]),
     "svmd_cascade_rank_barrier": (c_int32, [c_void_p]),

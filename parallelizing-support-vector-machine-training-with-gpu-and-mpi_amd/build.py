@@ -142,19 +142,44 @@ def build_apps(force=False, verbose=False):
 SANITIZE = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-O1", "-g"]
 
 
+TSANITIZE = ["-fsanitize=thread", "-fno-omit-frame-pointer", "-O1", "-g"]
+
+
+def host_clang() -> str:
+    """The ROCm LLVM's host clang++ (compiler-rt of LLVM 22): its TSan runtime intercepts
+    pthread_cond_clockwait, which libstdc++ 11's condition_variable uses and the system gcc 11's libtsan
+    does not -- under g++ every wait looks like it returned without the mutex (false 'double lock' and
+    data-race reports on everything a condition variable protects)."""
+    exe = ROCM / "lib" / "llvm" / "bin" / "clang++"
+    if not exe.exists():
+        raise RuntimeError(f"{exe} not found (the TSan build needs the ROCm LLVM host compiler)")
+    return str(exe)
+
+
+def _build_host_exe(out_dir: Path, app: str, san, force, verbose, cxx: str = "g++") -> Path:
+    out_dir.mkdir(exist_ok=True)
+    exe = out_dir / app
+    srcs = [*CORE_SRCS, CSRC / "apps" / f"{app}.cpp"]
+    if force or _stale(exe, [*srcs, *CORE_HDRS, CSRC / "apps" / "cli_common.h", Path(__file__)]):
+        flags = [f for f in CXXFLAGS if f != "-O3"] + san
+        tmp = out_dir / f".{app}.{os.getpid()}"  # link aside, then rename: a concurrent run of the
+        _run([cxx, *flags, *srcs, "-o", tmp], verbose)  # old file keeps its inode (no ETXTBSY)
+        os.replace(tmp, exe)
+    return exe
+
+
 def build_sanitized(force=False, verbose=False) -> Path:
     """Host-only ASan+UBSan build of the CPU core and the serial CLI: one static
     executable ``bin_asan/svm_serial`` (sanitizers on host code only; no GPU code involved)."""
-    out_dir = PKG / "bin_asan"
-    out_dir.mkdir(exist_ok=True)
-    exe = out_dir / "svm_serial"
-    srcs = [*CORE_SRCS, CSRC / "apps" / "svm_serial.cpp"]
-    if force or _stale(exe, [*srcs, *CORE_HDRS, CSRC / "apps" / "cli_common.h"]):
-        flags = [f for f in CXXFLAGS if f != "-O3"] + SANITIZE
-        tmp = out_dir / f".svm_serial.{os.getpid()}"  # link aside, then rename: a concurrent run of the
-        _run(["g++", *flags, *srcs, "-o", tmp], verbose)  # old file keeps its inode (no ETXTBSY)
-        os.replace(tmp, exe)
-    return exe
+    return _build_host_exe(PKG / "bin_asan", "svm_serial", SANITIZE, force, verbose)
+
+
+def build_sanitized_threads(force=False, verbose=False):
+    """The threaded host code (strict loopback and hostcomm cascades, abort, resume, the decomposition
+    oracle's worker team and its distributed thread ranks: apps/svm_threads.cpp) built twice: ASan +
+    UBSan (``bin_asan/svm_threads``) and TSan (``bin_tsan/svm_threads``).  Returns both paths."""
+    return (_build_host_exe(PKG / "bin_asan", "svm_threads", SANITIZE, force, verbose),
+            _build_host_exe(PKG / "bin_tsan", "svm_threads", TSANITIZE, force, verbose, cxx=host_clang()))
 
 
 def build_all(force=False, verbose=False, hip=True):
@@ -176,6 +201,8 @@ def main(argv=None):
         print(p)
     if a.sanitize:
         print(build_sanitized(a.force, a.verbose))
+        for p in build_sanitized_threads(a.force, a.verbose):
+            print(p)
 
 
 if __name__ == "__main__":

@@ -22,6 +22,7 @@
 #include <limits>
 #include <vector>
 
+#include "../cascade/cascade_capi.h"
 #include "internal.h"
 
 using namespace svm355;
@@ -38,23 +39,28 @@ struct Shape {
   int64_t NB = 0, per = 0, L = 0;
 };
 
-// decomp_shape (decomp.hip) at world = 1
-Shape shape(int64_t n, int qws) {
+// decomp_shape (decomp.hip): blocks a multiple of 8 (of 8 * world when world does not divide 8), so
+// 1, 2, 4 or 8 ranks own whole blocks of the one-rank partition
+Shape shape(int64_t n, int qws, int world) {
   Shape d;
   d.q = std::max(4, std::min(qws, kMaxWS));
   const int64_t nb0 = std::max<int64_t>((n + kSelPts - 1) / kSelPts, std::min<int64_t>(64, (n + 63) / 64));
-  d.NB = (nb0 + 7) / 8 * 8;
+  const int64_t mult = (8 % world == 0) ? 8 : int64_t(8) * world;
+  d.NB = (nb0 + mult - 1) / mult * mult;
   d.per = (n + d.NB - 1) / d.NB;
   d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
   d.L = 2 * d.NB * d.T;
-  d.ok = n >= 2 && n < int64_t(UINT32_MAX) && d.L <= kMaxWS && d.per <= kSelPts;
+  d.ok = n >= 2 && n < int64_t(UINT32_MAX) && d.L <= kMaxWS && d.per <= kSelPts && world >= 1;
   return d;
 }
 
+// One candidate record (ws_select_kernel's CandRec: f and the point id, -1 = none); 16 bytes with no
+// padding, so the records cross the transport as plain bytes.
 struct Cand {
   double f;
-  int32_t id;
+  int64_t id;
 };
+static_assert(sizeof(Cand) == 16, "candidate records are exchanged as 16-byte records");
 
 // One device GEMV + half-sum pass: f[i] += sum over halves c of half(c, i) (see the header comment).
 void gemv_update(const double* K, int64_t ldk, int64_t n, const int32_t* cols, const double* coef, int64_t cnt,
@@ -87,17 +93,18 @@ void gemv_update(const double* K, int64_t ldk, int64_t n, const int32_t* cols, c
   });
 }
 
-}  // namespace
-
-extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n,
-                                             double* alpha, int32_t warm, const svm_params* pp, int32_t qws,
-                                             double tau_frac, int32_t inner_wss, svm_result* res, int64_t* stats,
-                                             svm_decomp_trace* tr) {
-  svm_params p;
-  if (pp)
-    p = *pp;
-  else
-    svm_default_params(&p);
+// The solve of one rank (t == nullptr: one rank).  Distributed (decomp.hip run_decomp, world > 1):
+// this rank owns the blocks [rank NB / world, (rank + 1) NB / world) of the global block partition,
+// keeps f for their points only, selects their candidates, and ONE all-gather of the candidate records
+// per outer iteration (rank-major) gives every rank the same list; every rank then builds the same
+// working set and runs the same inner solve on its alpha replica (K is all n x n on every rank), and
+// updates f for its own rows.  The block partition is the one-rank partition for world | 8, so the
+// trajectory is the one-rank trajectory bit for bit.  Returns SVM_OK or an error code (set_error);
+// transport failures throw (TransportError / CascadeAborted).
+int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, double* alpha, int32_t warm,
+                 const svm_params& p, int32_t qws, double tau_frac, int32_t inner_wss, svm_result* res,
+                 int64_t* stats, svm_decomp_trace* tr, Transport* t) {
+  const int world = t ? t->world() : 1, rank = t ? t->rank() : 0;
   if (!K || !y || !alpha || n < 2 || ldk < n) {
     set_error("svm_decomp_train_gram: bad arguments");
     return SVM_ERR_ARG;
@@ -106,10 +113,24 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
     set_error("svm_decomp_train_gram: tau_frac must be in [0, 0.5)");
     return SVM_ERR_ARG;
   }
-  const Shape sh = shape(n, qws > 0 ? qws : kMaxWS);
+  if (tr && world != 1) {
+    set_error("svm_decomp_train_gram: a trace needs one rank");
+    return SVM_ERR_ARG;
+  }
+  const Shape sh = shape(n, qws > 0 ? qws : kMaxWS, world);
   if (!sh.ok) {
     set_error("svm_decomp_train_gram: n = %lld is outside the solver's shapes", (long long)n);
     return SVM_ERR_ARG;
+  }
+  const int64_t NBr = sh.NB / world, bb0 = rank * NBr;
+  const int64_t lo = std::min<int64_t>(n, bb0 * sh.per), hi = std::min<int64_t>(n, (bb0 + NBr) * sh.per);
+  const int64_t nloc = hi - lo, Lr = 2 * NBr * sh.T, LhR = NBr * sh.T;
+  // fault injection (tests): rank SVM355_DECOMP_FAIL_RANK fails at the start of outer iteration
+  // SVM355_DECOMP_FAIL_OUTER (default 0); its peers must leave their all-gather with an error
+  int fail_outer = -1;
+  if (const char* fr = getenv("SVM355_DECOMP_FAIL_RANK"); fr && world > 1 && atoi(fr) == rank) {
+    const char* fo = getenv("SVM355_DECOMP_FAIL_OUTER");
+    fail_outer = fo ? std::max(0, atoi(fo)) : 0;
   }
   const auto t0 = std::chrono::steady_clock::now();
   WorkerTeam team(std::max<int32_t>(1, std::min<int32_t>(resolve_threads(p.n_threads), int32_t(n / 256) + 1)));
@@ -119,10 +140,11 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
   auto in_low = [&](int32_t yi, double a) { return (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi); };
 
   // ---- start: cold (alpha = 0, f = -y: ws_init_kernel) or warm (f = -y + K (alpha y) over the
-  // nonzero alphas, ascending, in chunks of kMaxWS columns: decomp.hip's warm start)
-  std::vector<double> f(static_cast<size_t>(n));
+  // nonzero alphas, ascending, in chunks of kMaxWS columns: decomp.hip's warm start); f of this
+  // rank's rows [lo, hi) only
+  std::vector<double> f(static_cast<size_t>(std::max<int64_t>(nloc, 1)));
   int64_t warm_cols = 0;
-  for (int64_t i = 0; i < n; ++i) f[size_t(i)] = -static_cast<double>(y[i]);
+  for (int64_t i = lo; i < hi; ++i) f[size_t(i - lo)] = -static_cast<double>(y[i]);
   if (!warm) {
     for (int64_t i = 0; i < n; ++i) alpha[i] = 0.0;
   } else {
@@ -135,26 +157,30 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
       }
     warm_cols = int64_t(nzc.size());
     for (size_t c0 = 0; c0 < nzc.size(); c0 += kMaxWS)
-      gemv_update(K, ldk, n, nzc.data() + c0, nzv.data() + c0, int64_t(std::min<size_t>(kMaxWS, nzc.size() - c0)),
-                  f.data(), team);
+      gemv_update(K + lo * ldk, ldk, nloc, nzc.data() + c0, nzv.data() + c0,
+                  int64_t(std::min<size_t>(kMaxWS, nzc.size() - c0)), f.data(), team);
   }
 
   int64_t outer = 0, inner_total = 0, changed_total = 0, last_inner_it = 0;
   int32_t last_reason = SVM_STOP_CONVERGED, stop = SVM_STOP_RUNNING;
   double bh = inf, bl = -inf;
-  std::vector<Cand> cand(size_t(sh.L));
+  std::vector<Cand> cown(size_t(std::max<int64_t>(Lr, 1))), call(size_t(sh.L));
   std::vector<int32_t> W;
   std::vector<double> a, a0, ft, kh, kl;
   std::vector<int32_t> yw, cols;
   std::vector<double> coef;
   if (tr) tr->count = 0;
   for (;;) {
-    // ---- selection: per block, T picks per side in (value, lowest index) order
-    const int64_t Lh = sh.NB * sh.T;
-    team.parallel_for(sh.NB, [&](int64_t blo, int64_t bhi) {
+    if (outer == fail_outer) {
+      set_error("decomposition SMO: injected failure of rank %d at outer iteration %lld", rank, (long long)outer);
+      return SVM_ERR_INTERNAL;
+    }
+    // ---- selection over this rank's blocks: per block, T picks per side in (value, lowest index) order
+    team.parallel_for(NBr, [&](int64_t blo, int64_t bhi) {
       std::vector<char> th, tl;
-      for (int64_t b = blo; b < bhi; ++b) {
-        const int64_t b0 = b * sh.per, b1 = std::min<int64_t>(n, b0 + sh.per);
+      for (int64_t bl_ = blo; bl_ < bhi; ++bl_) {
+        const int64_t b = bb0 + bl_;
+        const int64_t b0 = std::min<int64_t>(n, b * sh.per), b1 = std::min<int64_t>(n, b0 + sh.per);
         const int64_t cnt = std::max<int64_t>(0, b1 - b0);
         th.assign(size_t(cnt), 0);
         tl.assign(size_t(cnt), 0);
@@ -162,7 +188,7 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
           double mv = inf, xv = -inf;
           int64_t mi = -1, xi = -1;
           for (int64_t i = b0; i < b1; ++i) {
-            const double ai = alpha[i], fi = f[size_t(i)];
+            const double ai = alpha[i], fi = f[size_t(i - lo)];
             if (!th[size_t(i - b0)] && in_high(y[i], ai) && fi < mv) {
               mv = fi;
               mi = i;
@@ -172,22 +198,27 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
               xi = i;
             }
           }
-          cand[size_t(b * sh.T + k)] = mi >= 0 ? Cand{mv, int32_t(mi)} : Cand{0.0, -1};
-          cand[size_t(Lh + b * sh.T + k)] = xi >= 0 ? Cand{xv, int32_t(xi)} : Cand{0.0, -1};
+          cown[size_t(bl_ * sh.T + k)] = mi >= 0 ? Cand{mv, mi} : Cand{0.0, -1};
+          cown[size_t(LhR + bl_ * sh.T + k)] = xi >= 0 ? Cand{xv, xi} : Cand{0.0, -1};
           if (mi >= 0) th[size_t(mi - b0)] = 1;
           if (xi >= 0) tl[size_t(xi - b0)] = 1;
         }
       }
     });
+    // ---- the candidate exchange: rank-major [rank r: I_high picks of its blocks, then I_low picks]
+    if (world > 1)
+      t->allgather(cown.data(), Lr * int64_t(sizeof(Cand)), call.data());
+    else
+      std::copy(cown.begin(), cown.begin() + sh.L, call.begin());
     // ---- build: bounds, stop test, the sorted de-duplicated working set
     bh = inf;
     bl = -inf;
-    std::vector<std::pair<int32_t, double>> ids;
-    ids.reserve(cand.size());
-    for (int64_t t = 0; t < sh.L; ++t) {
-      const Cand& c = cand[size_t(t)];
+    std::vector<std::pair<int64_t, double>> ids;
+    ids.reserve(call.size());
+    for (int64_t u = 0; u < sh.L; ++u) {
+      const Cand& c = call[size_t(u)];
       if (c.id < 0) continue;
-      if (t < Lh)
+      if (u % Lr < LhR)
         bh = std::fmin(bh, c.f);
       else
         bl = std::fmax(bl, c.f);
@@ -196,10 +227,10 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
     std::sort(ids.begin(), ids.end(), [](const auto& u, const auto& v) { return u.first < v.first; });
     W.clear();
     std::vector<double> Wf;
-    for (size_t t = 0; t < ids.size(); ++t)
-      if (t == 0 || ids[t].first != ids[t - 1].first) {
-        W.push_back(ids[t].first);
-        Wf.push_back(ids[t].second);
+    for (size_t q = 0; q < ids.size(); ++q)
+      if (q == 0 || ids[q].first != ids[q - 1].first) {
+        W.push_back(int32_t(ids[q].first));
+        Wf.push_back(ids[q].second);
       }
     const int m = int(W.size());
     if (outer > 0 && last_inner_it == 0)
@@ -388,7 +419,7 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
     changed_total += int64_t(cols.size());
     last_inner_it = it;
     last_reason = reason;
-    gemv_update(K, ldk, n, cols.data(), coef.data(), int64_t(cols.size()), f.data(), team);
+    gemv_update(K + lo * ldk, ldk, nloc, cols.data(), coef.data(), int64_t(cols.size()), f.data(), team);
     if (tr && tr->count < tr->cap) {
       const int64_t o = tr->count++;
       if (tr->m) tr->m[o] = m;
@@ -429,6 +460,85 @@ extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const
     res->n_sv = svm_sv_indices(alpha, n, p.sv_tol, nullptr);
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  return SVM_OK;
+}
+
+svm_params params_or_default(const svm_params* pp) {
+  svm_params p;
+  if (pp)
+    p = *pp;
+  else
+    svm_default_params(&p);
+  return p;
+}
+
+}  // namespace
+
+extern "C" SVM_API int svm_decomp_train_gram(const double* K, int64_t ldk, const int32_t* y, int64_t n,
+                                             double* alpha, int32_t warm, const svm_params* pp, int32_t qws,
+                                             double tau_frac, int32_t inner_wss, svm_result* res, int64_t* stats,
+                                             svm_decomp_trace* tr) {
+  return decomp_solve(K, ldk, y, n, alpha, warm, params_or_default(pp), qws, tau_frac, inner_wss, res, stats, tr,
+                      nullptr);
+}
+
+// This process's rank of the distributed form over caller-supplied host collectives (a gloo group
+// under torchrun: the CPU twin of the per-process device rank, svmd_cascade_rank_decomp).
+extern "C" SVM_API int svm_decomp_rank_train_gram(const svm_host_comm* comm, const double* K, int64_t ldk,
+                                                  const int32_t* y, int64_t n, double* alpha, int32_t warm,
+                                                  const svm_params* pp, int32_t qws, double tau_frac,
+                                                  int32_t inner_wss, svm_result* res, int64_t* stats) {
+  if (!host_comm_valid(comm)) {
+    set_error("svm_decomp_rank_train_gram: bad communicator");
+    return SVM_ERR_ARG;
+  }
+  try {
+    auto t = make_hostcomm_transport(*comm, nullptr);
+    return decomp_solve(K, ldk, y, n, alpha, warm, params_or_default(pp), qws, tau_frac, inner_wss, res, stats,
+                        nullptr, comm->world > 1 ? t.get() : nullptr);
+  } catch (const std::exception& e) {
+    set_error("decomposition SMO: %s", e.what());
+    return SVM_ERR_INTERNAL;
+  }
+}
+
+// world thread-ranks of this process over a strict loopback group (the thread-rank twin; the ranks'
+// alpha replicas must come out identical).  alpha / res / stats: rank 0's.
+extern "C" SVM_API int svm_decomp_group_train_gram(int32_t world, const double* K, int64_t ldk, const int32_t* y,
+                                                   int64_t n, double* alpha, int32_t warm, const svm_params* pp,
+                                                   int32_t qws, double tau_frac, int32_t inner_wss, svm_result* res,
+                                                   int64_t* stats, double comm_timeout_s) {
+  if (world < 1 || !K || !y || !alpha || n < 2) {
+    set_error("svm_decomp_group_train_gram: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  const svm_params p = params_or_default(pp);
+  auto token = std::make_shared<AbortToken>();
+  auto lg = std::make_shared<LoopbackGroup>(world, WaitPolicy{token, comm_timeout_s > 0 ? comm_timeout_s : 600.0});
+  auto be = make_cpu_backend();
+  std::vector<std::unique_ptr<LoopbackTransport>> tr;
+  for (int r = 0; r < world; ++r) tr.push_back(std::make_unique<LoopbackTransport>(lg, r, be.get()));
+  std::vector<std::vector<double>> replicas{size_t(world)};
+  for (int r = 1; r < world; ++r) replicas[size_t(r)].assign(alpha, alpha + n);  // warm starts: the same start
+  try {
+    run_rank_threads(
+        world, token,
+        [&](int r) {
+          double* a = r == 0 ? alpha : replicas[size_t(r)].data();
+          const int rc = decomp_solve(K, ldk, y, n, a, warm, p, qws, tau_frac, inner_wss, r == 0 ? res : nullptr,
+                                      r == 0 ? stats : nullptr, nullptr, world > 1 ? tr[size_t(r)].get() : nullptr);
+          if (rc != SVM_OK) throw CascadeError(svm_last_error());
+        },
+        [&](int) {});
+  } catch (const std::exception& e) {
+    set_error("decomposition SMO: %s", e.what());
+    return SVM_ERR_INTERNAL;
+  }
+  for (int r = 1; r < world; ++r)
+    if (!std::equal(alpha, alpha + n, replicas[size_t(r)].begin())) {
+      set_error("decomposition SMO: rank %d's alpha replica differs from rank 0's", r);
+      return SVM_ERR_INTERNAL;
+    }
   return SVM_OK;
 }
 

@@ -782,13 +782,20 @@ struct Group {
 };
 
 // ----------------------------------------------------------------------------- process rank
+// tr: RCCL over the rank's communicator, or (svmd_cascade_rank_create_hostcomm) the caller's host
+// collectives with device buffers staged through host memory -- the per-process launch rehearsed with
+// several processes on one GPU, where RCCL refuses to run.
 struct ProcRank {
   int device = 0;
   bool broken = false;
   double timeout_s = 600.0;
   std::unique_ptr<HipBackend> be;
   ncclComm_t comm = nullptr;
-  std::unique_ptr<RcclTransport> tr;
+  std::unique_ptr<Transport> tr;
+  RcclTransport* rccl = nullptr;  // tr when it is RCCL (deadline / abort policy per call)
+  void set_policy(WaitPolicy wp) {
+    if (rccl) rccl->set_policy(std::move(wp));
+  }
 };
 
 // Runs `script` (exercise.cpp) on every rank of a group; "" on success, else the first error (the
@@ -877,10 +884,9 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   bool used = false;
   double prep = 0.0;
   svm_result res{};
-  // fault injection (tests): this rank fails while the others wait in the solve's first candidate
-  // all-gather; the group's abort must end every rank with an error, not a hang
-  if (const char* fr = getenv("SVM355_DECOMP_FAIL_RANK"); fr && world > 1 && atoi(fr) == rank)
-    throw CascadeError("injected failure before the solve");
+  // fault injection (tests): SVM355_DECOMP_FAIL_RANK / _OUTER make that rank fail at that outer
+  // iteration inside the solve (run_decomp) while the others wait in their candidate all-gather; the
+  // group's abort must end every rank with an error, not a hang
   check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, o),
         "decomposition SMO");
   if (!used) throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan)");
@@ -1155,7 +1161,7 @@ SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y
     svm_default_params(&p);
   try {
     (void)hipSetDevice(pr->device);
-    pr->tr->set_policy(WaitPolicy{nullptr, pr->timeout_s});
+    pr->set_policy(WaitPolicy{nullptr, pr->timeout_s});
     try {
       decomp_on_rank(*pr->be, pr->tr->world() > 1 ? pr->tr.get() : nullptr, X, y, n, d, p, q, alpha_out, r, stats,
                      ms_out, mm_out);
@@ -1201,10 +1207,12 @@ SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32
     std::memcpy(&id, uid, sizeof(id));
     const ncclResult_t rc = RC().CommInitRank(&p->comm, world, id, rank);
     if (rc != ncclSuccess) throw CascadeError(std::string("ncclCommInitRank: ") + RC().GetErrorString(rc));
-    p->tr = std::make_unique<RcclTransport>(p->comm, device, p->be->stream(), WaitPolicy{nullptr, p->timeout_s});
+    auto rt = std::make_unique<RcclTransport>(p->comm, device, p->be->stream(), WaitPolicy{nullptr, p->timeout_s});
+    p->rccl = rt.get();
+    p->tr = std::move(rt);
     require_rccl_runtime();
     if (preflight_enabled()) {
-      p->tr->set_policy(WaitPolicy{nullptr, kPreflightTimeout});
+      p->set_policy(WaitPolicy{nullptr, kPreflightTimeout});
       try {
         exercise_transport(*p->tr, *p->be, preflight_script(world, kPreflightBytes));
       } catch (const std::exception& e) {
@@ -1214,11 +1222,39 @@ SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32
         svmd_cascade_rank_destroy(raw);
         throw CascadeError(std::string("RCCL preflight failed: ") + e.what());
       }
-      p->tr->set_policy(WaitPolicy{nullptr, p->timeout_s});
+      p->set_policy(WaitPolicy{nullptr, p->timeout_s});
     }
     return p.release();
   } catch (const std::exception& e) {
     set_error("svmd_cascade_rank_create: %s", e.what());
+    return nullptr;
+  }
+}
+
+// A process rank on `device` whose exchanges run through the caller's host collectives (e.g. a gloo
+// group under torchrun), device buffers staged through host memory (hostcomm.cpp).  Any number of
+// processes may share one GPU: the per-process path of the N-GPU run (the distributed decomposition,
+// the cascades) rehearsed on one device.  The callbacks must outlive the rank.  A preflight of the
+// driver's op set runs first (collective: every rank creates its rank at the same time).
+SVM_API void* svmd_cascade_rank_create_hostcomm(const svm_host_comm* comm, int32_t device, double comm_timeout_s) {
+  try {
+    if (!host_comm_valid(comm)) throw CascadeError("bad communicator");
+    auto p = std::make_unique<ProcRank>();
+    p->device = device;
+    p->timeout_s = timeout_or_default(comm_timeout_s);
+    if (hipSetDevice(device) != hipSuccess) throw CascadeError("hipSetDevice(" + std::to_string(device) + ") failed");
+    p->be = std::make_unique<HipBackend>(device);
+    p->tr = make_hostcomm_transport(*comm, p->be.get());
+    if (preflight_enabled()) {
+      try {
+        exercise_transport(*p->tr, *p->be, preflight_script(comm->world, kPreflightBytes));
+      } catch (const std::exception& e) {
+        throw CascadeError(std::string("hostcomm preflight failed: ") + e.what());
+      }
+    }
+    return p.release();
+  } catch (const std::exception& e) {
+    set_error("svmd_cascade_rank_create_hostcomm: %s", e.what());
     return nullptr;
   }
 }
@@ -1250,7 +1286,7 @@ SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* h, const void* X, int32_t u
     (void)hipSetDevice(p->device);
     const CascadeConfig cfg = config_from(c);
     const WaitPolicy wp{nullptr, (c && c->comm_timeout_s > 0) ? c->comm_timeout_s : p->timeout_s};
-    p->tr->set_policy(wp);
+    p->set_policy(wp);
     CascadeOutput o;
     try {
       o = run_cascade(*p->tr, *p->be, X, u8 != 0, y, ids, n_part, d, n_total, cfg);
@@ -1259,7 +1295,7 @@ SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* h, const void* X, int32_t u
       p->broken = true;
       throw;
     }
-    return build_cascade_out({&o}, *p->be, p->tr->world(), p->tr->rank(), "rccl", "hip");
+    return build_cascade_out({&o}, *p->be, p->tr->world(), p->tr->rank(), p->tr->name(), "hip");
   } catch (const std::exception& e) {
     set_error("cascade: %s", e.what());
     return nullptr;
@@ -1274,9 +1310,9 @@ SVM_API int svmd_cascade_rank_exercise(void* h, const char* script, double timeo
   }
   try {
     (void)hipSetDevice(p->device);
-    p->tr->set_policy(WaitPolicy{nullptr, timeout_s > 0 ? timeout_s : kPreflightTimeout});
+    p->set_policy(WaitPolicy{nullptr, timeout_s > 0 ? timeout_s : kPreflightTimeout});
     exercise_transport(*p->tr, *p->be, script);
-    p->tr->set_policy(WaitPolicy{nullptr, p->timeout_s});
+    p->set_policy(WaitPolicy{nullptr, p->timeout_s});
     return SVM_OK;
   } catch (const std::exception& e) {
     p->tr->abort();

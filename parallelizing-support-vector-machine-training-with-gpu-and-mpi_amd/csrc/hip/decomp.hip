@@ -1348,6 +1348,14 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   if (const char* v = getenv("SVM355_DECOMP_BATCH")) batch = std::max(1, atoi(v));
   if (tr) batch = 1;  // the trace reads every outer iteration back
   int32_t* gate = &ctl->stop;
+  // fault injection (tests, world > 1): rank SVM355_DECOMP_FAIL_RANK fails when it is about to enqueue
+  // outer iteration SVM355_DECOMP_FAIL_OUTER (default 0: before the first selection), while its peers
+  // wait in their candidate all-gathers (decomp_cpu.cpp has the same hook)
+  int64_t fail_outer = -1;
+  if (const char* fr = getenv("SVM355_DECOMP_FAIL_RANK"); fr && world > 1 && atoi(fr) == rank) {
+    const char* fo = getenv("SVM355_DECOMP_FAIL_OUTER");
+    fail_outer = fo ? std::max(0, atoi(fo)) : 0;
+  }
   const int64_t max_batches = p.max_iter / std::max(1, batch) + 64;  // a stop comes well before: never spin
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                            \
   do {                                                                                                             \
@@ -1376,6 +1384,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   for (int64_t bt = 0;; ++bt) {
     DecompCtl* pub = tr ? nullptr : ctl_pub + (bt & 1);  // the trace path copies the block itself
     for (int bi = 0; bi < batch; ++bi) {
+      if (bt * batch + bi == fail_outer) {
+        set_error("injected failure of rank %d at outer iteration %lld", rank, (long long)fail_outer);
+        return SVM_ERR_INTERNAL;
+      }
       if (NBr > 0)
         hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
                            T, p.C, p.eps, cown, cown + NBr * T, ctl);

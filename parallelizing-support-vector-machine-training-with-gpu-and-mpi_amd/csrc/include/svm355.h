@@ -242,6 +242,21 @@ SVM_API svm_cascade_out* svm_cascade_rank_fit_cpu(const svm_host_comm* comm, con
                                                   const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
                                                   const svm_cascade_cfg* cfg);
 
+// The distributed form of svm_decomp_train_gram (decomp.hip's world > 1 solve on the CPU oracle): this
+// process's rank owns 1/world of the selection blocks and of f, and the ranks all-gather their
+// candidate records once per outer iteration through `comm`; every rank passes the whole K and gets the
+// whole alpha (a replica).  For world dividing 8 the trajectory is svm_decomp_train_gram's bit for bit.
+// Fault injection: SVM355_DECOMP_FAIL_RANK / SVM355_DECOMP_FAIL_OUTER (that rank fails at that outer
+// iteration; its peers leave their exchange with an error).
+SVM_API int svm_decomp_rank_train_gram(const svm_host_comm* comm, const double* K, int64_t ldk, const int32_t* y,
+                                       int64_t n, double* alpha, int32_t warm, const svm_params* p, int32_t q,
+                                       double tau_frac, int32_t inner_wss, svm_result* r, int64_t* stats);
+// The same over `world` thread-ranks of this process (strict loopback transport); alpha, r and stats
+// are rank 0's, and every rank's alpha replica must equal it.
+SVM_API int svm_decomp_group_train_gram(int32_t world, const double* K, int64_t ldk, const int32_t* y, int64_t n,
+                                        double* alpha, int32_t warm, const svm_params* p, int32_t q, double tau_frac,
+                                        int32_t inner_wss, svm_result* r, int64_t* stats, double comm_timeout_s);
+
 // Transport exerciser (tests): world CPU-backend thread-ranks over a loopback group (strict = RCCL
 // rules: matched collectives, rendezvous sends, deadlock detection) run `script` (exercise.cpp) with
 // checked payloads.  SVM_OK, or an error naming the ranks / op within timeout_s.

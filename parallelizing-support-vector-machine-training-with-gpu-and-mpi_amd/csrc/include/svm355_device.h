@@ -187,6 +187,10 @@ SVM_API int64_t svmd_nccl_unique_id_bytes(void);
 SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap);
 SVM_API void* svmd_cascade_rank_create(int32_t device, const uint8_t* uid, int32_t world, int32_t rank,
                                        double comm_timeout_s);
+// The same rank over caller-supplied host collectives (svm_host_comm: a gloo group under torchrun), its
+// device buffers staged through host memory; several processes may share one GPU (the per-process
+// launch rehearsed on one device).  Every rank_* entry point below takes either kind of rank.
+SVM_API void* svmd_cascade_rank_create_hostcomm(const svm_host_comm* comm, int32_t device, double comm_timeout_s);
 SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* rank, const void* X, int32_t u8, const int32_t* y,
                                                const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,
                                                const svm_cascade_cfg* cfg);

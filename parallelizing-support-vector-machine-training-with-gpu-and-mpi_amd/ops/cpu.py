@@ -83,6 +83,42 @@ def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Op
     return a, SMOResult.from_struct(r), stats, tr
 
 
+def _decomp_stats(st) -> dict:
+    return {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
+            "solve_us": int(st[3]), "update_columns": int(st[4])}
+
+
+def decomp_train_gram_dist(K: np.ndarray, y: np.ndarray, params: SVMParams, world: int = 1, comm=None,
+                           alpha: Optional[np.ndarray] = None, q: int = 1024, tau_frac: float = 0.1,
+                           inner_wss: int = 3, comm_timeout_s: float = 120.0):
+    """The distributed form of ``decomp_train_gram`` (decomp.hip's world > 1 solve on the CPU oracle):
+    ``comm`` = a ``HostCommRank`` (this process's rank over a gloo group, torchrun), or ``world``
+    thread-ranks of this process over the strict loopback transport.  Every rank owns 1/world of the
+    selection blocks and of f and all-gathers its candidate records once per outer iteration; for world
+    dividing 8 the result is ``decomp_train_gram``'s bit for bit.  Returns (alpha, SMOResult, stats)."""
+    K = _c64(K)
+    y = _c32(y)
+    n = y.shape[0]
+    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    r = N.SvmResult()
+    st = (ctypes.c_int64 * 8)()
+    p = params.to_struct()
+    if comm is not None:
+        comm.error = None
+        rc = N.core().svm_decomp_rank_train_gram(ctypes.addressof(comm.comm), N.ptr(K), K.shape[1], N.ptr(y), n,
+                                                 N.ptr(a), int(alpha is not None), ctypes.byref(p), int(q),
+                                                 float(tau_frac), int(inner_wss), ctypes.byref(r), st)
+        if rc != 0 and comm.error is not None:
+            raise N.NativeError(f"{N.last_error()} (collective error: {comm.error!r})") from comm.error
+        N.check(rc, "svm_decomp_rank_train_gram")
+    else:
+        N.check(N.core().svm_decomp_group_train_gram(int(world), N.ptr(K), K.shape[1], N.ptr(y), n, N.ptr(a),
+                                                     int(alpha is not None), ctypes.byref(p), int(q), float(tau_frac),
+                                                     int(inner_wss), ctypes.byref(r), st, float(comm_timeout_s)),
+                "svm_decomp_group_train_gram")
+    return a, SMOResult.from_struct(r), _decomp_stats(st)
+
+
 def rbf_matrix(A: np.ndarray, B: np.ndarray, gamma: float, n_threads: int = 0) -> np.ndarray:
     """Reference-exact RBF kernel matrix (direct sum of squared differences)."""
     A = _c64(A)

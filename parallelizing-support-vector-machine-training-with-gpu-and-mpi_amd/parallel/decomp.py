@@ -19,8 +19,12 @@ decomposition solver's (tests/test_gpu_decomp.py).  It pays where the GEMV and t
 dominate: large n (see README "Distributed decomposition").
 
 Launch forms: a ``DeviceGroup`` of this process (thread ranks, ``ncclCommInitAll``; or
-``transport="loopback"``: P ranks rehearsed on the visible GPU), or one ``RcclRank`` per process
-under torchrun (``ncclCommInitRank``).
+``transport="loopback"``: P ranks rehearsed on the visible GPU), or one rank per process under
+torchrun: ``RcclRank`` (``ncclCommInitRank``) or ``HostCommDeviceRank`` (the same driver with the
+candidate all-gather over a gloo group, device buffers staged through the host: P processes may share
+ONE GPU, so the per-process path runs at world > 1 on a one-GPU box).  On the CPU the same solve runs
+on the decomposition oracle (``HostCommRank`` under torchrun, or ``transport="cpu"`` thread ranks):
+the multi-process twin the CPU tests launch.
 """
 from __future__ import annotations
 
@@ -60,6 +64,35 @@ def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: 
             "rank_ms": [float(x) for x in ms[:world]], "wall_ms": wall}
 
 
+def cpu_fit(X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024, world: int = 1,
+            comm=None) -> dict:
+    """The same distributed solve on the CPU oracle (csrc/core/decomp_cpu.cpp): ``comm`` = this process's
+    ``HostCommRank`` (torchrun over gloo: the CPU twin of the per-process GPU rank), else ``world``
+    thread-ranks of this process.  Every rank holds the whole reference-exact kernel matrix of the
+    min-max scaled rows (``ops.cpu.rbf_matrix``; small n only), owns 1/world of the selection blocks and
+    of f, and all-gathers its candidate records once per outer iteration."""
+    from ..ops import cpu as C
+    from ..utils.data import MinMaxScaler, check_labels
+
+    params = params or SVMParams()
+    X = np.asarray(X)
+    n, d = X.shape
+    if n > 20000:
+        raise ValueError(f"the CPU decomposition oracle holds the whole {n} x {n} kernel matrix: n <= 20000")
+    y = check_labels(y, n)
+    sc = MinMaxScaler().fit(X)
+    Xs = sc.transform(X)
+    t0 = time.perf_counter()
+    with trace_range(f"svm355.decomp.cpu world={comm.world if comm is not None else world} n={n}"):
+        K = C.rbf_matrix(Xs, Xs, params.gamma, params.n_threads)
+        a, r, st = C.decomp_train_gram_dist(K, y, params, world=world, comm=comm, q=q,
+                                            comm_timeout_s=getattr(comm, "timeout_s", 120.0))
+    wall = (time.perf_counter() - t0) * 1e3
+    return {"alpha": a, "b": r.b, "b_high": r.b_high, "b_low": r.b_low, "iterations": r.iterations,
+            "stop_reason": r.stop_reason, "n_sv": int(np.count_nonzero(a > params.sv_tol)), "mn": sc.min_,
+            "mx": sc.max_, "stats": {**st, "inner_threads": 0}, "rank_ms": [wall], "wall_ms": wall, "rows": Xs}
+
+
 def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
     """One distributed decomposition solve over a ``DeviceGroup`` (its ranks are this process's
     threads; RCCL or the loopback rehearsal)."""
@@ -90,7 +123,13 @@ class DistributedDecompSVC:
         from .rccl import DeviceGroup
 
         t0 = time.perf_counter()
-        if self.rank is not None:
+        if self.rank is not None and self.rank.device == "cpu":  # HostCommRank: the CPU twin under torchrun
+            out = cpu_fit(X, y, self.params, self.working_set, comm=self.rank)
+            dev = "cpu"
+        elif self.rank is None and self.transport == "cpu":  # thread ranks on the CPU oracle
+            out = cpu_fit(X, y, self.params, self.working_set, world=self.world)
+            dev = "cpu"
+        elif self.rank is not None:
             out = rank_fit(self.rank, X, y, self.params, self.working_set)
             dev = f"cuda:{self.rank.device}"
         else:
@@ -110,7 +149,9 @@ class DistributedDecompSVC:
         m.n_iter_, m.stop_reason_ = out["iterations"], out["stop_reason"]
         X = np.asarray(X)
         with trace_range("svm355.decomp.model"):
-            if X.dtype == np.uint8:
+            if dev == "cpu":
+                m.support_vectors_ = out["rows"][sup]
+            elif X.dtype == np.uint8:
                 m._device_model_from_u8(X[sup], dev)
             else:  # pixel values held as FP64 (validated integers): widened on the host
                 m.support_vectors_ = m.scaler_.transform(X[sup])

@@ -123,3 +123,45 @@ class HostCommRank:
 
     def close(self) -> None:
         pass
+
+
+class HostCommDeviceRank:
+    """This process's GPU rank with its exchanges over a ``torch.distributed`` group instead of RCCL
+    (``svmd_cascade_rank_create_hostcomm``): device buffers are staged through host memory around the
+    gloo collectives.  RCCL refuses two ranks on one GPU, this does not, so ``torchrun
+    --nproc-per-node P bench.py --gpus P --transport hostcomm`` runs the per-process path of the N-GPU
+    run (distributed decomposition, cascades) with P processes on ONE GPU: the same native drivers as
+    ``RcclRank``, only the transport differs.  Used wherever an ``RcclRank`` is (its ``handle`` takes
+    the same ``svmd_cascade_rank_*`` entry points).  Collective: every rank constructs it together."""
+
+    def __init__(self, device: int, group=None, comm_timeout_s: float = 600.0):
+        self.host = HostCommRank(group, comm_timeout_s)  # owns the callbacks: must outlive the handle
+        self.device, self.world, self.rank = int(device), self.host.world, self.host.rank
+        self.handle = N.hip().svmd_cascade_rank_create_hostcomm(ctypes.addressof(self.host.comm), self.device,
+                                                               float(comm_timeout_s))
+        if not self.handle:
+            err = N.last_error()
+            raise N.NativeError(f"{err} (collective error: {self.host.error!r})" if self.host.error else err)
+
+    @property
+    def error(self):
+        return self.host.error
+
+    def barrier(self) -> None:
+        N.check(N.hip().svmd_cascade_rank_barrier(self.handle), "svmd_cascade_rank_barrier")
+
+    def exercise(self, script: str, timeout_s: float = 20.0) -> None:
+        rc = N.hip().svmd_cascade_rank_exercise(self.handle, script.encode(), float(timeout_s))
+        if rc != 0:
+            raise N.NativeError(N.last_error())
+
+    def close(self) -> None:
+        if self.handle:
+            N.hip().svmd_cascade_rank_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

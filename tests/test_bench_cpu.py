@@ -2,6 +2,7 @@
 solve plus rank 0's merge; the solo device times of a serial-solve rehearsal when present), the
 launch checks of ``--gpus N``, and the solve-log fields the critical path reads from the native
 driver."""
+import json
 import sys
 from pathlib import Path
 
@@ -103,6 +104,17 @@ def test_bench_decomp_solver_needs_gpus_and_its_own_parallel_mode(capsys):
                        "--rows", "600"]) == 2
 
 
-def test_bench_parallel_decomp_refuses_cpu(capsys):
-    assert bench.main(["--gpus", "2", "--device", "cpu", "--parallel", "decomp", "--rows", "600", "--steps", "1"]) == 2
-    assert "--parallel decomp needs uint8 pixel rows on GPUs" in capsys.readouterr().err
+def test_bench_parallel_decomp_cpu_twin_thread_ranks(capsys):
+    """--device cpu --parallel decomp: the distributed decomposition's CPU twin on thread ranks (strict
+    loopback), bit-identical to the one-rank oracle solve."""
+    assert bench.main(["--gpus", "2", "--device", "cpu", "--parallel", "decomp", "--rows", "600", "--steps", "1",
+                       "--baseline-1gpu", "1"]) == 0
+    out = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert out["config"]["parallelism"] == "distributed-decomp-dp2"
+    assert out["launch_form"] == "thread ranks on the CPU oracle (loopback)"
+    assert out["bit_identical_to_1gpu"] is True and out["stop_reason"] == "converged"
+
+
+def test_bench_hostcomm_needs_torchrun(capsys):
+    assert bench.main(["--gpus", "2", "--transport", "hostcomm", "--parallel", "decomp", "--rows", "600"]) == 2
+    assert "--transport hostcomm is a per-process transport" in capsys.readouterr().err

@@ -102,3 +102,57 @@ def test_oracle_reports_the_real_working_set_capacity():
     assert st["working_set"] == 128  # 64 blocks x 2 sides x 1 pick
     assert max(x["m"] for x in tr.records()) <= 128
     assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_distributed_oracle_thread_ranks_are_bit_identical(prob2k, world):
+    """decomp.hip's world > 1 form on the CPU oracle: every rank owns 1/world of the blocks and of f,
+    the candidate records are all-gathered (strict loopback), each rank keeps an alpha replica (the
+    native side requires them all equal).  For world | 8 the block partition is the one-rank one, so
+    alpha, b and the iteration counts equal the one-rank solve bit for bit."""
+    K, y = prob2k
+    p = SVMParams(n_threads=2)
+    a, r, st, _ = C.decomp_train_gram(K, y, p)
+    a2, r2, st2 = C.decomp_train_gram_dist(K, y, p, world=world)
+    np.testing.assert_array_equal(a2, a)
+    assert r2.b == r.b and r2.iterations == r.iterations
+    assert st2["outer_iterations"] == st["outer_iterations"] and st2["update_columns"] == st["update_columns"]
+
+
+def test_distributed_oracle_other_world_converges(prob2k):
+    """world = 3 does not divide 8: the blocks round to a multiple of 24 (another partition, another
+    trajectory), and the solve still meets the stop test with the same support vectors."""
+    K, y = prob2k
+    p = SVMParams(n_threads=2)
+    a, r, st = C.decomp_train_gram_dist(K, y, p, world=3)
+    assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
+    ref, _, _, _ = C.decomp_train_gram(K, y, p)
+    np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), np.flatnonzero(ref > p.sv_tol))
+
+
+def test_distributed_oracle_warm_start_is_bit_identical(prob2k):
+    K, y = prob2k
+    p = SVMParams(n_threads=2)
+    a, _, _, _ = C.decomp_train_gram(K, y, p)
+    w = a.copy()
+    i = int(np.flatnonzero((a > 1e-3) & (a < p.C - 1e-3))[0])
+    j = int(np.flatnonzero((y == y[i]) & (a > 1e-3) & (a < p.C - 1e-3) & (np.arange(len(y)) != i))[0])
+    delta = 0.5 * min(a[i], p.C - a[j])
+    w[i] -= delta
+    w[j] += delta
+    a1, r1, st1, _ = C.decomp_train_gram(K, y, p, alpha=w)
+    a4, r4, st4 = C.decomp_train_gram_dist(K, y, p, world=4, alpha=w)
+    np.testing.assert_array_equal(a4, a1)
+    assert r4.b == r1.b and st4["outer_iterations"] == st1["outer_iterations"] >= 1
+
+
+def test_distributed_oracle_failing_rank_ends_every_rank(prob2k, monkeypatch):
+    """SVM355_DECOMP_FAIL_RANK / _OUTER: rank 2 fails at outer iteration 3 while its peers wait in the
+    candidate all-gather; every rank leaves with the failing rank's error (no hang)."""
+    from svm355._native import NativeError
+
+    K, y = prob2k
+    monkeypatch.setenv("SVM355_DECOMP_FAIL_RANK", "2")
+    monkeypatch.setenv("SVM355_DECOMP_FAIL_OUTER", "3")
+    with pytest.raises(NativeError, match="rank 2: .*injected failure of rank 2 at outer iteration 3"):
+        C.decomp_train_gram_dist(K, y, SVMParams(n_threads=1), world=4, comm_timeout_s=30)

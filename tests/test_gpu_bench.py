@@ -75,3 +75,58 @@ def test_torchrun_one_process_default_decomp():
     assert out["bit_identical_to_1gpu"] is True and out["speedup_vs_1gpu"] > 0
     assert out["cascade_star"]["converged"] and out["cascade_tree"]["converged"]
     assert out["rccl_runtime"].startswith("2.")
+
+
+def _torchrun(nproc, *args, env_extra=None, timeout=280):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=str(ROOT), **(env_extra or {}))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", str(nproc), *args]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    return p, time.perf_counter() - t0
+
+
+@pytest.mark.parametrize("nproc,rows", [(2, 60000), (4, 6000)])
+def test_torchrun_processes_share_one_gpu_over_hostcomm(nproc, rows):
+    """the per-process path of the N-GPU headline (torchrun, one rank per process,
+    svmd_cascade_rank_decomp) at world > 1 on the one GPU of the box.  RCCL refuses two ranks on one
+    device, so the ranks exchange over the gloo group (HostCommDeviceRank: the candidate all-gather and
+    the row all-gather staged through host memory); the rest -- the native driver, the block ownership,
+    the replicated inner solve, bench.py's torchrun branch and timing max -- is the RCCL run's code.
+    The model must equal the one-GPU decomposition solve bit for bit; at 60k the star and tree cascades
+    run on the same per-process ranks too."""
+    casc = "1" if rows == 60000 else "0"
+    p, wall = _torchrun(nproc, "--parallel", "decomp", "--transport", "hostcomm", "--rows", str(rows),
+                        "--test-rows", "1000", "--steps", "1", "--warmup", "1", "--baseline-1gpu", "1",
+                        "--cascade-steps", casc)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == nproc and out["launch"].startswith("torchrun")
+    assert out["config"]["parallelism"] == f"distributed-decomp-dp{nproc}" and out["config"]["global_batch"] == rows
+    assert out["launch_form"].startswith("one rank per process over gloo, host-staged")
+    assert out["stop_reason"] == "converged" and out["bit_identical_to_1gpu"] is True
+    assert out["ms_per_step"] <= wall * 1e3
+    if rows == 60000:
+        assert out["n_sv"] == 1380
+        for topo in ("star", "tree"):
+            c = out[f"cascade_{topo}"]
+            assert c["converged"] and c["transport"] == "hostcomm" and c["accuracy"] > 0.99
+            assert abs(c["b_minus_headline_b"]) <= 10 * 1e-5
+
+
+def test_torchrun_hostcomm_rank_failing_mid_solve_ends_every_process():
+    """Rank 1 fails at outer iteration 3 of the distributed decomposition while rank 0 waits in its
+    candidate all-gather: both processes exit non-zero and torchrun reports the failure, well within
+    the comm deadline (the reference's MPI_Abort contract)."""
+    p, wall = _torchrun(2, "--parallel", "decomp", "--transport", "hostcomm", "--rows", "6000", "--test-rows", "500",
+                        "--steps", "1", "--warmup", "0", "--baseline-1gpu", "0", "--comm-timeout", "20",
+                        env_extra={"SVM355_DECOMP_FAIL_RANK": "1", "SVM355_DECOMP_FAIL_OUTER": "3"}, timeout=200)
+    assert p.returncode != 0
+    err = p.stdout + p.stderr
+    assert "injected failure of rank 1 at outer iteration 3" in err, err[-3000:]
+    assert wall < 150

@@ -168,3 +168,62 @@ def test_torchrun_cascade_cli_is_mpirun_np(tmp_path):
     ja, jb = json.loads(a.read_text()), json.loads(b.read_text())
     assert ja["transport"] == "hostcomm" and ja["world"] == 2
     assert ja["b"] == jb["b"] and ja["n_sv"] == jb["n_sv"] and ja["rounds"] == jb["rounds"]
+
+
+@pytest.mark.parametrize("nproc", [1, 2, 4])
+def test_torchrun_decomp_ranks_match_one_rank(nproc):
+    """The distributed decomposition solver's per-process path (bench.py --parallel decomp under torchrun,
+    the launch the driver's N-GPU run takes) on its CPU twin: every process a rank over gloo
+    (``HostCommRank`` -> svm_decomp_rank_train_gram), owning 1/P of the selection blocks and of f, the
+    candidate records all-gathered per outer iteration.  alpha, b and the iteration counts must equal
+    the one-rank solve (bench.py's bit_identical_to_1gpu compares every bit of alpha)."""
+    out = _torchrun_bench(nproc, "--parallel", "decomp", "--rows", "1200", "--test-rows", "200", "--steps", "1",
+                          "--warmup", "0", "--baseline-1gpu", "1")
+    assert out["n_gpus"] == nproc and out["launch"].startswith("torchrun")
+    assert out["config"]["parallelism"] == f"distributed-decomp-dp{nproc}"
+    assert out["launch_form"] == "one rank per process (CPU oracle over gloo)"
+    assert out["stop_reason"] == "converged" and out["decomp_stats"]["outer_iterations"] >= 1
+    assert out["bit_identical_to_1gpu"] is True
+
+
+_DECOMP_FAIL_SCRIPT = textwrap.dedent("""
+    import datetime, os, sys, time
+    import torch.distributed as dist
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.hostcomm import HostCommRank
+    from svm355.utils.data import synthetic_mnist
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+    r = dist.get_rank()
+    tr = synthetic_mnist(1200, seed=5)
+    t0 = time.time()
+    try:
+        DistributedDecompSVC(dist.get_world_size(), rank=HostCommRank(comm_timeout_s=8.0)).fit(tr.X, tr.y)
+    except Exception as e:
+        print(f"rank {r} failed after {time.time() - t0:.1f} s: {e}", flush=True)
+        os._exit(3)  # MPI_Abort-like: an orderly exit would wait for the process group's teardown
+    print(f"rank {r} finished", flush=True)
+""")
+
+
+def test_a_decomp_rank_failing_mid_solve_ends_every_process():
+    """Rank 1 of 3 fails at outer iteration 2 of the distributed decomposition (SVM355_DECOMP_FAIL_RANK /
+    _OUTER) while ranks 0 and 2 wait in the candidate all-gather: every process must exit non-zero
+    within the deadline (the reference's MPI_Abort, mpi_svm_main3.cpp:420-428)."""
+    port, env = _port(), dict(_env(), SVM355_DECOMP_FAIL_RANK="1", SVM355_DECOMP_FAIL_OUTER="2")
+    procs = []
+    for r in range(3):
+        e = dict(env, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _DECOMP_FAIL_SCRIPT], cwd=ROOT, env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    t0 = time.time()
+    try:
+        outs = [p.communicate(timeout=150)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert time.time() - t0 < 120
+    assert [p.returncode for p in procs] == [3, 3, 3], outs
+    assert "injected failure of rank 1 at outer iteration 2" in outs[1], outs[1]
+    for r in (0, 2):
+        assert f"rank {r} failed" in outs[r] and "hostcomm allgather" in outs[r], outs[r]

@@ -44,3 +44,41 @@ def test_asan_serial_csv_with_malformed_rows(asan_exe, tmp_path):
     (tmp_path / "d_test_data.csv").write_text("\n".join(lines[:120]) + "\n")
     out = _run(asan_exe, ["--dataset", "d", "--gamma", "0.01"], tmp_path)
     assert out.startswith("n = 300")
+
+
+# ---- the threaded host code: apps/svm_threads.cpp runs the strict-loopback
+# cascades (star P = 2/3/8, tree P = 2/4/8), the same cascades over HostCommTransport (its callbacks
+# served by loopback ranks in threads), an abort mid-round, a checkpoint + resume, the decomposition
+# oracle's 8-thread worker team and its distributed form on 8 loopback / 4 hostcomm thread ranks with a
+# rank failing mid-solve.  Every scenario checks its own result (bit-identical models, the failing
+# rank's error on every rank); the sanitizers check the memory and the synchronisation.
+
+@pytest.fixture(scope="module")
+def thread_exes():
+    return build.build_sanitized_threads()
+
+
+def _run_threads(exe, args, env_extra, timeout):
+    env = {"PATH": "/usr/bin:/bin", "TMPDIR": "/tmp", **env_extra}
+    r = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=timeout, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "ALL SCENARIOS OK" in r.stdout, out[-5000:]
+    for bad in ("runtime error", "AddressSanitizer", "LeakSanitizer", "ThreadSanitizer"):
+        assert bad not in out, out[-5000:]
+    return r.stdout
+
+
+def test_asan_ubsan_threaded_cascades_hostcomm_and_decomp(thread_exes):
+    out = _run_threads(thread_exes[0], [], {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:exitcode=23",
+                                            "UBSAN_OPTIONS": "print_stacktrace=1"}, timeout=900)
+    for line in ("cascade hostcomm star P=8", "cascade loopback tree P=8", "cascade checkpoint + resume",
+                 "decomp distributed, 8 loopback thread ranks", "decomp rank failing mid-solve"):
+        assert line in out
+
+
+def test_tsan_threaded_cascades_hostcomm_and_decomp(thread_exes):
+    """TSan (ROCm clang's runtime: gcc 11's libtsan misreads libstdc++'s condition-variable waits).
+    The quick scenario list (star P = 3, tree P = 4, both transports) keeps the 5-15x TSan slowdown
+    within the test budget; ``bin_tsan/svm_threads`` without --quick runs the full list."""
+    out = _run_threads(thread_exes[1], ["--quick"], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"}, timeout=900)
+    assert "cascade hostcomm tree P=4" in out and "decomp distributed, 4 hostcomm ranks" in out
