@@ -204,6 +204,7 @@ _CORE_SIGS = {
                                      POINTER(SvmResult), _P, c_int64]),
     "svm_decomp_train_gram": (c_int32, [_P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32, c_double,
                                         c_int32, POINTER(SvmResult), POINTER(c_int64), POINTER(SvmDecompTrace)]),
+    "svm_crash_handler_install": (c_int32, [c_char_p]),
     "svm_decomp_gemv_ref": (c_int32, [_P, c_int64, c_int64, _P, _P, c_int64, _P]),
     "svm_decomp_rank_train_gram": (c_int32, [_P, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32,
                                              c_double, c_int32, POINTER(SvmResult), POINTER(c_int64)]),
@@ -340,6 +341,10 @@ def core():
                 build.build_core()
             # RTLD_GLOBAL so the device library resolves the core's symbols from this copy.
             _core = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), _CORE_SIGS)
+            crash = os.environ.get("SVM355_CRASH_MAPS")
+            if crash:  # crash evidence: signal, PC, backtrace and /proc/self/maps appended to this file
+                check(_core.svm_crash_handler_install(crash.replace("{pid}", str(os.getpid())).encode()),
+                      "svm_crash_handler_install")
     return _core
 
 

@@ -1182,6 +1182,13 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     ldc_cache = (nloc + 3) & ~int64_t(3);  // a multiple of 4: 16-byte row pairs (or quads) in the reader
     const size_t slot_b = size_t(ldc_cache) * 8;
     cap = std::min<int64_t>(cap, int64_t((free_b + ctx->rc_cache_bytes) / 2 / slot_b) - kMaxWS);
+    // and at most a quarter of the GPU's HBM (SVM355_DECOMP_CCACHE_FRAC): the slab is a grow-only
+    // buffer of the context, kept for the next fit, that PyTorch's allocator cannot see -- it must leave
+    // room for the caller's tensors and other contexts on the device.  At 1M rows that is
+    // ~8,000 slots of 8 MB for ~6,100 distinct columns a fit moves, so no fit of n <= 1M loses a hit.
+    double frac = 0.25;
+    if (const char* v = getenv("SVM355_DECOMP_CCACHE_FRAC")) frac = std::min(0.9, std::max(0.0, atof(v)));
+    cap = std::min<int64_t>(cap, int64_t(double(total_b) * frac / double(slot_b)) - kMaxWS);
     int64_t min_cap = 256;
     if (const char* v = getenv("SVM355_DECOMP_CCACHE_SLOTS")) {  // tests: a small cache (its scratch path)
       cap = std::min<int64_t>(cap, atoll(v));

@@ -257,6 +257,11 @@ SVM_API int svm_decomp_group_train_gram(int32_t world, const double* K, int64_t 
                                         double* alpha, int32_t warm, const svm_params* p, int32_t q, double tau_frac,
                                         int32_t inner_wss, svm_result* r, int64_t* stats, double comm_timeout_s);
 
+// Crash evidence (opt-in; Python: SVM355_CRASH_MAPS=<path>, "{pid}" replaced by the process id): on
+// SIGSEGV / SIGBUS / SIGILL / SIGFPE / SIGABRT append the signal, faulting address, PC, a raw backtrace
+// and /proc/self/maps to `path` (async-signal-safe calls only), then chain to the previous handler.
+SVM_API int svm_crash_handler_install(const char* path);
+
 // Transport exerciser (tests): world CPU-backend thread-ranks over a loopback group (strict = RCCL
 // rules: matched collectives, rendezvous sends, deadlock detection) run `script` (exercise.cpp) with
 // checked payloads.  SVM_OK, or an error naming the ranks / op within timeout_s.

@@ -107,6 +107,20 @@ def available() -> bool:
     return True
 
 
+def device_empty(shape, dtype, device) -> torch.Tensor:
+    """``torch.empty`` for the library's large device buffers.  On an out-of-memory error the memory the
+    library itself holds outside PyTorch's allocator -- the Gram and the row-cache / column-cache slab
+    its contexts keep between fits, and the grow-only Gram buffers (``release_gram_buffers``) -- is
+    handed back and the allocation retried once: a cache kept for speed never makes a later allocation
+    fail."""
+    try:
+        return torch.empty(shape, dtype=dtype, device=device)
+    except torch.OutOfMemoryError:
+        release_gram_buffers()
+        torch.cuda.empty_cache()
+        return torch.empty(shape, dtype=dtype, device=device)
+
+
 def upload_rows(X: np.ndarray, device, ld: Optional[int] = None) -> torch.Tensor:
     """Host (n, d) rows -> device (n, ld) zero-padded FP64 rows.
 
@@ -117,14 +131,14 @@ def upload_rows(X: np.ndarray, device, ld: Optional[int] = None) -> torch.Tensor
         X = np.ascontiguousarray(X)
         n, d = X.shape
         ld = padded_dim(d) if ld is None else ld
-        out = torch.empty((n, ld), dtype=torch.float64, device=device)
+        out = device_empty((n, ld), torch.float64, device)
         ctx = DeviceContext.get(out.device)
         N.check(ctx.lib.svmd_upload_rows_u8(ctx.bind(), N.ptr(X), n, d, N.ptr(out), ld), "svmd_upload_rows_u8")
         return out
     X = np.ascontiguousarray(X, dtype=np.float64)
     n, d = X.shape
     ld = padded_dim(d) if ld is None else ld
-    out = torch.empty((n, ld), dtype=torch.float64, device=device)
+    out = device_empty((n, ld), torch.float64, device)
     ctx = DeviceContext.get(out.device)
     N.check(ctx.lib.svmd_upload_rows(ctx.bind(), N.ptr(X), n, d, N.ptr(out), ld), "svmd_upload_rows")
     return out
@@ -262,7 +276,7 @@ def gram_buffer(n: int, device) -> torch.Tensor:
     if buf is None or buf.numel() < n * ldk:
         bufs.pop(key, None)
         del buf
-        buf = bufs[key] = torch.empty(n * ldk, dtype=torch.float64, device=device)
+        buf = bufs[key] = device_empty(n * ldk, torch.float64, device)
     return buf[: n * ldk].view(n, ldk)
 
 
@@ -359,7 +373,7 @@ def train(X: torch.Tensor, sqn: torch.Tensor, y: torch.Tensor, alpha: torch.Tens
 def upload_u8(X: np.ndarray, device) -> torch.Tensor:
     """Host uint8 pixel rows (n, d) -> the same bytes on the device (n, d) uint8."""
     X = np.ascontiguousarray(X, dtype=np.uint8)
-    out = torch.empty(X.shape, dtype=torch.uint8, device=device)
+    out = device_empty(X.shape, torch.uint8, device)
     ctx = DeviceContext.get(out.device)
     N.check(ctx.lib.svmd_memcpy_h2d(ctx.bind(), N.ptr(out), N.ptr(X), X.nbytes), "svmd_memcpy_h2d")
     return out
@@ -473,7 +487,7 @@ def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tens
     FP64 rows); None when the integer plan does not apply."""
     n, d = Xu.shape
     if out is None:
-        out = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=Xu.device)
+        out = device_empty((n, (n + 1) // 2 * 2), torch.float64, Xu.device)
     a, b, _ = _host_stats(mn, mx)
     used = ctypes.c_int32(0)
     ctx = _ctx_for(Xu)
@@ -504,7 +518,7 @@ def rbf_gram_sym(X: torch.Tensor, sqn: Optional[torch.Tensor], gamma: float, mn=
     _check_rows(X)
     n = X.shape[0]
     if out is None:
-        out = torch.empty((n, (n + 1) // 2 * 2), dtype=torch.float64, device=X.device)
+        out = device_empty((n, (n + 1) // 2 * 2), torch.float64, X.device)
     ctx = _ctx_for(X)
     a, b, d = _host_stats(mn, mx)
     used = ctypes.c_int32(0)

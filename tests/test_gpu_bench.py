@@ -71,7 +71,7 @@ def test_torchrun_one_process_default_decomp():
     out = json.loads(lines[0])
     _check_common(out, 1, 2, wall)
     assert out["launch"].startswith("torchrun") and out["config"]["parallelism"] == "distributed-decomp-dp1"
-    assert out["launch_form"] == "one rank per process"
+    assert out["launch_form"] == "one rank per process (RCCL)"
     assert out["bit_identical_to_1gpu"] is True and out["speedup_vs_1gpu"] > 0
     assert out["cascade_star"]["converged"] and out["cascade_tree"]["converged"]
     assert out["rccl_runtime"].startswith("2.")

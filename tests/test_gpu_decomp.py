@@ -210,10 +210,12 @@ def test_distributed_process_rank_world1_equals_one_gpu():
     np.testing.assert_array_equal(m.alpha_, one.alpha_)
 
 
-def test_distributed_rank_failure_ends_every_rank(monkeypatch):
-    """A rank that fails (SVM355_DECOMP_FAIL_RANK) while the others wait in the solve's candidate
-    all-gather: the group's abort ends every rank with the error instead of a hang, and the loopback
-    group stays usable for the next fit."""
+@pytest.mark.parametrize("fail_outer", [None, "3"])
+def test_distributed_rank_failure_ends_every_rank(monkeypatch, fail_outer):
+    """A rank that fails (SVM355_DECOMP_FAIL_RANK; before the first selection, or mid-solve at outer
+    iteration SVM355_DECOMP_FAIL_OUTER) while the others wait in the solve's candidate all-gather: the
+    group's abort ends every rank with the error instead of a hang, and the loopback group stays usable
+    for the next fit."""
     from svm355._native import NativeError
     from svm355.parallel.decomp import DistributedDecompSVC
     from svm355.parallel.rccl import DeviceGroup
@@ -222,14 +224,42 @@ def test_distributed_rank_failure_ends_every_rank(monkeypatch):
     g = DeviceGroup(2, "loopback")
     try:
         monkeypatch.setenv("SVM355_DECOMP_FAIL_RANK", "1")
+        if fail_outer:
+            monkeypatch.setenv("SVM355_DECOMP_FAIL_OUTER", fail_outer)
         t0 = time.perf_counter()
         with pytest.raises(NativeError, match="injected failure"):
             DistributedDecompSVC(2, group=g).fit(tr.X, tr.y)
         assert time.perf_counter() - t0 < 60
         monkeypatch.delenv("SVM355_DECOMP_FAIL_RANK")
+        monkeypatch.delenv("SVM355_DECOMP_FAIL_OUTER", raising=False)
         m = DistributedDecompSVC(2, group=g).fit(tr.X, tr.y)
     finally:
         g.close()
     one = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
     assert m.stop_reason_ == "converged" and m.b_ == one.b_
     np.testing.assert_array_equal(m.alpha_, one.alpha_)
+
+
+def test_column_cache_leaves_the_device_to_torch():
+    """the decomposition's column cache (a grow-only slab of the context, outside PyTorch's
+    allocator) takes at most a quarter of the HBM, and a later torch allocation that needs that memory
+    gets it: ``ops.device.device_empty`` hands the library's caches back on an out-of-memory error."""
+    import ctypes
+
+    from svm355.ops import device as D
+
+    tr = synthetic_mnist(250000, seed=3).compact()
+    m = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    assert m.stop_reason_ == "converged"
+    ctx = D.DeviceContext.get("cuda:0")
+    slab = ctypes.c_int64(0)
+    assert ctx.lib.svmd_cache_bytes(ctx.handle, None, ctypes.byref(slab)) == 0
+    free, total = torch.cuda.mem_get_info(0)
+    assert 0 < slab.value <= total // 4  # the cache ran (250k rows outgrow the last-level cache), capped
+    need = free + slab.value // 2  # more than is free: only the slab's memory makes it fit
+    t = D.device_empty(need // 8, torch.float64, "cuda:0")
+    assert ctx.lib.svmd_cache_bytes(ctx.handle, None, ctypes.byref(slab)) == 0 and slab.value == 0
+    del t
+    torch.cuda.empty_cache()
+    m2 = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)  # the cache is rebuilt on demand
+    assert m2.b_ == m.b_
