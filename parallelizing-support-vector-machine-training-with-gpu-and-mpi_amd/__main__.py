@@ -11,10 +11,13 @@ cascade  the MPI Cascade programs (code/mpi_svm_main2.cpp ``--topology star`` = 
          thread-ranks on the C++ oracle.  stdout follows the reference's ``[rank 0] ...`` lines
          (SURVEY §5.5).  ``--native`` runs the C++ CLI bin/svm_cascade (same driver, no Python).
 
-scale    the rank-count sweep of code/mpi_svm2.sh / mpi_svm3.sh (``mpirun -np P`` for each P):
-         the cascade at P = 1, 2, 4, 8 ... ranks (one GPU each; ``--transport loopback`` rehearses P
-         ranks on fewer GPUs and times every solve alone), the single-GPU trainer on the same data,
-         and the reference's Table 3 / 4 layout (time, speed-ups, rounds, #SV, accuracy per P)
+scale    the rank-count sweep of code/mpi_svm2.sh / mpi_svm3.sh (``mpirun -np P`` for each P), for
+         every training size of ``--sizes`` (default 60000 and 1000000): the N-GPU trainer at P = 1,
+         2, 4, 8 ... ranks (one GPU each; ``--transport loopback`` rehearses P ranks on fewer GPUs
+         and times every rank's device work alone, so the critical path of P GPUs is measured) --
+         ``--trainer decomp`` (default): the distributed decomposition solver, bit-identical to one
+         GPU; ``--trainer cascade``: the reference's Cascade SVM (``--topology star|tree``) -- next to
+         the single-GPU trainer on the same data, in the reference's Table 3 / 4 layout
 
 multiclass  all-digit one-vs-rest (models/multiclass.py): one shared Gram per GPU, class solves
          concurrent on streams; ``--gpus P`` deals the classes over P ranks (torchrun, RCCL).
@@ -219,39 +222,41 @@ REF_SERIAL_60K_S = 3285.662
 def _scale(argv) -> int:
     ap = argparse.ArgumentParser(prog="svm355 scale", description="mpi_svm2.sh / mpi_svm3.sh over rank counts")
     ap.add_argument("--ranks", default="1,2,4,8", help="comma-separated rank counts P")
+    ap.add_argument("--trainer", choices=["decomp", "cascade"], default="decomp",
+                    help="the distributed decomposition solver (default; the one-GPU trainer's trajectory on P "
+                         "GPUs) or the reference's Cascade SVM")
     ap.add_argument("--topology", choices=["star", "tree"], default="star")
-    ap.add_argument("--synthetic", default="60000,10000", help="N[,M]: MNIST-shaped synthetic data")
-    ap.add_argument("--train", default=None, help="reference CSV (instead of --synthetic)")
+    ap.add_argument("--sizes", default="60000,1000000", help="comma-separated training sizes N (synthetic)")
+    ap.add_argument("--synthetic", default=None, help="N[,M]: one MNIST-shaped synthetic size (overrides --sizes)")
+    ap.add_argument("--test-rows", type=int, default=10000)
+    ap.add_argument("--train", default=None, help="reference CSV (instead of synthetic data)")
     ap.add_argument("--test", default=None)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu", action="store_true", help="CPU thread-ranks on the native oracle")
     ap.add_argument("--transport", choices=["auto", "rccl", "loopback"], default="auto",
                     help="rccl: one GPU per rank (P > visible GPUs is skipped); loopback: P ranks share the "
-                         "visible GPUs and every solve is also timed alone (critical-path estimate)")
+                         "visible GPUs and every rank's device work is also timed alone (critical path)")
     ap.add_argument("--repeats", type=int, default=3, help="timed fits per P (median reported)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--comm-timeout", type=float, default=120.0)
-    ap.add_argument("--json", default=None, help="write the per-P rows to this file")
+    ap.add_argument("--json", default=None, help="write the per-size, per-P rows to this file")
     a = ap.parse_args(argv)
     ranks = [int(v) for v in a.ranks.split(",")]
     if a.transport == "loopback" and not a.cpu:
         os.environ["SVM355_CASCADE_SERIAL_SOLVES"] = "1"  # read when the rank backends are created
+    if a.cpu and a.trainer == "decomp":
+        print("svm355 scale: the CPU oracle of the decomposition holds an n x n kernel matrix; use "
+              "--trainer cascade with --cpu", file=sys.stderr)
+        return 2
 
     import numpy as np
 
     from .models.svc import SVC
     from .parallel.cascade import CascadeSVM, critical_path
+    from .parallel.decomp import DistributedDecompSVC
     from .utils.config import SVMParams, default_threads
     from .utils.data import load_csv, synthetic_mnist
 
-    if a.train:
-        tr = load_csv(a.train)
-        te = load_csv(a.test) if a.test else None
-    else:
-        parts = a.synthetic.split(",")
-        n, m = int(parts[0]), int(parts[1]) if len(parts) > 1 else 10000
-        tr, te = synthetic_mnist(n, seed=a.seed), synthetic_mnist(m, seed=a.seed, offset=n)
-    X = tr.X if a.cpu else tr.compact().X  # pixels travel as uint8, widened on the device
     ndev = 0
     if not a.cpu:
         import torch
@@ -271,61 +276,92 @@ def _scale(argv) -> int:
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts))
 
-    # the single-device baseline: the GPU trainer (cuda:0) or the serial oracle
-    base_dev = "cpu" if a.cpu else "cuda:0"
-    single = SVC(device=base_dev)
-    t_single = timed(lambda: single.fit(X, tr.y))
-    rows = []
+    if a.train:
+        datasets = [(load_csv(a.train), load_csv(a.test) if a.test else None)]
+    else:
+        if a.synthetic:
+            parts = a.synthetic.split(",")
+            sizes, m = [int(parts[0])], int(parts[1]) if len(parts) > 1 else a.test_rows
+        else:
+            sizes, m = [int(v) for v in a.sizes.split(",")], a.test_rows
+        datasets = [(synthetic_mnist(n, seed=a.seed), synthetic_mnist(m, seed=a.seed, offset=n)) for n in sizes]
     from .parallel.rccl import DeviceGroup
 
-    for P in ranks:
-        if not a.cpu and a.transport in ("auto", "rccl") and P > ndev:
-            print(f"svm355 scale: P = {P} needs {P} GPUs ({ndev} visible), skipped "
-                  "(--transport loopback rehearses it on the visible GPUs)", file=sys.stderr)
-            continue
-        if a.topology == "tree" and P & (P - 1):
-            print(f"svm355 scale: the tree cascade needs a power-of-2 P, {P} skipped", file=sys.stderr)
-            continue
-        threads = max(1, default_threads() // P) if a.cpu else default_threads()
-        model = CascadeSVM(SVMParams(n_threads=threads), topology=a.topology, comm_timeout_s=a.comm_timeout)
-        group = None if a.cpu else DeviceGroup(P, a.transport, a.comm_timeout)
-        try:
-            t = timed(lambda: model.fit(X, tr.y, world=P, device="cpu" if a.cpu else "cuda", group=group))
-        finally:
-            if group is not None:
-                group.close()
-        r = model.result
-        _, crit_ms = critical_path(r.solves, a.topology)
-        ref = REF_CASCADE_S[a.topology].get(P)
-        row = {"P": P, "train_s": round(t, 6), "driver_train_ms": round(r.train_ms, 3),
-               "critical_path_solve_ms": crit_ms,
-               "critical_path_basis": "solo device time per solve" if any(s.get("solo_ms", -1.0) >= 0 for s in r.solves)
-               else "wall time per solve",
-               "speedup_vs_single": round(t_single / t, 4), "efficiency_vs_single": round(t_single / t / P, 4),
-               "rounds": r.rounds, "converged": r.converged, "n_sv": int(len(r.ids)), "b": r.b,
-               "rank0_smo_iterations": int(sum(s["iterations"] for s in r.solves if s["rank"] == 0)),
-               "accuracy": model.score(te.X, te.y) if te is not None and te.n else None,
-               "transport": r.transport}
-        if ref and tr.n == 60000:
-            row["speedup_vs_ref_cascade_same_P"] = round(ref / t, 2)
-        if tr.n == 60000:
-            row["speedup_vs_ref_serial"] = round(REF_SERIAL_60K_S / t, 2)
-        rows.append(row)
-    acc1 = single.score(te.X, te.y) if te is not None and te.n else None
-    print(f"single {'CPU oracle' if a.cpu else 'GPU trainer'}: {t_single:.4f} s, {single.n_iter_} iterations, "
-          f"{len(single.support_)} SVs, accuracy {acc1}")
-    print(f"{'P':>3} {'train (s)':>10} {'crit. path (s)':>15} {'vs single':>10} {'efficiency':>11} {'rounds':>7} "
-          f"{'#SV':>6} {'rank-0 it':>10} {'accuracy':>9}")
-    for r in rows:
-        acc = f"{r['accuracy']:.4f}" if r["accuracy"] is not None else "-"
-        print(f"{r['P']:>3} {r['train_s']:>10.4f} {r['critical_path_solve_ms'] / 1e3:>15.4f} "
-              f"{r['speedup_vs_single']:>10.3f} {r['efficiency_vs_single']:>11.3f} {r['rounds']:>7} {r['n_sv']:>6} "
-              f"{r['rank0_smo_iterations']:>10} {acc:>9}")
+    out_sizes = []
+    for tr, te in datasets:
+        X = tr.X if a.cpu else tr.compact().X  # pixels travel as uint8, widened on the device
+        # the single-device baseline: the GPU trainer (cuda:0) or the serial oracle
+        base_dev = "cpu" if a.cpu else "cuda:0"
+        single = SVC(device=base_dev)
+        t_single = timed(lambda: single.fit(X, tr.y))
+        rows = []
+        for P in ranks:
+            if not a.cpu and a.transport in ("auto", "rccl") and P > ndev:
+                print(f"svm355 scale: P = {P} needs {P} GPUs ({ndev} visible), skipped "
+                      "(--transport loopback rehearses it on the visible GPUs)", file=sys.stderr)
+                continue
+            if a.trainer == "cascade" and a.topology == "tree" and P & (P - 1):
+                print(f"svm355 scale: the tree cascade needs a power-of-2 P, {P} skipped", file=sys.stderr)
+                continue
+            group = None if a.cpu else DeviceGroup(P, a.transport, a.comm_timeout)
+            try:
+                if a.trainer == "decomp":
+                    model = DistributedDecompSVC(P, group=group)
+                    t = timed(lambda: model.fit(X, tr.y))
+                    solo = model.solo_
+                    row = {"P": P, "train_s": round(t, 6), "outer_iterations": model.stats_["outer_iterations"],
+                           "iterations": int(model.n_iter_), "n_sv": int(len(model.support_)), "b": model.b_,
+                           "bit_identical_to_1gpu": bool(model.n_iter_ == single.n_iter_ and model.b_ == single.b_
+                                                         and np.array_equal(model.alpha_, single.alpha_)),
+                           "critical_path_solve_ms": solo["critical_path_ms"] if solo else None,
+                           "critical_path_basis": "solo device time per rank segment" if solo else None,
+                           "solo": solo, "accuracy": model.score(te.X, te.y) if te is not None and te.n else None,
+                           "transport": group.transport if group is not None else "cpu"}
+                else:
+                    threads = max(1, default_threads() // P) if a.cpu else default_threads()
+                    model = CascadeSVM(SVMParams(n_threads=threads), topology=a.topology,
+                                       comm_timeout_s=a.comm_timeout)
+                    t = timed(lambda: model.fit(X, tr.y, world=P, device="cpu" if a.cpu else "cuda", group=group))
+                    r = model.result
+                    _, crit_ms = critical_path(r.solves, a.topology)
+                    row = {"P": P, "train_s": round(t, 6), "driver_train_ms": round(r.train_ms, 3),
+                           "critical_path_solve_ms": crit_ms,
+                           "critical_path_basis": "solo device time per solve"
+                           if any(s.get("solo_ms", -1.0) >= 0 for s in r.solves) else "wall time per solve",
+                           "rounds": r.rounds, "converged": r.converged, "n_sv": int(len(r.ids)), "b": r.b,
+                           "rank0_smo_iterations": int(sum(s["iterations"] for s in r.solves if s["rank"] == 0)),
+                           "accuracy": model.score(te.X, te.y) if te is not None and te.n else None,
+                           "transport": r.transport}
+                    ref = REF_CASCADE_S[a.topology].get(P)
+                    if ref and tr.n == 60000:
+                        row["speedup_vs_ref_cascade_same_P"] = round(ref / t, 2)
+            finally:
+                if group is not None:
+                    group.close()
+            eff_t = row["critical_path_solve_ms"] / 1e3 if (a.transport == "loopback" and row["critical_path_solve_ms"]) \
+                else t
+            row.update(speedup_vs_single=round(t_single / eff_t, 4), efficiency_vs_single=round(t_single / eff_t / P, 4))
+            if tr.n == 60000:
+                row["speedup_vs_ref_serial"] = round(REF_SERIAL_60K_S / eff_t, 2)
+            rows.append(row)
+        acc1 = single.score(te.X, te.y) if te is not None and te.n else None
+        what = "distributed decomposition" if a.trainer == "decomp" else f"{a.topology} cascade"
+        print(f"n = {tr.n}: single {'CPU oracle' if a.cpu else 'GPU trainer'}: {t_single:.4f} s, {single.n_iter_} "
+              f"iterations, {len(single.support_)} SVs, accuracy {acc1}; {what} per P "
+              f"({'speed-ups from the solo-timed critical path' if a.transport == 'loopback' else 'wall time'}):")
+        print(f"{'P':>3} {'train (s)':>10} {'crit. path (s)':>15} {'vs single':>10} {'efficiency':>11} {'#SV':>6} "
+              f"{'accuracy':>9}")
+        for r in rows:
+            acc = f"{r['accuracy']:.4f}" if r["accuracy"] is not None else "-"
+            cp = f"{r['critical_path_solve_ms'] / 1e3:.4f}" if r["critical_path_solve_ms"] else "-"
+            print(f"{r['P']:>3} {r['train_s']:>10.4f} {cp:>15} {r['speedup_vs_single']:>10.3f} "
+                  f"{r['efficiency_vs_single']:>11.3f} {r['n_sv']:>6} {acc:>9}")
+        out_sizes.append({"n": tr.n, "single_s": t_single, "single_iterations": int(single.n_iter_),
+                          "single_n_sv": int(len(single.support_)), "single_accuracy": acc1, "rows": rows})
     if a.json:
         Path(a.json).write_text(json.dumps({
-            "program": f"svm355 scale ({a.topology})", "n": tr.n, "single_s": t_single,
-            "single_iterations": int(single.n_iter_), "single_n_sv": int(len(single.support_)),
-            "single_accuracy": acc1, "device": base_dev, "transport": a.transport, "rows": rows}) + "\n")
+            "program": f"svm355 scale ({a.trainer if a.trainer == 'decomp' else a.topology + ' cascade'})",
+            "device": "cpu" if a.cpu else "cuda:0", "transport": a.transport, "sizes": out_sizes}) + "\n")
     return 0
 
 

@@ -28,6 +28,25 @@ svm_params resolve(const svm_params* p) {
 
 }  // namespace
 
+namespace svm355 {
+int tu_warm_capi(hipStream_t s);
+int tu_warm_cascade_dev(hipStream_t s);
+int tu_warm_decomp(hipStream_t s);
+int tu_warm_dsmo(hipStream_t s);
+int tu_warm_gram_mfma(hipStream_t s);
+int tu_warm_igram(hipStream_t s);
+int tu_warm_prep_kernels(hipStream_t s);
+int tu_warm_rowcache(hipStream_t s);
+int tu_warm_smo(hipStream_t s);
+int tu_warm_all(hipStream_t s) {
+  int bad = 0;
+  for (auto fn : {tu_warm_capi, tu_warm_cascade_dev, tu_warm_decomp, tu_warm_dsmo, tu_warm_gram_mfma, tu_warm_igram,
+                  tu_warm_prep_kernels, tu_warm_rowcache, tu_warm_smo})
+    bad |= fn(s);
+  return bad;
+}
+}  // namespace svm355
+
 extern "C" {
 
 SVM_API int64_t svmd_padded_dim(int64_t d) { return padded_dim(d); }
@@ -81,11 +100,6 @@ SVM_API int svmd_memcpy_d2h(void* h, void* dst_h, const void* src_d, int64_t byt
 
 SVM_API void svmd_destroy(void* h);
 
-namespace {
-__global__ void module_warm_kernel(int* p) {
-  if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
-}
-}  // namespace
 
 SVM_API void* svmd_create(int32_t device) {
   if (hipSetDevice(device) != hipSuccess) {
@@ -103,10 +117,10 @@ SVM_API void* svmd_create(int32_t device) {
     delete ctx;
     return nullptr;
   }
-  // Pay the one-time costs here, not inside the first solve: load this library's code object (one
-  // launch), and allocate the pinned state block and a small solver workspace (grown on demand).
-  hipLaunchKernelGGL(module_warm_kernel, dim3(1), dim3(64), 0, ctx->stream, nullptr);
-  if (hipGetLastError() != hipSuccess || ctx->ensure_pinned(size_t(1) << 16) != SVM_OK ||
+  // Pay the one-time costs here, not inside the first solve: load every code object of the library
+  // (one launch per translation unit), and allocate the pinned state block and a small solver
+  // workspace (grown on demand).
+  if (tu_warm_all(ctx->stream) != 0 || hipGetLastError() != hipSuccess || ctx->ensure_pinned(size_t(1) << 16) != SVM_OK ||
       ctx->ensure_ws(size_t(16) << 20) != SVM_OK || hipStreamSynchronize(ctx->stream) != hipSuccess) {
     set_error("svmd_create: warm-up on device %d failed", device);
     svmd_destroy(ctx);
@@ -709,3 +723,5 @@ SVM_API void svmd_trace_push(const char* name) { roctxRangePushA(name ? name : "
 SVM_API void svmd_trace_pop(void) { roctxRangePop(); }
 
 }  // extern "C"
+
+SVMD_TU_WARM(capi)

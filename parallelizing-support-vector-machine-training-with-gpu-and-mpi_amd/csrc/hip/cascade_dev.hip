@@ -779,6 +779,10 @@ struct Group {
   std::vector<std::unique_ptr<RcclTransport>> rtr;  // persistent (pinned / device scratch)
   std::unique_ptr<RankPool> pool;                   // one persistent host thread per rank
   std::mutex mu;  // one fit at a time
+  // loopback rehearsal with SVM355_CASCADE_SERIAL_SOLVES=1: the distributed decomposition's per-rank
+  // solo segment times (DecompSolo) and their summary (svmd_cascade_group_decomp_solo)
+  std::mutex solo_mu;
+  std::vector<double> solo_report;
 };
 
 // ----------------------------------------------------------------------------- process rank
@@ -839,7 +843,7 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
 // all-gathered through `tr` (null: one GPU).  alpha_out (host, n doubles) may be null.
 void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
                     const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
-                    double* mm_out) {
+                    double* mm_out, DecompSolo* solo = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
   auto check = [](int rc, const char* what) {
     if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
@@ -878,6 +882,7 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   DecompOpts o;
   o.world = world;
   o.rank = rank;
+  o.solo = solo;
   if (tr)
     o.allgather = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
                    [tr](void* ev) { return tr->event_wait(ev, "decomposition SMO: a batch of outer iterations"); }};
@@ -1118,6 +1123,10 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
     }
   }
   std::vector<double> ms(static_cast<size_t>(P), 0.0);
+  const char* serial = getenv("SVM355_CASCADE_SERIAL_SOLVES");
+  std::vector<DecompSolo> solo(static_cast<size_t>(serial && atoi(serial) != 0 && !g->rccl && P > 1 ? P : 0));
+  for (auto& sr : solo) sr.mu = &g->solo_mu;
+  g->solo_report.clear();
   try {
     g->pool->run(
         token,
@@ -1125,7 +1134,7 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
           if (hipSetDevice(g->devices[size_t(rr)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
           decomp_on_rank(*g->be[size_t(rr)], P > 1 ? tr[size_t(rr)] : nullptr, X, y, n, d, p, q,
                          rr == 0 ? alpha_out : nullptr, rr == 0 ? r : nullptr, rr == 0 ? stats : nullptr,
-                         &ms[size_t(rr)], rr == 0 ? mm_out : nullptr);
+                         &ms[size_t(rr)], rr == 0 ? mm_out : nullptr, solo.empty() ? nullptr : &solo[size_t(rr)]);
         },
         [&](int rr) {
           (void)hipSetDevice(g->devices[size_t(rr)]);
@@ -1138,7 +1147,43 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
   }
   if (rank_ms)
     for (int rr = 0; rr < P; ++rr) rank_ms[rr] = ms[size_t(rr)];
+  if (!solo.empty()) {
+    // critical path of P GPUs: per outer iteration the slowest rank's selection, then the slowest
+    // rank's rest (the ranks meet at the candidate all-gather in between); exchanges excluded
+    size_t iters = solo[0].sel_ms.size();
+    for (const auto& sr : solo) iters = std::min({iters, sr.sel_ms.size(), sr.rest_ms.size()});
+    double sel = 0.0, rest = 0.0;
+    for (size_t k = 0; k < iters; ++k) {
+      double ms_sel = 0.0, ms_rest = 0.0;
+      for (const auto& sr : solo) {
+        ms_sel = std::max(ms_sel, sr.sel_ms[k]);
+        ms_rest = std::max(ms_rest, sr.rest_ms[k]);
+      }
+      sel += ms_sel;
+      rest += ms_rest;
+    }
+    g->solo_report = {sel + rest, sel, rest, double(iters)};
+    for (const auto& sr : solo) {  // then per rank: its own selection and rest totals
+      double a = 0.0, b = 0.0;
+      for (double v : sr.sel_ms) a += v;
+      for (double v : sr.rest_ms) b += v;
+      g->solo_report.push_back(a);
+      g->solo_report.push_back(b);
+    }
+  }
   return SVM_OK;
+}
+
+// The last distributed decomposition fit's solo timing on a loopback rehearsal (SVM355_CASCADE_SERIAL_SOLVES=1):
+// out = [critical path ms, of it selection ms, of it the rest ms, outer iterations, then per rank: its
+// selection ms, its rest ms]; returns the number of values (0: the last fit was not timed solo).
+SVM_API int64_t svmd_cascade_group_decomp_solo(void* h, double* out, int64_t cap) {
+  auto* g = static_cast<Group*>(h);
+  if (!g) return 0;
+  std::lock_guard<std::mutex> lk(g->mu);
+  const int64_t k = std::min<int64_t>(cap, int64_t(g->solo_report.size()));
+  for (int64_t i = 0; i < k; ++i) out[i] = g->solo_report[size_t(i)];
+  return int64_t(g->solo_report.size());
 }
 
 // One process rank of the distributed decomposition SMO (every rank passes all n rows and labels).
@@ -1339,3 +1384,5 @@ SVM_API int svmd_cascade_rank_barrier(void* h) {
 }
 
 }  // extern "C"
+
+SVMD_TU_WARM(cascade_dev)

@@ -122,6 +122,9 @@ struct DeviceCtx {
     return SVM_ERR_ARG;                                          \
   }
 
+// Load every translation unit's code object on s (hip_util.h SVMD_TU_WARM): svmd_create.
+int tu_warm_all(hipStream_t s);
+
 // Kernel launchers implemented in the .hip translation units (all enqueue on `s`).
 int launch_widen_u8(hipStream_t s, const uint8_t* src, int64_t n, int64_t d, int64_t ld, double* dst);
 int launch_minmax(hipStream_t s, const double* X, int64_t n, int64_t d, int64_t ld, double* mn,

@@ -4,6 +4,8 @@
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <mutex>
+#include <vector>
 
 #include "ctx.h"
 
@@ -28,6 +30,16 @@ struct DecompAllGather {
   explicit operator bool() const { return bool(gather); }
 };
 
+// One-GPU rehearsal of P ranks with every rank's device work timed alone (SVM355_CASCADE_SERIAL_SOLVES=1,
+// as the cascade rehearsal's solves): the ranks sharing the device take `mu` around each of their two
+// device segments per outer iteration -- the selection (before the candidate all-gather) and the rest
+// (build, K(W, W), inner solve, f update) -- and time them with events, so the P-GPU critical path is
+// sum over outer iterations of max over ranks of each segment (exchanges excluded).
+struct DecompSolo {
+  std::mutex* mu = nullptr;
+  std::vector<double> sel_ms, rest_ms;  // per outer iteration of this rank
+};
+
 // How a solve runs beyond its problem: the distributed form (world > 1: this GPU's rank and the
 // candidate all-gather), a warm start (alpha holds the start; f = K (alpha y) - y over its nonzero
 // entries), and an optional per-outer-iteration trace (tests; one GPU only, one synchronisation per
@@ -37,6 +49,7 @@ struct DecompOpts {
   DecompAllGather allgather;
   bool warm = false;
   svm_decomp_trace* trace = nullptr;
+  DecompSolo* solo = nullptr;  // world > 1 rehearsal on one GPU: per-rank solo timing (above)
 };
 
 // The rows a solve reads its kernel values from: the exact-integer plan's quantised rows (Q; int8

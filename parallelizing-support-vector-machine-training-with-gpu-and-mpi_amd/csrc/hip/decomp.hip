@@ -1385,6 +1385,36 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     SVM_WS_INNER_(NT, PER, false, true);     \
   else                                       \
     SVM_WS_INNER_(NT, PER, false, false)
+  // solo timing (DecompSolo): the two device segments of an outer iteration under the shared mutex,
+  // each timed alone and waited for before the mutex is released
+  DecompSolo* solo = (world > 1 && !tr) ? o.solo : nullptr;
+  hipEvent_t sev[4] = {nullptr, nullptr, nullptr, nullptr};
+  struct SoloEvents {
+    hipEvent_t* e;
+    ~SoloEvents() {
+      for (int i = 0; i < 4; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } sev_guard{sev};
+  if (solo)
+    for (auto& e : sev) SVMD_CHECK(hipEventCreate(&e));
+  std::unique_lock<std::mutex> solo_lk;
+  auto solo_begin = [&](int k) -> int {
+    if (!solo) return SVM_OK;
+    solo_lk = std::unique_lock<std::mutex>(*solo->mu);
+    SVMD_CHECK(hipEventRecord(sev[2 * k], s));
+    return SVM_OK;
+  };
+  auto solo_end = [&](int k) -> int {
+    if (!solo) return SVM_OK;
+    SVMD_CHECK(hipEventRecord(sev[2 * k + 1], s));
+    SVMD_CHECK(hipEventSynchronize(sev[2 * k + 1]));
+    float ms = 0.0f;
+    SVMD_CHECK(hipEventElapsedTime(&ms, sev[2 * k], sev[2 * k + 1]));
+    (k == 0 ? solo->sel_ms : solo->rest_ms).push_back(double(ms));
+    solo_lk.unlock();
+    return SVM_OK;
+  };
   const DecompCtl* fin = nullptr;  // the readback that saw the stop
   DecompCtl* ctl_pub = nullptr;  // ctl_h as the device addresses it
   SVMD_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctl_pub), ctl_h, 0));
@@ -1395,11 +1425,14 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
         set_error("injected failure of rank %d at outer iteration %lld", rank, (long long)fail_outer);
         return SVM_ERR_INTERNAL;
       }
+      if ((rc = solo_begin(0))) return rc;
       if (NBr > 0)
         hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
                            T, p.C, p.eps, cown, cown + NBr * T, ctl);
       SVMD_LAUNCH_CHECK();
+      if ((rc = solo_end(0))) return rc;
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
+      if ((rc = solo_begin(1))) return rc;
       hipLaunchKernelGGL(ws_build_kernel, dim3(1), dim3(kMaxWS), 0, s, call, int(sh.L), int(Lr), int(NBr * T), int(T),
                          p.tau, tau_frac, int64_t(p.max_iter), W, Wf, ctl, mcount, pub);
       SVMD_LAUNCH_CHECK();
@@ -1435,6 +1468,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       SVMD_LAUNCH_CHECK();
       rc = f_update(cols, coef, mcount, bt * batch + bi < 4);
       if (rc) return rc;
+      if ((rc = solo_end(1))) return rc;
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
     }
@@ -1901,3 +1935,5 @@ SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t
 }
 
 }  // extern "C"
+
+SVMD_TU_WARM(decomp)

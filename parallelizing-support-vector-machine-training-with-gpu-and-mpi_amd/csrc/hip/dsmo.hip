@@ -805,3 +805,5 @@ SVM_API int svmd_dsmo_rank_solve(void* h, double* alpha_out, svm_result* r, doub
 }
 
 }  // extern "C"
+
+SVMD_TU_WARM(dsmo)

@@ -306,3 +306,5 @@ int launch_gemv_rows(hipStream_t s, const double* K, int64_t ldk, int64_t m, int
 }
 
 }  // namespace svm355
+
+SVMD_TU_WARM(gram_mfma)

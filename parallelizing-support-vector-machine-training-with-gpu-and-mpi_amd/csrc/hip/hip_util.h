@@ -23,6 +23,23 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
 #define SVMD_LAUNCH_CHECK() SVMD_CHECK(hipGetLastError())
 
+// One trivial kernel per translation unit.  Every .hip file is its own fat binary, and HIP loads a
+// code object at the first launch of any kernel in it: 0.5-9.3 ms per file on MI355X (smo.hip's is the
+// largest), which the first fit paid inside its timed region (profiles/r5_cold_fit_trace.txt).
+// svmd_create launches every file's kernel (tu_warm_all, capi.hip), so no fit loads a code object.
+#define SVMD_TU_WARM(name)                                                                  \
+  namespace svm355 {                                                                        \
+  namespace {                                                                               \
+  __global__ void tu_warm_kernel_##name(int* p) {                                           \
+    if (p && threadIdx.x == 0) *p = 0;                                                      \
+  }                                                                                         \
+  }                                                                                         \
+  int tu_warm_##name(hipStream_t s) {                                                       \
+    hipLaunchKernelGGL(tu_warm_kernel_##name, dim3(1), dim3(64), 0, s, nullptr);            \
+    return hipPeekAtLastError() == hipSuccess ? 0 : 1;                                      \
+  }                                                                                         \
+  }
+
 namespace svm355 {
 
 constexpr int kWave = 64;  // CDNA wavefront width (hard-coded per the gfx950 guide)

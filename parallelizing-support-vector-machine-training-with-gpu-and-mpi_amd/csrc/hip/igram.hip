@@ -1291,3 +1291,5 @@ int launch_igram_slab(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
 }
 
 }  // namespace svm355
+
+SVMD_TU_WARM(igram)

@@ -260,3 +260,5 @@ int launch_gather_rows(hipStream_t s, const double* src, int64_t ld, const int64
 }
 
 }  // namespace svm355
+
+SVMD_TU_WARM(prep_kernels)

@@ -582,3 +582,5 @@ int run_smo_rowcache(DeviceCtx* ctx, const double* X_d, const double* sqn_d, int
 }
 
 }  // namespace svm355
+
+SVMD_TU_WARM(rowcache)

@@ -1293,3 +1293,5 @@ int count_sv(DeviceCtx* ctx, const double* alpha, int64_t n, int64_t rows, doubl
 }
 
 }  // namespace svm355
+
+SVMD_TU_WARM(smo)

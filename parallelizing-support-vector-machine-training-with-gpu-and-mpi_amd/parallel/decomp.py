@@ -97,7 +97,14 @@ def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] =
     """One distributed decomposition solve over a ``DeviceGroup`` (its ranks are this process's
     threads; RCCL or the loopback rehearsal)."""
     lib = N.hip()
-    return _fit_native(lib.svmd_cascade_group_decomp, group.handle, X, y, params or SVMParams(), q, group.world)
+    out = _fit_native(lib.svmd_cascade_group_decomp, group.handle, X, y, params or SVMParams(), q, group.world)
+    buf = np.zeros(4 + 2 * group.world)
+    k = int(lib.svmd_cascade_group_decomp_solo(group.handle, N.ptr(buf), buf.size))
+    if k:  # a loopback rehearsal with SVM355_CASCADE_SERIAL_SOLVES=1: every rank's device work timed alone
+        out["solo"] = {"critical_path_ms": float(buf[0]), "select_ms": float(buf[1]), "rest_ms": float(buf[2]),
+                       "outer_iterations": int(buf[3]),
+                       "rank_select_ms": [float(v) for v in buf[4:k:2]], "rank_rest_ms": [float(v) for v in buf[5:k:2]]}
+    return out
 
 
 def rank_fit(rank, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
@@ -161,6 +168,7 @@ class DistributedDecompSVC:
         self.n_iter_, self.stop_reason_ = out["iterations"], out["stop_reason"]
         self.stats_ = out["stats"]
         self.rank_ms_ = out["rank_ms"]
+        self.solo_ = out.get("solo")  # per-rank solo timing of a one-GPU rehearsal (None otherwise)
         self.timings_ = {"solve_ms": out["stats"]["solve_us"] / 1e3, "native_ms": out["wall_ms"],
                          **out["stats"]}
         self.fit_time_ = time.perf_counter() - t0

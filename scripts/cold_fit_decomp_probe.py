@@ -9,7 +9,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
 from svm355 import SVC  # noqa: E402
 from svm355.ops import device as D  # noqa: E402
 from svm355.utils.data import synthetic_mnist  # noqa: E402

@@ -95,14 +95,23 @@ def test_cli_scale_sweeps_rank_counts(tmp_path, topology):
     """scale = mpi_svm2.sh / mpi_svm3.sh over P: one row per rank count (the tree skips P = 3), the
     single-device baseline, and the same converged model at every P (CPU thread-ranks)."""
     js = tmp_path / "scale.json"
-    out = _run(["scale", "--cpu", "--synthetic", "500,200", "--ranks", "1,2,3,4", "--topology", topology,
-                "--repeats", "1", "--warmup", "0", "--json", str(js)], tmp_path)
+    out = _run(["scale", "--cpu", "--trainer", "cascade", "--synthetic", "500,200", "--ranks", "1,2,3,4",
+                "--topology", topology, "--repeats", "1", "--warmup", "0", "--json", str(js)], tmp_path)
     s = json.loads(js.read_text())
-    assert s["device"] == "cpu" and s["single_n_sv"] > 0
-    rows = s["rows"]
+    assert s["device"] == "cpu" and len(s["sizes"]) == 1 and s["sizes"][0]["n"] == 500
+    sz = s["sizes"][0]
+    assert sz["single_n_sv"] > 0
+    rows = sz["rows"]
     assert [r["P"] for r in rows] == ([1, 2, 3, 4] if topology == "star" else [1, 2, 4])
     for r in rows:
         assert r["converged"] and r["rounds"] >= 1 and r["n_sv"] > 0
         assert r["accuracy"] > 0.9
         assert r["critical_path_solve_ms"] > 0 and r["efficiency_vs_single"] > 0
     assert "efficiency" in out and "single CPU oracle" in out
+
+
+def test_cli_scale_decomp_needs_a_gpu(tmp_path):
+    """The default trainer is the distributed decomposition, which runs on GPUs: --cpu asks for the cascade."""
+    r = subprocess.run([sys.executable, "-m", "svm355", "scale", "--cpu", "--synthetic", "400,100"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "--trainer cascade" in r.stderr

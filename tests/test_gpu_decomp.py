@@ -263,3 +263,31 @@ def test_column_cache_leaves_the_device_to_torch():
     torch.cuda.empty_cache()
     m2 = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)  # the cache is rebuilt on demand
     assert m2.b_ == m.b_
+
+
+def test_scale_cli_decomp_rehearsal_times_every_rank_alone(tmp_path):
+    """``python -m svm355 scale`` (the mpirun -np P sweep) defaults to the distributed decomposition; on
+    one GPU (--transport loopback) every rank's device work per outer iteration is timed alone
+    (SVM355_CASCADE_SERIAL_SOLVES), so each P's critical path is measured, and every P's model is the
+    one-GPU model bit for bit."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    js = tmp_path / "s.json"
+    r = subprocess.run([sys.executable, "-m", "svm355", "scale", "--transport", "loopback", "--ranks", "1,2,4",
+                        "--sizes", "6000", "--test-rows", "500", "--repeats", "1", "--warmup", "0", "--json", str(js)],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    s = json.loads(js.read_text())
+    rows = s["sizes"][0]["rows"]
+    assert [x["P"] for x in rows] == [1, 2, 4]
+    for x in rows:
+        assert x["bit_identical_to_1gpu"] is True
+    for x in rows[1:]:
+        solo = x["solo"]
+        assert solo and solo["outer_iterations"] >= 1 and len(solo["rank_select_ms"]) == x["P"]
+        assert 0 < solo["select_ms"] + solo["rest_ms"] == pytest.approx(solo["critical_path_ms"])
+        assert x["critical_path_solve_ms"] == solo["critical_path_ms"]
