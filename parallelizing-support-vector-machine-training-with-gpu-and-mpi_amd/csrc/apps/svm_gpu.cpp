@@ -73,6 +73,13 @@ int main(int argc, char** argv) {
   auto* alpha = static_cast<double*>(dev.alloc(n * 8));
   CK(svmd_synchronize(dev.ctx));
 
+  // --solver auto resolves as SVC(solver="auto"): the decomposition, unless a pairwise-only knob was asked
+  // for (a forced Gram path or second-order pair selection), which then selects the pairwise SMO
+  if (o.solver == 2 && (o.gram_mode != 0 || o.p.wss == 2)) o.solver = 0;
+  if (o.solver == 1 && (o.gram_mode != 0 || o.p.wss == 2)) {
+    fprintf(stderr, "svm_gpu: --gram and --wss second apply to the pairwise SMO (--solver smo)\n");
+    return 2;
+  }
   svm_result r{};
   svmd_timing tm{};
   int32_t int_gram = 0;

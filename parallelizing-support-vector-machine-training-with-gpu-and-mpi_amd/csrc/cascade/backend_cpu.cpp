@@ -84,13 +84,24 @@ class CpuBackend final : public Backend {
   void record_ids(const double* rec, int64_t k, int64_t ld, int64_t* ids) override {
     for (int64_t i = 0; i < k; ++i) ids[i] = int64_t(rec[i * (ld + 3) + ld + 2]);
   }
+  static constexpr double kDenseKBudget = 4.0 * (1ull << 30);  // bytes of one solve's dense kernel matrix
   SolveStats solve(DSet& S, int64_t d, const svm_params& p, const double*, const double*, int solver,
                    int64_t) override {
     svm_result r{};
+    // the decomposition oracle holds the set's dense k x k kernel matrix: above the budget (a 60k
+    // single-rank set would need 28.8 GB) the solve streams rows with the pairwise oracle instead, and
+    // the log says so (solver 0)
+    if (solver == 1 && S.k >= 2 && double(S.k) * double(S.k) * 8.0 > kDenseKBudget) solver = 0;
     if (solver == 1 && S.k >= 2) {
       // the decomposition oracle (decomp_cpu.cpp) on the set's kernel matrix (the reference's direct
       // RBF, svm_rbf_matrix), warm started from S.a
-      std::vector<double> K(size_t(S.k) * size_t(S.k));
+      std::vector<double> K;
+      try {
+        K.resize(size_t(S.k) * size_t(S.k));
+      } catch (const std::bad_alloc&) {
+        throw CascadeError("CPU backend: no memory for the " + std::to_string(S.k) + " x " + std::to_string(S.k) +
+                           " kernel matrix of a decomposition solve");
+      }
       check(svm_rbf_matrix(S.X.as<double>(), S.k, S.X.as<double>(), S.k, d, p.gamma, K.data(), p.n_threads),
             "svm_rbf_matrix");
       int64_t ds[8] = {};

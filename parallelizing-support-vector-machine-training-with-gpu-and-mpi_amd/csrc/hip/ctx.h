@@ -173,9 +173,10 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
                       int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                       const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m, const QuantPlan& P,
                       double gamma, double* part, int64_t ldp);
-bool launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
-                     int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
-                     int64_t ldk, const int32_t* gate);
+// K(W, W) through the narrow column store; *launched = false (SVM_OK) when its shape limits do not apply.
+int launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
+                    int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
+                    int64_t ldk, const int32_t* gate, bool* launched);
 int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                           int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                           const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,

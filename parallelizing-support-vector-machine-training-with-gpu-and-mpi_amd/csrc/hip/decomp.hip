@@ -1441,8 +1441,11 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                            WNw);
         SVMD_LAUNCH_CHECK();
         // K(W, W) over the full capacity (rows beyond m are never read); skipped once stopped
-        if (!(kww_narrow && launch_igram_ww(s, Qw, N0w, WNw, stw, kMaxWS, wid, wid + kMaxWS, P, p.gamma, Kw, ldw,
-                                            gate))) {
+        bool ww = false;
+        if (kww_narrow && (rc = launch_igram_ww(s, Qw, N0w, WNw, stw, kMaxWS, wid, wid + kMaxWS, P, p.gamma, Kw, ldw,
+                                                gate, &ww)))
+          return rc;
+        if (!ww) {
           rc = launch_igram_sym(s, Qw, N0w, WNw, const_cast<double*>(stw), kMaxWS, P, p.gamma, Kw, ldw, false, gate);
           if (rc) return rc;
         }
@@ -1666,6 +1669,16 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
     }
   }
   if (ld % 16 != 0 || ld < d || o.world != 1) return SVM_OK;  // the FP64 block kernel's k-steps
+  // The FP64-row solve keeps the moved columns' block K(rows, <= 1024 columns) per f update: n x 1024
+  // doubles of workspace (8 GB at 1M rows).  When that does not fit 80 % of what the device has free
+  // (plus the context's current workspace, which it would replace), nothing runs (*used = false) and
+  // the caller takes the pairwise solver (SVC(solver="auto")).
+  {
+    size_t free_b = 0, total_b = 0;
+    SVMD_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const double need = double(n) * double(kMaxWS) * 8.0 + double(size_t(kMaxWS) * ld * 16);
+    if (need > 0.8 * double(free_b + ctx->ws_bytes)) return SVM_OK;
+  }
   // FP64 rows: their squared norms in the context's grow-only buffer, then the solve
   const size_t need = size_t(n) * 8;
   if (need > ctx->gram_bytes) {

@@ -1237,10 +1237,11 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
 // workgroups for 1,024 rows where the triangular Gram launch has 72, and the same kernel values bit
 // for bit.  ids: the identity 0 .. n-1 on the device (columns k at K + k * ldk; K(W, W) is symmetric,
 // so that is also its row k); the diagonal is 1 (local row == column).  false when kq is too wide.
-bool launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
-                     int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
-                     int64_t ldk, const int32_t* gate) {
-  if (P.kq > kNarrowMaxKq || n <= 0 || n > 32 * 65535) return false;
+int launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
+                    int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
+                    int64_t ldk, const int32_t* gate, bool* launched) {
+  *launched = false;
+  if (P.kq > kNarrowMaxKq || n <= 0 || n > 32 * 65535) return SVM_OK;  // not applicable: the caller's fallback
   int kused = 0;
   for (int k = int(P.perm.size()) - 1; k >= 0; --k)
     if (P.perm[k] >= 0) {
@@ -1256,7 +1257,9 @@ bool launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const 
   else
     hipLaunchKernelGGL(igram_colstore_narrow_kernel<false>, grid, dim3(256), lds, s, Qw, n, P.kq, P.main0, N0w, WNw,
                        stw, P.w0, -gamma, Qw, N0w, WNw, ids, ids, count, int64_t(0), K, ldk, kused, gate, true);
-  return hipGetLastError() == hipSuccess;
+  SVMD_LAUNCH_CHECK();  // a launch error (or one an earlier kernel left) is reported, never a silent fallback
+  *launched = true;
+  return SVM_OK;
 }
 
 // K(rows [0, n), rows [col0, col0 + ncols)) of already quantised rows (Q, N0, WN; step weights

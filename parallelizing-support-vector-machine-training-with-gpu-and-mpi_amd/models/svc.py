@@ -154,13 +154,16 @@ class SVC:
             alpha = torch.empty(X.shape[0], dtype=torch.float64, device=device)  # the cold start zeroes it
         torch.cuda.synchronize(device)
         t1 = time.perf_counter()
+        out = None
         if decomp:
             out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set,
                                       warm=alpha0 is not None)
-            if out is None:
-                raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16")
+            if out is None and self.solver == "decomp":
+                raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16, or the FP64-row "
+                                 "solve's workspace (n x 1024 doubles) does not fit the device")
+        if out is not None:
             res, tm = out
-        else:
+        else:  # the pairwise solver (also solver="auto" when the decomposition's workspace does not fit)
             res, tm = D.train(Xd, sqn, yd, alpha, self.params, warm=alpha0 is not None, mn=mn, mx=mx, gram=self.gram,
                               kcache=self.kcache)
         a = alpha.cpu().numpy()
