@@ -513,6 +513,7 @@ def main(argv=None):
     elif mode == "decomp":
         extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
                  "stop_reason": model.stop_reason_, "decomp_stats": model.stats_, "rank_ms": model.rank_ms_,
+                 "rank_host_wait_ms": getattr(model, "host_wait_ms_", None),
                  "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
                  "launch_form": ("one rank per process" + (" (CPU oracle over gloo)" if cpu else
                                                            f" over gloo, host-staged ({a.gpus} processes on "

@@ -783,6 +783,7 @@ struct Group {
   // solo segment times (DecompSolo) and their summary (svmd_cascade_group_decomp_solo)
   std::mutex solo_mu;
   std::vector<double> solo_report;
+  std::vector<double> host_wait_ms;  // the last distributed decomposition fit's per-rank host wait
 };
 
 // ----------------------------------------------------------------------------- process rank
@@ -843,7 +844,7 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
 // all-gathered through `tr` (null: one GPU).  alpha_out (host, n doubles) may be null.
 void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
                     const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
-                    double* mm_out, DecompSolo* solo = nullptr) {
+                    double* mm_out, DecompSolo* solo = nullptr, double* host_wait_ms = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
   auto check = [](int rc, const char* what) {
     if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
@@ -883,6 +884,7 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   o.world = world;
   o.rank = rank;
   o.solo = solo;
+  o.host_wait_ms = host_wait_ms;
   if (tr)
     o.allgather = {[tr](const void* send, int64_t bytes, void* recv) { tr->allgather_async(send, bytes, recv); },
                    [tr](void* ev) { return tr->event_wait(ev, "decomposition SMO: a batch of outer iterations"); }};
@@ -1127,6 +1129,7 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
   std::vector<DecompSolo> solo(static_cast<size_t>(serial && atoi(serial) != 0 && !g->rccl && P > 1 ? P : 0));
   for (auto& sr : solo) sr.mu = &g->solo_mu;
   g->solo_report.clear();
+  g->host_wait_ms.assign(size_t(P), 0.0);
   try {
     g->pool->run(
         token,
@@ -1134,7 +1137,8 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
           if (hipSetDevice(g->devices[size_t(rr)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
           decomp_on_rank(*g->be[size_t(rr)], P > 1 ? tr[size_t(rr)] : nullptr, X, y, n, d, p, q,
                          rr == 0 ? alpha_out : nullptr, rr == 0 ? r : nullptr, rr == 0 ? stats : nullptr,
-                         &ms[size_t(rr)], rr == 0 ? mm_out : nullptr, solo.empty() ? nullptr : &solo[size_t(rr)]);
+                         &ms[size_t(rr)], rr == 0 ? mm_out : nullptr, solo.empty() ? nullptr : &solo[size_t(rr)],
+                         &g->host_wait_ms[size_t(rr)]);
         },
         [&](int rr) {
           (void)hipSetDevice(g->devices[size_t(rr)]);
@@ -1172,6 +1176,17 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
     }
   }
   return SVM_OK;
+}
+
+// The last distributed decomposition fit's host time per rank blocked in the per-batch waits (the one
+// wait per outer iteration: RCCL's event poll under the deadline, or hipEventSynchronize); returns P.
+SVM_API int64_t svmd_cascade_group_decomp_waits(void* h, double* out, int64_t cap) {
+  auto* g = static_cast<Group*>(h);
+  if (!g) return 0;
+  std::lock_guard<std::mutex> lk(g->mu);
+  const int64_t k = std::min<int64_t>(cap, int64_t(g->host_wait_ms.size()));
+  for (int64_t i = 0; i < k; ++i) out[i] = g->host_wait_ms[size_t(i)];
+  return int64_t(g->host_wait_ms.size());
 }
 
 // The last distributed decomposition fit's solo timing on a loopback rehearsal (SVM355_CASCADE_SERIAL_SOLVES=1):

@@ -50,6 +50,7 @@ struct DecompOpts {
   bool warm = false;
   svm_decomp_trace* trace = nullptr;
   DecompSolo* solo = nullptr;  // world > 1 rehearsal on one GPU: per-rank solo timing (above)
+  double* host_wait_ms = nullptr;  // out: host time blocked in the per-batch waits (all outer iterations)
 };
 
 // The rows a solve reads its kernel values from: the exact-integer plan's quantised rows (Q; int8

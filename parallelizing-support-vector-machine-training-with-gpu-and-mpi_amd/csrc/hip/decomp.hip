@@ -1520,7 +1520,9 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     if (bt == 0) continue;  // keep one batch queued ahead of the wait
     const int64_t pb = bt - 1;
     hipEvent_t ev = ctx->ev_ctl[pb & 1];
+    const auto tw = std::chrono::steady_clock::now();
     if (!(world > 1 && allgather.wait && allgather.wait(ev))) SVMD_CHECK(hipEventSynchronize(ev));
+    if (o.host_wait_ms) *o.host_wait_ms += ms_since(tw);
     if (ctl_h[pb & 1].stop != SVM_STOP_RUNNING) {
       fin = ctl_h + (pb & 1);  // batch bt (queued) runs as no-ops; the state is final
       break;

@@ -98,6 +98,9 @@ def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] =
     threads; RCCL or the loopback rehearsal)."""
     lib = N.hip()
     out = _fit_native(lib.svmd_cascade_group_decomp, group.handle, X, y, params or SVMParams(), q, group.world)
+    waits = np.zeros(group.world)
+    if int(lib.svmd_cascade_group_decomp_waits(group.handle, N.ptr(waits), waits.size)) == group.world:
+        out["host_wait_ms"] = [round(float(v), 3) for v in waits]
     buf = np.zeros(4 + 2 * group.world)
     k = int(lib.svmd_cascade_group_decomp_solo(group.handle, N.ptr(buf), buf.size))
     if k:  # a loopback rehearsal with SVM355_CASCADE_SERIAL_SOLVES=1: every rank's device work timed alone
@@ -169,6 +172,7 @@ class DistributedDecompSVC:
         self.stats_ = out["stats"]
         self.rank_ms_ = out["rank_ms"]
         self.solo_ = out.get("solo")  # per-rank solo timing of a one-GPU rehearsal (None otherwise)
+        self.host_wait_ms_ = out.get("host_wait_ms")  # per-rank host time blocked in the per-batch waits
         self.timings_ = {"solve_ms": out["stats"]["solve_us"] / 1e3, "native_ms": out["wall_ms"],
                          **out["stats"]}
         self.fit_time_ = time.perf_counter() - t0

@@ -254,6 +254,7 @@ def test_column_cache_leaves_the_device_to_torch():
     ctx = D.DeviceContext.get("cuda:0")
     slab = ctypes.c_int64(0)
     assert ctx.lib.svmd_cache_bytes(ctx.handle, None, ctypes.byref(slab)) == 0
+    torch.cuda.empty_cache()  # no cached torch blocks: an allocation beyond `free` must come from the slab
     free, total = torch.cuda.mem_get_info(0)
     assert 0 < slab.value <= total // 4  # the cache ran (250k rows outgrow the last-level cache), capped
     need = free + slab.value // 2  # more than is free: only the slab's memory makes it fit

@@ -77,8 +77,7 @@ def test_asan_ubsan_threaded_cascades_hostcomm_and_decomp(thread_exes):
 
 
 def test_tsan_threaded_cascades_hostcomm_and_decomp(thread_exes):
-    """TSan (ROCm clang's runtime: gcc 11's libtsan misreads libstdc++'s condition-variable waits).
-    The quick scenario list (star P = 3, tree P = 4, both transports) keeps the 5-15x TSan slowdown
-    within the test budget; ``bin_tsan/svm_threads`` without --quick runs the full list."""
-    out = _run_threads(thread_exes[1], ["--quick"], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"}, timeout=900)
-    assert "cascade hostcomm tree P=4" in out and "decomp distributed, 4 hostcomm ranks" in out
+    """TSan (ROCm clang's runtime: gcc 11's libtsan misreads libstdc++'s condition-variable waits), the
+    full scenario list (~1.5 min)."""
+    out = _run_threads(thread_exes[1], [], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"}, timeout=900)
+    assert "cascade hostcomm tree P=8" in out and "decomp distributed, 4 hostcomm ranks" in out
