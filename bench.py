@@ -293,9 +293,11 @@ def main(argv=None):
 
             group = DeviceGroup(a.gpus, a.transport, a.comm_timeout)
 
+    cascade_comm_ok = [True]  # false once a failed cascade aborted the ranks' communicators
+
     def barrier_sync():
         sync()
-        if crank is not None:
+        if crank is not None and cascade_comm_ok[0]:
             crank.barrier()  # RCCL all-reduce over the cascade's own communicators
         if dist is not None:
             dist.barrier()
@@ -315,8 +317,12 @@ def main(argv=None):
         else:
             model = cascade_fit(a.topology)
 
+    # fault injection (tests): SVM355_BENCH_CASCADE_FAIL="rank,round" makes that cascade rank fail at that round
+    cfail = [int(v) for v in os.environ.get("SVM355_BENCH_CASCADE_FAIL", "-1,-1").split(",")]
+
     def cascade_fit(topology):
-        c = CascadeSVM(params, topology=topology, comm_timeout_s=a.comm_timeout, solver=cascade_solver)
+        c = CascadeSVM(params, topology=topology, comm_timeout_s=a.comm_timeout, solver=cascade_solver,
+                       fail_rank=cfail[0], fail_round=cfail[1])
         if multiproc:
             return c.fit_rank(crank, part.X, part.y, np.arange(lo, hi), a.n)
         return c.fit(full.X, full.y, world=a.gpus, device="cpu" if cpu else "cuda", group=group)
@@ -399,29 +405,33 @@ def main(argv=None):
     # (barrier + device sync on both sides, max over ranks), with its rounds, SV history and critical path.
     cascades = {}
     if mode == "decomp" and a.cascade_steps > 0 and not cpu:
+        # After the headline: a cascade that fails (on any rank) is reported in the line instead of ending
+        # the run -- the headline was already measured.  Its ranks' communicators are then aborted, so no
+        # further cascade runs and the closing barriers skip them (the launcher's gloo group still works).
         for topo in ("star", "tree"):
             if topo == "tree" and a.gpus & (a.gpus - 1):
                 cascades[f"cascade_{topo}"] = {"skipped": "the classical cascade needs a power-of-2 number of GPUs"}
                 continue
-            cm = None
 
-            def cstep():
-                nonlocal cm
-                try:
+            def run_topo():
+                cm = cascade_fit(topo)  # warm
+                barrier_sync()
+                tc = time.perf_counter()
+                for _ in range(a.cascade_steps):
                     cm = cascade_fit(topo)
-                except Exception as e:  # noqa: BLE001
-                    if multiproc:
-                        print(f"bench.py rank {rank}: cascade ({topo}) failed: {e}", file=sys.stderr, flush=True)
-                        os._exit(1)
-                    raise
+                barrier_sync()
+                return cm, (time.perf_counter() - tc) / a.cascade_steps
 
-            cstep()  # warm
-            barrier_sync()
-            tc = time.perf_counter()
-            for _ in range(a.cascade_steps):
-                cstep()
-            barrier_sync()
-            cel = (time.perf_counter() - tc) / a.cascade_steps
+            err = ""
+            try:
+                cm, cel = run_topo()
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line
+                err = f"{type(e).__name__}: {e}"
+                print(f"bench.py rank {rank}: cascade ({topo}) failed: {err}", file=sys.stderr, flush=True)
+            if not agree(not err):
+                cascades[f"cascade_{topo}"] = {"error": err or "failed on another rank"}
+                cascade_comm_ok[0] = False
+                break
             if dist is not None:
                 e = torch.tensor([cel], dtype=torch.float64)
                 dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -656,7 +666,10 @@ def main(argv=None):
                 f.write(s + "\n")
     for h in (crank, group, dgroup, drank):
         if h is not None:
-            h.close()
+            try:
+                h.close()
+            except Exception as e:  # noqa: BLE001 - an aborted communicator; the line is already printed
+                print(f"bench.py rank {rank}: close: {e}", file=sys.stderr, flush=True)
     if dist is not None:
         dist.destroy_process_group()
     return 0

@@ -51,6 +51,11 @@ class HostCommRank:
     def __init__(self, group=None, comm_timeout_s: float = 600.0):
         import torch.distributed as dist
 
+        # The rank's own gloo group unless one is given (collective: every rank constructs its rank
+        # together): a collective this rank abandons after a timeout stays pending on it, and must not be
+        # matched against the launcher's own control collectives on the default group afterwards.
+        if group is None:
+            group = dist.new_group(backend="gloo")
         self.dist, self.group = dist, group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.timeout_s = float(comm_timeout_s)

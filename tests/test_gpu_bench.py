@@ -130,3 +130,17 @@ def test_torchrun_hostcomm_rank_failing_mid_solve_ends_every_process():
     err = p.stdout + p.stderr
     assert "injected failure of rank 1 at outer iteration 3" in err, err[-3000:]
     assert wall < 150
+
+
+def test_a_failing_cascade_after_the_headline_is_reported_not_fatal():
+    """The N-GPU line's cascades run after the headline was measured: a cascade rank that fails
+    (SVM355_BENCH_CASCADE_FAIL) ends that cascade on every rank, the line still carries the headline and
+    the error, and every process exits 0 (per-process launch, two ranks sharing the GPU)."""
+    p, wall = _torchrun(2, "--parallel", "decomp", "--transport", "hostcomm", "--rows", "6000", "--test-rows", "500",
+                        "--steps", "1", "--warmup", "1", "--baseline-1gpu", "0", "--cascade-steps", "1",
+                        "--comm-timeout", "30", env_extra={"SVM355_BENCH_CASCADE_FAIL": "1,1"}, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["stop_reason"] == "converged" and out["value"] > 0
+    assert "error" in out["cascade_star"] and "cascade_tree" not in out
