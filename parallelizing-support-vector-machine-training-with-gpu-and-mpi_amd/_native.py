@@ -296,6 +296,7 @@ _HIP_SIGS = {
     "svmd_cascade_rank_create_hostcomm": (c_void_p, [_P, c_int32, c_double]),
     "svmd_cascade_group_decomp_solo": (c_int64, [c_void_p, _P, c_int64]),
     "svmd_cascade_group_decomp_waits": (c_int64, [c_void_p, _P, c_int64]),
+    "svmd_cascade_rank_decomp_wait": (c_double, [c_void_p]),
     "svmd_cascade_rank_fit": (POINTER(SvmCascadeOut), [c_void_p, _P, c_int32, _P, _P, c_int64, c_int64, c_int64,
                                                        POINTER(SvmCascadeCfg)]),
     "svmd_cascade_rank_barrier": (c_int32, [c_void_p]),

@@ -798,6 +798,7 @@ struct ProcRank {
   ncclComm_t comm = nullptr;
   std::unique_ptr<Transport> tr;
   RcclTransport* rccl = nullptr;  // tr when it is RCCL (deadline / abort policy per call)
+  double host_wait_ms = 0.0;       // the last distributed decomposition fit's host wait
   void set_policy(WaitPolicy wp) {
     if (rccl) rccl->set_policy(std::move(wp));
   }
@@ -1223,8 +1224,9 @@ SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y
     (void)hipSetDevice(pr->device);
     pr->set_policy(WaitPolicy{nullptr, pr->timeout_s});
     try {
+      pr->host_wait_ms = 0.0;
       decomp_on_rank(*pr->be, pr->tr->world() > 1 ? pr->tr.get() : nullptr, X, y, n, d, p, q, alpha_out, r, stats,
-                     ms_out, mm_out);
+                     ms_out, mm_out, nullptr, &pr->host_wait_ms);
     } catch (...) {
       pr->tr->abort();  // the peers' waits fail too
       pr->broken = true;
@@ -1235,6 +1237,12 @@ SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y
     set_error("decomposition SMO: %s", e.what());
     return SVM_ERR_DEVICE;
   }
+}
+
+// The last svmd_cascade_rank_decomp fit's host time blocked in the per-batch waits (ms).
+SVM_API double svmd_cascade_rank_decomp_wait(void* h) {
+  auto* pr = static_cast<ProcRank*>(h);
+  return pr ? pr->host_wait_ms : 0.0;
 }
 
 SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap) {

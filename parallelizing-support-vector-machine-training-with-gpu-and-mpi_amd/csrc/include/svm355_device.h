@@ -197,6 +197,8 @@ SVM_API int64_t svmd_cascade_group_decomp_solo(void* group, double* out, int64_t
 // The last svmd_cascade_group_decomp fit's per-rank host time blocked in the per-batch waits (ms);
 // returns the number of ranks.
 SVM_API int64_t svmd_cascade_group_decomp_waits(void* group, double* out, int64_t cap);
+// The same for this process's rank (svmd_cascade_rank_decomp).
+SVM_API double svmd_cascade_rank_decomp_wait(void* rank);
 SVM_API void* svmd_cascade_rank_create_hostcomm(const svm_host_comm* comm, int32_t device, double comm_timeout_s);
 SVM_API svm_cascade_out* svmd_cascade_rank_fit(void* rank, const void* X, int32_t u8, const int32_t* y,
                                                const int64_t* ids, int64_t n_part, int64_t d, int64_t n_total,

@@ -113,7 +113,9 @@ def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] =
 def rank_fit(rank, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
     """This process's rank of a distributed decomposition solve (every rank passes all rows)."""
     lib = N.hip()
-    return _fit_native(lib.svmd_cascade_rank_decomp, rank.handle, X, y, params or SVMParams(), q, 1)
+    out = _fit_native(lib.svmd_cascade_rank_decomp, rank.handle, X, y, params or SVMParams(), q, 1)
+    out["host_wait_ms"] = [round(float(lib.svmd_cascade_rank_decomp_wait(rank.handle)), 3)]
+    return out
 
 
 class DistributedDecompSVC:
