@@ -276,7 +276,41 @@ def main(argv=None):
         from svm355.parallel.decomp import DistributedDecompSVC
 
         if multiproc:
-            crank = proc_rank()
+            # One rank per process.  Before any timed fit, a preflight solve of the first PREFLIGHT_ROWS rows
+            # must equal the one-GPU solve bit for bit on every rank; if the RCCL rank cannot be set up or
+            # its preflight fails on any rank, the ranks fall back together to the host-staged gloo
+            # transport (the same driver; slower exchanges), and the line says why.
+            err = ""
+            try:
+                crank = proc_rank()
+            except Exception as e:  # noqa: BLE001 - the fallback below, reported in the line
+                err = f"rank set-up: {type(e).__name__}: {e}"
+            if agree(not err) and not cpu:
+                pre = full.subset(0, min(PREFLIGHT_ROWS, a.n))
+                try:
+                    m = DistributedDecompSVC(a.gpus, rank=crank).fit(pre.X, pre.y)
+                    ref = SVC(device=str(dev), solver="decomp").fit(pre.X, pre.y)
+                    if not (m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)):
+                        err = (f"preflight differs from the one-GPU solve (iterations {m.n_iter_} vs {ref.n_iter_}, "
+                               f"b {m.b_!r} vs {ref.b_!r})")
+                except Exception as e:  # noqa: BLE001
+                    err = f"preflight: {type(e).__name__}: {e}"
+            if not agree(not err):
+                if cpu or hostcomm:
+                    print(f"bench.py rank {rank}: distributed decomposition unavailable: {err or 'another rank'}",
+                          file=sys.stderr, flush=True)
+                    os._exit(1)
+                fallback_reason = f"RCCL: {err or 'failed on another rank'}; exchanges over gloo (host-staged)"
+                if rank == 0:
+                    print(f"bench.py: {fallback_reason}", file=sys.stderr, flush=True)
+                if crank is not None:
+                    try:
+                        crank.close()
+                    except Exception:  # noqa: BLE001 - an aborted communicator
+                        pass
+                from svm355.parallel.hostcomm import HostCommDeviceRank
+
+                crank = HostCommDeviceRank(dev_index, comm_timeout_s=a.comm_timeout)
         elif cpu:
             pass  # thread ranks on the CPU oracle (DistributedDecompSVC(transport="cpu"))
         else:
@@ -521,13 +555,14 @@ def main(argv=None):
                         "(pairwise_solver: that solve's fit, SV set and b on the same rows)"
                         if a.solver == "decomp" else "")})
     elif mode == "decomp":
-        extra = {"n_sv": int(len(model.support_)), "iterations": int(model.n_iter_), "b": float(model.b_),
+        extra = {"n_sv": int(len(model.support_)), "fallback_reason": fallback_reason, "iterations": int(model.n_iter_), "b": float(model.b_),
                  "stop_reason": model.stop_reason_, "decomp_stats": model.stats_, "rank_ms": model.rank_ms_,
                  "rank_host_wait_ms": getattr(model, "host_wait_ms_", None),
                  "warmup_fit_ms": warm_ms, "cold_fit_ms": warm_ms[0] if warm_ms else None,
                  "launch_form": ("one rank per process" + (" (CPU oracle over gloo)" if cpu else
                                                            f" over gloo, host-staged ({a.gpus} processes on "
-                                                           f"{min(ndev, a.gpus)} GPU(s))" if hostcomm else " (RCCL)")
+                                                           f"{min(ndev, a.gpus)} GPU(s))"
+                                                           if type(crank).__name__ == "HostCommDeviceRank" else " (RCCL)")
                                  if multiproc else "thread ranks on the CPU oracle (loopback)" if cpu
                                  else "thread ranks, one GPU each")
                  if a.transport != "loopback" else f"rehearsal: {a.gpus} ranks on one GPU",

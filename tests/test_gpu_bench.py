@@ -144,3 +144,18 @@ def test_a_failing_cascade_after_the_headline_is_reported_not_fatal():
     out = json.loads(lines[0])
     assert out["stop_reason"] == "converged" and out["value"] > 0
     assert "error" in out["cascade_star"] and "cascade_tree" not in out
+
+
+def test_torchrun_falls_back_to_gloo_when_rccl_is_unusable():
+    """The per-process decomposition's set-up: a rank whose RCCL cannot be loaded (SVM355_RCCL_LIB points
+    nowhere) makes every rank fall back to the host-staged gloo transport before any timed fit; the
+    line reports why, and the preflight solve equals the one-GPU solve."""
+    p, wall = _torchrun(1, "--parallel", "decomp", "--rows", "6000", "--test-rows", "500", "--steps", "1",
+                        "--warmup", "1", "--baseline-1gpu", "1", "--cascade-steps", "0",
+                        env_extra={"SVM355_RCCL_LIB": "/nonexistent/librccl.so"}, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["fallback_reason"].startswith("RCCL: rank set-up") and "gloo" in out["fallback_reason"]
+    assert out["launch_form"].startswith("one rank per process over gloo")
+    assert out["bit_identical_to_1gpu"] is True
