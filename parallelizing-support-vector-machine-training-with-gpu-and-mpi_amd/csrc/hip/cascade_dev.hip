@@ -897,7 +897,9 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   // group's abort must end every rank with an error, not a hang
   check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, o),
         "decomposition SMO");
-  if (!used) throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan)");
+  if (!used)
+    throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan), or n = " +
+                       std::to_string(n) + " is beyond the solver's 2,097,152 rows");
   if (alpha_out) be.d2h(alpha_out, ad, n * 8);
   be.sync();
   if (r) *r = res;
@@ -1250,14 +1252,19 @@ SVM_API int svmd_nccl_unique_id(uint8_t* out, int64_t cap) {
     set_error("svmd_nccl_unique_id: need %zu bytes", sizeof(ncclUniqueId));
     return SVM_ERR_ARG;
   }
-  ncclUniqueId id;
-  const ncclResult_t rc = RC().GetUniqueId(&id);
-  if (rc != ncclSuccess) {
-    set_error("ncclGetUniqueId: %s", RC().GetErrorString(rc));
+  try {  // RC() throws when RCCL cannot be loaded: never across the C ABI
+    ncclUniqueId id;
+    const ncclResult_t rc = RC().GetUniqueId(&id);
+    if (rc != ncclSuccess) {
+      set_error("ncclGetUniqueId: %s", RC().GetErrorString(rc));
+      return SVM_ERR_DEVICE;
+    }
+    std::memcpy(out, &id, sizeof(id));
+    return SVM_OK;
+  } catch (const std::exception& e) {
+    set_error("svmd_nccl_unique_id: %s", e.what());
     return SVM_ERR_DEVICE;
   }
-  std::memcpy(out, &id, sizeof(id));
-  return SVM_OK;
 }
 
 SVM_API int64_t svmd_nccl_unique_id_bytes(void) { return int64_t(sizeof(ncclUniqueId)); }

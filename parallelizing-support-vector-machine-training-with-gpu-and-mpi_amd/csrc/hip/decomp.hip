@@ -1646,6 +1646,7 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
                     int64_t* stats, bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
+  if (!decomp_shape(n, q, o.world).ok) return SVM_OK;  // beyond the solver's shapes: the caller's fallback
   const char* fe = getenv("SVM355_DECOMP_F64");
   const bool force_f64 = fe && atoi(fe) == 1;
   QuantPlan P;
@@ -1712,6 +1713,9 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
                   bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
+  // beyond the solver's shapes (n > 512 blocks x 4,096 points = 2,097,152 rows): nothing runs, the caller
+  // takes the pairwise solver (SVC(solver="auto"))
+  if (!decomp_shape(n, q, o.world).ok) return SVM_OK;
   QuantPlan P;
   if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;  // igram's LDS table bound
   int8_t* Q;

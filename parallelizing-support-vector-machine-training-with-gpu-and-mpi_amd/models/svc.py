@@ -159,8 +159,9 @@ class SVC:
             out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set,
                                       warm=alpha0 is not None)
             if out is None and self.solver == "decomp":
-                raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16, or the FP64-row "
-                                 "solve's workspace (n x 1024 doubles) does not fit the device")
+                raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16, n is beyond the "
+                                 "solver's 2,097,152 rows, or the FP64-row solve's workspace (n x 1024 doubles) does "
+                                 "not fit the device")
         if out is not None:
             res, tm = out
         else:  # the pairwise solver (also solver="auto" when the decomposition's workspace does not fit)

@@ -105,8 +105,15 @@ class RcclRank:
         """Every rank of an initialised torch.distributed group calls this collectively."""
         import torch.distributed as dist
 
-        obj = [cls.unique_id() if dist.get_rank() == 0 else None]
+        obj = [None]
+        if dist.get_rank() == 0:
+            try:
+                obj[0] = cls.unique_id()
+            except Exception as e:  # noqa: BLE001 - every rank must learn it, not wait in the broadcast
+                obj[0] = f"{type(e).__name__}: {e}"
         dist.broadcast_object_list(obj, src=0)
+        if isinstance(obj[0], str):
+            raise N.NativeError(f"RCCL unique id on rank 0 failed: {obj[0]}")
         return cls(device, obj[0], dist.get_world_size(), dist.get_rank(), comm_timeout_s)
 
     def barrier(self) -> None:

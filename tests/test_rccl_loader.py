@@ -10,3 +10,21 @@ def test_rccl_runtime_is_the_headers_library_even_inside_pytorch():
     info = rccl_info()
     assert info["rccl_skew"] is False and info["rccl_header"] == info["rccl_runtime"] != "unknown"
     assert info["rccl_path"].endswith("librccl.so.1") and "torch" not in info["rccl_path"]
+
+
+def test_unloadable_rccl_is_an_error_not_an_abort():
+    """SVM355_RCCL_LIB pointing nowhere: the entry points that need RCCL report an error through the C ABI
+    (svmd_nccl_unique_id) instead of letting a C++ exception terminate the process -- the per-process
+    bench then falls back to the gloo transport (tests/test_gpu_bench.py)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = ("from svm355.parallel.rccl import RcclRank\n"
+            "from svm355._native import NativeError\n"
+            "try:\n    RcclRank.unique_id()\nexcept NativeError as e:\n    print('ERR', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=Path(__file__).resolve().parents[1],
+                       env={**__import__("os").environ, "SVM355_RCCL_LIB": "/nonexistent/librccl.so"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "ERR" in r.stdout and "cannot load /nonexistent/librccl.so" in r.stdout
