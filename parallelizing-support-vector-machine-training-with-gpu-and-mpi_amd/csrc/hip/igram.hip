@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
 #pragma unroll
             for (int nj = 0; nj < 2; ++nj)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) xacc[nj][r] += wgt * double(acc[nj][r]);
+              for (int r = 0; r < 16; ++r) xacc[nj][r] = __builtin_fma(wgt, double(acc[nj][r]), xacc[nj][r]);
             fresh = true;
           }
         }
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
             if (wgt != 0.0) {  // last k-step of an extra group: flush its exact cross term
 #pragma unroll
               for (int r = 0; r < 16; ++r)
-                if (2 * (r & ~3) < gc) xacc[r] += wgt * double(acc[r]);  // quarters of real columns only
+                if (2 * (r & ~3) < gc) xacc[r] = __builtin_fma(wgt, double(acc[r]), xacc[r]);  // quarters of real columns only
               fresh = true;
             }
           }

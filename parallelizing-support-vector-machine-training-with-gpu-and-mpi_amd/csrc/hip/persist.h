@@ -346,14 +346,14 @@ __device__ __forceinline__ double k12_exact(const QRows& q, int64_t ih, int64_t 
     const int s = __builtin_ctzll(m0);
     m0 &= m0 - 1;
     const int32_t ps = __builtin_amdgcn_readlane(P0, s);
-    x += read_lane64(wl[0], s) * double(ps - prev);
+    x = __builtin_fma(read_lane64(wl[0], s), double(ps - prev), x);
     prev = ps;
   }
   while (m1) {
     const int s = __builtin_ctzll(m1);
     m1 &= m1 - 1;
     const int32_t ps = __builtin_amdgcn_readlane(P1, s);
-    x += read_lane64(wl[1], s) * double(ps - prev);
+    x = __builtin_fma(read_lane64(wl[1], s), double(ps - prev), x);
     prev = ps;
   }
   const int32_t acc = __builtin_amdgcn_readlane(nsteps > 64 ? P1 : P0, 63) - prev;
@@ -592,11 +592,11 @@ struct CachedRows {
 #pragma unroll
           for (int e = 0; e < EG; ++e) {
             if (DA) {
-              xa[e] += wg * double(acca[e]);
+              xa[e] = __builtin_fma(wg, double(acca[e]), xa[e]);
               acca[e] = 0;
             }
             if (DB) {
-              xb[e] += wg * double(accb[e]);
+              xb[e] = __builtin_fma(wg, double(accb[e]), xb[e]);
               accb[e] = 0;
             }
           }

@@ -52,7 +52,7 @@ __device__ __forceinline__ double kval(const QRows& q, int64_t a, int64_t b, dou
       if (s < q.main_step0) {
         const double wg = q.step_w[s];
         if (wg != 0.0) {  // igram_tri_kernel's group flush, same order and expression
-          x += wg * double(acc);
+          x = __builtin_fma(wg, double(acc), x);
           acc = 0;
         }
       }
@@ -110,8 +110,8 @@ __device__ __forceinline__ void kval2(const QRows& q, int64_t a, int64_t b, int6
       if (s < q.main_step0) {
         const double wg = q.step_w[s];
         if (wg != 0.0) {
-          xa += wg * double(acca);
-          xb += wg * double(accb);
+          xa = __builtin_fma(wg, double(acca), xa);
+          xb = __builtin_fma(wg, double(accb), xb);
           acca = 0;
           accb = 0;
         }

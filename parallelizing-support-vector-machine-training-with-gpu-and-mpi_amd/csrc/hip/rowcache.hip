@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kNT) void kc_step_kernel(const KcPartial* __restric
       if (st_k < q.main_step0) {
         const double wg = q.step_w[st_k];
         if (wg != 0.0) {
-          x += wg * double(acc);
+          x = __builtin_fma(wg, double(acc), x);
           acc = 0;
         }
       }
