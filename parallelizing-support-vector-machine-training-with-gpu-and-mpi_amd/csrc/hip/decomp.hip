@@ -316,28 +316,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
                                                       const double* __restrict__ Wf, double C, double eps,
                                                       int32_t* __restrict__ cols, double* __restrict__ coef,
                                                       int32_t* __restrict__ mcount, DecompHost* __restrict__ hs,
-                                                      DecompCtl* __restrict__ pub, int pf_rows) {
+                                                      DecompCtl* __restrict__ pub) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
-  if (blockIdx.x != 0) {
-    // L2 prefetch helpers (grid 1 + 8 H): blocks 8, 16, .., 8 H are dealt to workgroup 0's XCD (observed
-    // round-robin placement; a different placement changes only speed) and read the first pf_rows rows of
-    // K(W, W) through that XCD's L2, so the solve's dependent row loads hit there instead of the last-level
-    // cache.  The other blocks exit at once.
-    if ((blockIdx.x & 7) == 0) {
-      const int hh = blockIdx.x / 8 - 1, H = int(gridDim.x - 1) / 8, mm = ctl->m;
-      const int rows = pf_rows < mm ? pf_rows : mm, pieces = (mm + 1) / 2;
-      double acc = 0.0;
-      for (int r = hh; r < rows; r += H) {
-        const double2* src = reinterpret_cast<const double2*>(Kw + int64_t(r) * ldw);
-        for (int c = threadIdx.x; c < pieces; c += NT) {
-          const double2 v = src[c];
-          acc += v.x + v.y;
-        }
-      }
-      if (acc < 0.0) alpha[0] = acc;  // never taken (kernel values are >= 0): keeps the loads
-    }
-    return;
-  }
   const int m = ctl->m;
   const double tau_in = ctl->tau_in;
   const int64_t max_inner = ctl->max_inner;
@@ -1168,11 +1148,6 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const bool inner_dp = inner_wss2 && (wss_env ? atoi(wss_env) >= 3 : true);
   // SVM355_DECOMP_WSS = 4: the second pair's j by the second-order gain of row i2 (opt-in)
   const bool inner_j2s = inner_dp && wss_env && atoi(wss_env) == 4;
-  // SVM355_DECOMP_PF_H helper workgroups on the inner solve's XCD prefetch the first SVM355_DECOMP_PF_ROWS
-  // rows of K(W, W) into its L2 (ws_inner_kernel)
-  const int pf_h = getenv("SVM355_DECOMP_PF_H") ? std::max(0, std::min(31, atoi(getenv("SVM355_DECOMP_PF_H")))) : 0;
-  const int pf_rows = getenv("SVM355_DECOMP_PF_ROWS") ? std::max(0, atoi(getenv("SVM355_DECOMP_PF_ROWS"))) : kMaxWS;
-  const int pf_grid = 1 + 8 * pf_h;
   const int64_t ldw = kMaxWS;              // K(W, W) row stride
   const int64_t ldp = 2 * (kMaxWS / 128);  // column halves of the f update
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1392,14 +1367,14 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
 #define SVM_WS_INNER_(NT, PER, PR, S2)                                                                            \
   do {                                                                                                             \
     if (inner_j2s && S2)                                                                                           \
-      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2, S2>), dim3(pf_grid), dim3(NT), 0, s, Kw, ldw, W, ctl, y,  \
-                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub, pf_rows);                                      \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,  \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
     else if (inner_dp && S2)                                                                                       \
-      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2>), dim3(pf_grid), dim3(NT), 0, s, Kw, ldw, W, ctl, y,      \
-                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub, pf_rows);                                      \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,      \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
     else                                                                                                           \
-      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(pf_grid), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha,   \
-                         Wf, p.C, p.eps, cols, coef, mcount, hs, pub, pf_rows);                                    \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha,   \
+                         Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                             \
   } while (0)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """L2 prefetch of K(W, W) for the inner solve: 60k / 250k decomposition fits with
 SVM355_DECOMP_PF_H helper workgroups on the inner solve's XCD reading the first SVM355_DECOMP_PF_ROWS rows
-of K(W, W) before / while the solve runs.  Prints the median fit time per setting and checks the model
+of K(W, W) before / while the solve runs.  The knobs exist only in commit 2254cc6 (measured, not kept:
+profiles/r5_inner_chain_variants.txt).  Prints the median fit time per setting and checks the model
 (SV count, b, iterations) is the same as without helpers (they only read)."""
 import os
 import sys
