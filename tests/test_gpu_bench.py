@@ -90,7 +90,7 @@ def _torchrun(nproc, *args, env_extra=None, timeout=280):
     return p, time.perf_counter() - t0
 
 
-@pytest.mark.parametrize("nproc,rows", [(2, 60000), (4, 6000)])
+@pytest.mark.parametrize("nproc,rows", [(2, 60000), (4, 6000), (8, 60000)])
 def test_torchrun_processes_share_one_gpu_over_hostcomm(nproc, rows):
     """the per-process path of the N-GPU headline (torchrun, one rank per process,
     svmd_cascade_rank_decomp) at world > 1 on the one GPU of the box.  RCCL refuses two ranks on one
