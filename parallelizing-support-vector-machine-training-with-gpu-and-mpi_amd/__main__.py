@@ -392,6 +392,9 @@ def _multiclass(argv) -> int:
     ap.add_argument("--gamma", type=float, default=0.00125)
     ap.add_argument("--tau", type=float, default=1e-5)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--solver", choices=["auto", "batched", "streams", "decomp"], default="auto",
+                    help="GPU class solves: one batched pairwise launch over a shared Gram (auto), or the "
+                         "decomposition solver per class with no Gram (decomp)")
     ap.add_argument("--gpus", type=int, default=0, help="launch torchrun with this many ranks (classes dealt over them)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
     ap.add_argument("--json", default=None)
@@ -429,7 +432,7 @@ def _multiclass(argv) -> int:
     else:
         tr = load_csv(a.train or f"{a.dataset}_train_data.csv")
         te = load_csv(a.test or f"{a.dataset}_test_data.csv")
-    model = OneVsRestSVC(C=a.C, gamma=a.gamma, tol=a.tau, device=dev)
+    model = OneVsRestSVC(C=a.C, gamma=a.gamma, tol=a.tau, device=dev, solver=a.solver if use_gpu else "auto")
     t0 = time.perf_counter()
     model.fit(tr.X, tr.labels, transport=transport)
     if use_gpu:
@@ -447,6 +450,7 @@ def _multiclass(argv) -> int:
                 "program": "svm355 multiclass", "world": world, "n": tr.n, "classes": model.classes_.tolist(),
                 "n_sv_union": int(len(model.support_)), "n_iter": model.n_iter_.tolist(),
                 "b": model.intercepts_b_.tolist(), "stop_reasons": model.stop_reasons_, "accuracy": acc,
+                "solver": getattr(model, "timings_", {}).get("smo_solver", "cpu"),
                 "training_ms": (t1 - t0) * 1e3, "prediction_ms": (t2 - t1) * 1e3}) + "\n")
     if world > 1:
         dist.destroy_process_group()

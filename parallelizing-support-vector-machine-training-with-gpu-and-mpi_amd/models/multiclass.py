@@ -8,7 +8,12 @@ each is latency-bound on one XCD's worth of workgroups, so they run in ONE launc
 (smo.hip smo_multi_kernel): every XCD forms a team of workgroups that exchanges its per-iteration
 candidates through that XCD's L2 and pulls classes from a shared queue — eight classes at once, and
 a team that finishes early takes the next class.  (``solver="streams"``: one persistent solve per
-class on ``concurrent_solves`` streams instead.)  Prediction evaluates one
+class on ``concurrent_solves`` streams instead.)  ``solver="decomp"`` (the GPU default, as for ``SVC``):
+no Gram at all -- every class is
+the working-set decomposition solver of ``SVC(solver="decomp")`` (decomp.hip) on the one copy of the
+device rows, the classes on ``concurrent_solves`` host threads of a persistent pool (each with its
+device context and stream): the one-workgroup inner solves of different classes run side by side on
+different CUs and their f-update GEMVs share the chip.  Prediction evaluates one
 cross-kernel block against the union of all classes' support vectors and applies every class's
 dual coefficients with one FP64 matrix product; the predicted label is the arg-max decision value.
 
@@ -23,7 +28,9 @@ dependency inside a solve.
 from __future__ import annotations
 
 import os
+import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
 import numpy as np
@@ -33,16 +40,51 @@ from ..utils.data import MinMaxScaler
 from ..utils.trace import trace_range
 
 
+_POOL_LOCK = threading.Lock()
+_POOLS: dict = {}
+_TLS = threading.local()
+
+
+def _pool(workers: int) -> ThreadPoolExecutor:
+    """A persistent pool per width for the decomposition class solves: its threads keep their device
+    contexts (DeviceContext is per thread) and streams from one fit to the next; never shut down under
+    a caller (thread ranks of one process may map onto the same pool at once)."""
+    workers = max(1, int(workers))
+    with _POOL_LOCK:
+        if workers not in _POOLS:
+            _POOLS[workers] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix=f"svm355-ovr{workers}")
+        return _POOLS[workers]
+
+
+def _thread_stream(device):
+    import torch
+
+    ss = getattr(_TLS, "streams", None)
+    if ss is None:
+        ss = _TLS.streams = {}
+    key = torch.device(device).index
+    if key not in ss:
+        ss[key] = torch.cuda.Stream(device)
+    return ss[key]
+
+
 class OneVsRestSVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
-                 gram: str = "auto", concurrent_solves: int = 8, solver: str = "auto", wss: str = "first"):
-        """``solver``: "batched" (default via "auto") runs all class solves in ONE kernel launch, a team
+                 gram: str = "auto", concurrent_solves: Optional[int] = None, solver: str = "auto",
+                 wss: str = "first"):
+        """``solver`` (GPU): "auto" = "decomp" unless ``wss="second"`` or a ``gram`` is forced, then
+        "batched".  "batched" runs all pairwise class solves in ONE kernel launch over the shared Gram, a team
         of workgroups per XCD pulling classes from a queue; "streams" runs one persistent solve per
-        class on ``concurrent_solves`` streams.  Results are identical either way.  ``wss="second"``:
+        class on ``concurrent_solves`` streams (default 8).  Results are identical either way.  "decomp":
+        the working-set decomposition solver per class with no Gram, ``concurrent_solves`` classes at a time
+        (default: all).  ``wss="second"``:
         the opt-in second-order working-set selection (as ``SVC(wss="second")``) in every class solve."""
-        if solver not in ("auto", "batched", "streams"):
-            raise ValueError("solver must be auto, batched or streams")
+        if solver not in ("auto", "batched", "streams", "decomp"):
+            raise ValueError("solver must be auto, batched, streams or decomp")
+        if solver == "decomp" and wss == "second":
+            raise ValueError("the decomposition solver has its own (second-order) inner selection; wss applies to "
+                             "the pairwise solvers")
         if wss not in ("first", "second"):
             raise ValueError("wss must be 'first' or 'second'")
         self.solver = solver
@@ -136,6 +178,8 @@ class OneVsRestSVC:
         from ..ops import device as D
 
         device = torch.device(self._dev())
+        if self.solver == "decomp" or (self.solver == "auto" and self.params.wss == 1 and self.gram == "auto"):
+            return self._fit_cuda_decomp(X, labels, device)
         t0 = time.perf_counter()
         d = X.shape[1]
         Xu = K = None
@@ -186,7 +230,7 @@ class OneVsRestSVC:
                 rs, self.batched_ = D.smo_multi(K, Yb, Ab, self.params, n=n)
                 alphas[mine] = Ab
                 results = dict(zip(mine, rs))
-            workers = max(1, min(self.concurrent_solves, len(mine)))
+            workers = max(1, min(self.concurrent_solves or 8, len(mine)))
             if results:
                 pass
             elif workers > 1:
@@ -217,6 +261,71 @@ class OneVsRestSVC:
         self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, "gram_ms": (t2 - t1) * 1e3,
                          "smo_ms_all_classes": (t3 - t2) * 1e3, "gram_path": path,
                          "smo_solver": "batched" if self.batched_ else "streams"}
+
+    def _fit_cuda_decomp(self, X, labels, device):
+        """Every class by the decomposition solver on the shared device rows (no Gram)."""
+        import torch
+
+        from .. import _native as N
+        from ..ops import device as D
+
+        t0 = time.perf_counter()
+        d = X.shape[1]
+        Xu = Xd = sqn = None
+        if X.dtype == np.uint8:
+            Xu = D.upload_u8(X, device)
+            mn, mx = D.minmax_u8(Xu)
+            rows = Xu
+        else:
+            Xd = D.upload_rows(X, device)
+            mn, mx, sqn = D.minmax_scale_(Xd, d)
+            rows = Xd
+        mm = torch.cat([mn, mx]).cpu().numpy()
+        mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
+        t1 = time.perf_counter()
+        n = X.shape[0]
+        ys = self._ys(labels)
+        ys_d = [torch.from_numpy(y).to(device) for y in ys]
+        alphas = torch.zeros((len(self.classes_), n), dtype=torch.float64, device=device)
+        torch.cuda.synchronize(device)
+        mine = [k for k in range(len(ys)) if self._mine(k)]
+
+        def solve(k):
+            s = _thread_stream(device)
+            with torch.cuda.stream(s):
+                out = D.train_decomp(rows, ys_d[k], alphas[k], self.params, mn_h, mx_h)
+            s.synchronize()
+            if out is None:
+                raise N.NativeError(f"class {self.classes_[k]}: the decomposition solver declined these rows "
+                                    "(no exact-integer plan for uint8 rows, or beyond its shapes); use "
+                                    "solver='batched'")
+            return out
+
+        with trace_range(f"svm355.ovr.decomp classes={len(mine)}"):
+            workers = self.concurrent_solves or len(mine)
+            outs = dict(zip(mine, _pool(min(workers, max(1, len(mine)))).map(solve, mine))) if mine else {}
+            torch.cuda.synchronize(device)
+        bs = [outs[k][0].b if k in outs else 0.0 for k in range(len(ys))]
+        iters = [outs[k][0].iterations if k in outs else 0 for k in range(len(ys))]
+        stops = [outs[k][0].stop_reason if k in outs else "" for k in range(len(ys))]
+        alphas, bs, iters, stops = self._combine(alphas, bs, iters, stops)
+        t2 = time.perf_counter()
+        a = alphas.cpu().numpy()
+        Y = np.stack(ys, 0)
+        sup = np.flatnonzero((a > self.params.sv_tol).any(0)).astype(np.int64)
+        self._finish(sup, (a * Y).T, bs, iters, stops)
+        idx = torch.from_numpy(self.support_).to(device)
+        Xs, ns = D.sv_rows_u8(Xu, idx, mn, mx) if Xu is not None else (D.gather_rows(Xd, idx), sqn[idx].contiguous())
+        self._dev_model = {"Xs": Xs, "ns": ns,
+                           "coef": torch.from_numpy(np.ascontiguousarray(self.dual_coef_)).to(device),
+                           "b": torch.tensor(self.intercepts_b_, dtype=torch.float64, device=device),
+                           "mn": mn, "mx": mx, "d": d, "device": device}
+        self.scaler_ = MinMaxScaler(mn_h, mx_h)
+        self.batched_ = False
+        self.class_timings_ = {int(self.classes_[k]): outs[k][1] for k in outs}
+        self.timings_ = {"upload_preprocess_ms": (t1 - t0) * 1e3, "gram_ms": 0.0,
+                         "smo_ms_all_classes": (t2 - t1) * 1e3, "gram_path": "none (decomposition)",
+                         "smo_solver": "decomp"}
 
     def _finish(self, sup, coef_full, bs, iters, stops):
         self.support_ = sup

@@ -636,7 +636,7 @@ def test_ovr_multiclass_gpu_matches_cpu(dev):
 
     tr = synthetic_mnist(1500, seed=31)
     te = synthetic_mnist(400, seed=31, offset=1500)
-    g = OneVsRestSVC(device="cuda:0").fit(tr.X, tr.labels)
+    g = OneVsRestSVC(device="cuda:0", solver="batched").fit(tr.X, tr.labels)
     c = OneVsRestSVC(device="cpu").fit(tr.X, tr.labels)
     assert g.timings_["gram_path"] == "int8-exact"
     assert all(s == "converged" for s in g.stop_reasons_)
@@ -707,9 +707,9 @@ def test_ovr_byte_path_equals_fp64_row_path(dev, monkeypatch):
     tr = synthetic_mnist(3000, seed=34)
     te = synthetic_mnist(400, seed=34, offset=3000)
     X = tr.compact().X
-    a = OneVsRestSVC(device="cuda:0").fit(X, tr.labels)
+    a = OneVsRestSVC(device="cuda:0", solver="batched").fit(X, tr.labels)
     monkeypatch.setenv("SVM355_U8_TRAIN", "0")
-    b = OneVsRestSVC(device="cuda:0").fit(X, tr.labels)
+    b = OneVsRestSVC(device="cuda:0", solver="batched").fit(X, tr.labels)
     assert a.timings_["gram_path"] == b.timings_["gram_path"] == "int8-exact"
     np.testing.assert_array_equal(a.n_iter_, b.n_iter_)
     np.testing.assert_array_equal(a.intercepts_b_, b.intercepts_b_)
@@ -717,6 +717,44 @@ def test_ovr_byte_path_equals_fp64_row_path(dev, monkeypatch):
     np.testing.assert_array_equal(a.dual_coef_, b.dual_coef_)
     assert torch.equal(a._dev_model["Xs"], b._dev_model["Xs"]) and torch.equal(a._dev_model["ns"], b._dev_model["ns"])
     np.testing.assert_array_equal(a.predict(te.compact().X), b.predict(te.compact().X))
+
+
+def test_ovr_decomposition_equals_its_oracle_per_class(dev):
+    """The GPU default one-vs-rest (solver="decomp": every class by the decomposition solver on the shared
+    device rows, no Gram, classes on concurrent host threads) gives, class by class, the CPU decomposition
+    oracle's alpha, b and iterations bit for bit (on the device's exact kernel values), the same from
+    uint8 and FP64 host rows, and predicts like the batched pairwise solve."""
+    from svm355 import OneVsRestSVC
+    from svm355.ops import device as Dv
+
+    tr = synthetic_mnist(2500, seed=36)
+    te = synthetic_mnist(400, seed=36, offset=2500)
+    Xb = tr.compact().X
+    g = OneVsRestSVC(device="cuda:0").fit(Xb, tr.labels)
+    f = OneVsRestSVC(device="cuda:0", solver="decomp").fit(tr.X, tr.labels)
+    p = OneVsRestSVC(device="cuda:0", solver="batched").fit(Xb, tr.labels)
+    assert g.timings_["smo_solver"] == "decomp" and g.timings_["gram_ms"] == 0.0
+    assert all(s == "converged" for s in g.stop_reasons_)
+    for a, b in ((g.support_, f.support_), (g.dual_coef_, f.dual_coef_), (g.intercepts_b_, f.intercepts_b_),
+                 (g.n_iter_, f.n_iter_)):
+        np.testing.assert_array_equal(a, b)
+    Xu = Dv.upload_u8(Xb, torch.device("cuda:0"))
+    mmd = torch.empty(2 * tr.d, dtype=torch.float64, device="cuda:0")
+    mn, mx = Dv.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    K = Dv.rbf_gram_u8(Xu, 0.00125, mm[: tr.d].copy(), mm[tr.d:].copy())
+    Kh = np.ascontiguousarray(K[: tr.n, : tr.n].cpu().numpy())
+    del K
+    Dv.release_gram_buffers()
+    coef = np.zeros((tr.n, len(g.classes_)))
+    coef[g.support_] = g.dual_coef_
+    for c, cls in enumerate(g.classes_):
+        y = np.where(tr.labels == cls, 1, -1).astype(np.int32)
+        a, r, _ = C.decomp_train_gram_dist(Kh, y, g.params)
+        np.testing.assert_array_equal(coef[g.support_, c], (a * y)[g.support_])
+        assert np.all(np.delete(a, g.support_) <= g.params.sv_tol)
+        assert r.b == g.intercepts_b_[c] and r.iterations == g.n_iter_[c]
+    assert float(np.mean(g.predict(te.compact().X) == p.predict(te.compact().X))) >= 0.995
 
 
 def test_gram_epilogue_exp_is_bit_identical_to_libm(dev):

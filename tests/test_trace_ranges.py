@@ -47,3 +47,4 @@ def test_phases_are_wrapped():
     assert "svm355.cascade." in inspect.getsource(cascade.CascadeSVM.fit)
     src = inspect.getsource(multiclass.OneVsRestSVC._fit_cuda)
     assert "svm355.ovr.gram" in src and "svm355.ovr.solve" in src
+    assert "svm355.ovr.decomp" in inspect.getsource(multiclass.OneVsRestSVC._fit_cuda_decomp)
