@@ -292,9 +292,14 @@ class OneVsRestSVC:
 
         def solve(k):
             s = _thread_stream(device)
-            with torch.cuda.stream(s):
-                out = D.train_decomp(rows, ys_d[k], alphas[k], self.params, mn_h, mx_h)
-            s.synchronize()
+            try:
+                with torch.cuda.stream(s):
+                    out = D.train_decomp(rows, ys_d[k], alphas[k], self.params, mn_h, mx_h)
+                s.synchronize()
+            finally:
+                # the pool thread's context keeps no column-cache slab between fits (large n: up to a
+                # quarter of the HBM per context, invisible to PyTorch's allocator)
+                D.release_gram_buffers()
             if out is None:
                 raise N.NativeError(f"class {self.classes_[k]}: the decomposition solver declined these rows "
                                     "(no exact-integer plan for uint8 rows, or beyond its shapes); use "
