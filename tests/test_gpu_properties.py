@@ -1,0 +1,76 @@
+"""Property-based GPU checks (hypothesis): random integer-valued data with a handful of column ranges
+(so the exact-integer plan has extra range groups, as on pixel data), random labels, C and gamma.
+
+* the device decomposition solver equals its CPU oracle bit for bit -- alpha, b, iterations -- given the
+  device's own exact kernel values;
+* those kernel values are within 1e-14 of the reference's FP64 RBF (direct sum) of the scaled rows;
+* the pairwise device solver (the reference's trajectory) ends on the same stop test.
+
+Few examples (each is a fresh problem on the GPU) and small n keep the run short."""
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from svm355 import SVC, SVMParams
+from svm355.ops import cpu as C
+from svm355.ops import device as D
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+SETTINGS = settings(max_examples=20, deadline=None, database=None,
+                    suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+RANGES = [255, 254, 200, 128, 100, 51, 17, 3]
+
+
+def _problem(seed, n, d, pos_frac):
+    rng = np.random.default_rng(seed)
+    vmax = rng.choice(RANGES, size=d)  # per-column maxima: several range groups
+    X = np.floor(rng.random((n, d)) * (vmax + 1)).astype(np.uint8)
+    X[0], X[1] = 0, vmax  # every column spans exactly [0, vmax]
+    y = np.where(rng.random(n) < pos_frac, 1, -1).astype(np.int32)
+    y[0], y[1] = 1, -1
+    return X, y
+
+
+problems = st.tuples(st.integers(0, 2**31 - 1), st.integers(200, 3000), st.integers(4, 96),
+                     st.floats(0.1, 0.9), st.sampled_from([1.0, 10.0, 100.0]),
+                     st.sampled_from([0.00125, 0.01, 0.05]))
+
+
+@SETTINGS
+@given(problems)
+def test_device_decomposition_equals_the_oracle_on_random_integer_data(prob):
+    seed, n, d, pos, Cb, gamma = prob
+    X, y = _problem(seed, n, d, pos)
+    p = SVMParams(C=Cb, gamma=gamma)
+    Xu = D.upload_u8(X, DEV)
+    mmd = torch.empty(2 * d, dtype=torch.float64, device=DEV)
+    mn, mx = D.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    mn_h, mx_h = mm[:d].copy(), mm[d:].copy()
+    K = D.rbf_gram_u8(Xu, gamma, mn_h, mx_h)
+    assert K is not None, "no exact-integer plan for integer data with these ranges"
+    Kh = np.ascontiguousarray(K[:n, :n].cpu().numpy())
+    del K
+    D.release_gram_buffers()
+    Xs = (X.astype(np.float64) - mn_h) / np.where(mx_h - mn_h < 1e-12, 1.0, mx_h - mn_h)
+    Kr = C.rbf_matrix(Xs, Xs, gamma, 8)  # the reference's direct sum of squared differences
+    assert np.max(np.abs(Kh - Kr)) <= 1e-14
+    yd = torch.from_numpy(y).to(DEV)
+    alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+    out = D.train_decomp(Xu, yd, alpha, p, mn_h, mx_h)
+    assert out is not None
+    res, _ = out
+    a_o, r_o, _, _ = C.decomp_train_gram(Kh, y, p.replace(n_threads=8))
+    np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
+    assert (res.b, res.iterations, res.stop_reason) == (r_o.b, r_o.iterations, r_o.stop_reason)
+    if res.stop_reason == "converged":
+        pw = SVC(C=Cb, gamma=gamma, device="cuda:0", solver="smo").fit(X, y)
+        assert pw.stop_reason_ == "converged"
+        a = pw.alpha_
+        f = Kh @ (a * y) - y
+        hi = ((y == 1) & (a < Cb - p.eps)) | ((y == -1) & (a > p.eps))
+        lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < Cb - p.eps))
+        assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-9
