@@ -68,7 +68,12 @@ def test_device_decomposition_equals_the_oracle_on_random_integer_data(prob):
     assert (res.b, res.iterations, res.stop_reason) == (r_o.b, r_o.iterations, r_o.stop_reason)
     if res.stop_reason == "converged":
         pw = SVC(C=Cb, gamma=gamma, device="cuda:0", solver="smo").fit(X, y)
-        assert pw.stop_reason_ == "converged"
+        # first-order pairwise SMO can need far more than the reference's 100,000-iteration cap where the
+        # decomposition's second-order inner choice converges (e.g. n = 200, d = 4, C = 10, gamma = 0.05:
+        # 208,806 iterations on the CPU oracle): then the cap is the reported reason
+        assert pw.stop_reason_ in ("converged", "max_iter")
+        if pw.stop_reason_ != "converged":
+            return
         a = pw.alpha_
         f = Kh @ (a * y) - y
         hi = ((y == 1) & (a < Cb - p.eps)) | ((y == -1) & (a > p.eps))
