@@ -79,3 +79,25 @@ def test_device_decomposition_equals_the_oracle_on_random_integer_data(prob):
         hi = ((y == 1) & (a < Cb - p.eps)) | ((y == -1) & (a > p.eps))
         lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < Cb - p.eps))
         assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-9
+
+
+@SETTINGS
+@given(problems)
+def test_device_pairwise_solver_equals_the_oracle_on_random_integer_data(prob):
+    """The reference's pairwise trajectory on the device (``SVC(solver="smo")``, resident Gram) is the CPU
+    pairwise oracle's bit for bit on the device's kernel values -- also when both end on the cap."""
+    seed, n, d, pos, Cb, gamma = prob
+    X, y = _problem(seed, n, d, pos)
+    p = SVMParams(C=Cb, gamma=gamma)
+    Xu = D.upload_u8(X, DEV)
+    mmd = torch.empty(2 * d, dtype=torch.float64, device=DEV)
+    mn, mx = D.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    K = D.rbf_gram_u8(Xu, gamma, mm[:d].copy(), mm[d:].copy())
+    Kh = np.ascontiguousarray(K[:n, :n].cpu().numpy())
+    del K
+    D.release_gram_buffers()
+    pw = SVC(C=Cb, gamma=gamma, device="cuda:0", solver="smo").fit(X, y)
+    a_o, r_o, _ = C.smo_train_gram(Kh, y, p.replace(n_threads=8))
+    np.testing.assert_array_equal(pw.alpha_, a_o)
+    assert (pw.b_, pw.n_iter_, pw.stop_reason_) == (r_o.b, r_o.iterations, r_o.stop_reason)
