@@ -101,3 +101,31 @@ def test_device_pairwise_solver_equals_the_oracle_on_random_integer_data(prob):
     a_o, r_o, _ = C.smo_train_gram(Kh, y, p.replace(n_threads=8))
     np.testing.assert_array_equal(pw.alpha_, a_o)
     assert (pw.b_, pw.n_iter_, pw.stop_reason_) == (r_o.b, r_o.iterations, r_o.stop_reason)
+
+
+@SETTINGS
+@given(st.tuples(st.integers(0, 2**31 - 1), st.integers(200, 2500), st.integers(2, 64), st.floats(0.2, 0.8),
+                 st.sampled_from([1.0, 10.0]), st.sampled_from([0.01, 0.1, 1.0])))
+def test_real_valued_rows_end_on_the_stop_test(prob):
+    """Real-valued rows (no exact-integer plan): the default GPU solver (the decomposition on FP64-MFMA
+    kernel values) ends on the stop test recomputed from the reference's FP64 RBF of the scaled rows."""
+    seed, n, d, pos, Cb, gamma = prob
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, d)) * rng.uniform(0.1, 10.0, size=d)
+    y = np.where(rng.random(n) < pos, 1, -1).astype(np.int32)
+    y[0], y[1] = 1, -1
+    m = SVC(C=Cb, gamma=gamma, device="cuda:0").fit(X, y)
+    assert m.timings_["solver"] == "decomp" and m.timings_["gram_path"] == "fp64"
+    assert m.stop_reason_ in ("converged", "max_iter")
+    if m.stop_reason_ != "converged":
+        return
+    rng_ = np.where(X.max(0) - X.min(0) < 1e-12, 1.0, X.max(0) - X.min(0))
+    Xs = (X - X.min(0)) / rng_
+    K = C.rbf_matrix(Xs, Xs, gamma, 8)
+    a, yf, p = m.alpha_, y.astype(np.float64), m.params
+    f = K @ (a * yf) - yf
+    hi = ((yf == 1) & (a < Cb - p.eps)) | ((yf == -1) & (a > p.eps))
+    lo = ((yf == 1) & (a > p.eps)) | ((yf == -1) & (a < Cb - p.eps))
+    # FP64-MFMA kernel values differ from the direct sum by a few ulps: allow their effect on f
+    assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-8 * max(1.0, float(np.abs(a).sum()))
+    assert np.all((a >= -1e-9) & (a <= Cb + 1e-9)) and abs(float(a @ yf)) <= 1e-9 * max(1.0, float(a.sum()))
