@@ -3,6 +3,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <vector>
 
 #include "ctx.h"
@@ -58,6 +60,14 @@ int tu_warm_igram(hipStream_t s);
 int tu_warm_prep_kernels(hipStream_t s);
 int tu_warm_rowcache(hipStream_t s);
 int tu_warm_smo(hipStream_t s);
+// The first context of the process on `device` (the code objects and the copy engine are the device's,
+// not the context's: later contexts -- thread ranks, a one-vs-rest pool -- skip the warm-ups).
+static bool first_context_on(int device) {
+  static std::mutex mu;
+  static std::set<int> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  return seen.insert(device).second;
+}
 int tu_warm_all(hipStream_t s) {
   int bad = 0;
   for (auto fn : {tu_warm_capi, tu_warm_cascade_dev, tu_warm_decomp, tu_warm_dsmo, tu_warm_gram_mfma, tu_warm_igram,
@@ -138,9 +148,11 @@ SVM_API void* svmd_create(int32_t device) {
     return nullptr;
   }
   // Pay the one-time costs here, not inside the first solve: load every code object of the library
-  // (one launch per translation unit), and allocate the pinned state block and a small solver
-  // workspace (grown on demand).
-  if (warm_copy_engine(ctx) != SVM_OK || tu_warm_all(ctx->stream) != 0 || hipGetLastError() != hipSuccess ||
+  // (one launch per translation unit) and set up the copy engine -- once per device and process --, and
+  // allocate the pinned state block and a small solver workspace (grown on demand).
+  const bool first = first_context_on(device);
+  if ((first && warm_copy_engine(ctx) != SVM_OK) || (first && tu_warm_all(ctx->stream) != 0) ||
+      hipGetLastError() != hipSuccess ||
       ctx->ensure_pinned(size_t(1) << 16) != SVM_OK ||
       ctx->ensure_ws(size_t(16) << 20) != SVM_OK || hipStreamSynchronize(ctx->stream) != hipSuccess) {
     set_error("svmd_create: warm-up on device %d failed", device);
