@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/r5ab
 export TMPDIR=/tmp
-for k in 1 2; do
-  timeout -k 10 300 python -u scripts/ovr_decomp_probe.py 60000 > gpurun_out/r5ab/ovr$k.txt 2>&1 || exit $?
-  grep -E "^decomp|^batched" gpurun_out/r5ab/ovr$k.txt
+for k in 1; do
+  timeout -k 10 300 python -u scripts/ovr_workers_probe.py > gpurun_out/r5ab/ovr$k.txt 2>&1 || exit $?
+  grep workers gpurun_out/r5ab/ovr$k.txt
 done
