@@ -18,7 +18,7 @@ mmd = torch.empty(2 * tr.d, dtype=torch.float64, device=dev)
 mn, mx = D.minmax_u8(Xu, out=mmd)
 mm = mmd.cpu().numpy()
 rng = np.random.default_rng(1)
-for m in (64, 128, 192, 320, 512):
+for m in (64, 128, 160, 192, 320, 512):
     cols = np.sort(rng.choice(60000, size=m, replace=False)).astype(np.int32)
     coef = rng.uniform(-1, 1, size=m)
     for _ in range(6):
