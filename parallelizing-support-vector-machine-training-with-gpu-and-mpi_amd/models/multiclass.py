@@ -339,6 +339,96 @@ class OneVsRestSVC:
         self.n_iter_ = np.asarray(iters)
         self.stop_reasons_ = list(stops)
 
+    # ------------------------------------------------------------------ persistence
+    def _host_sv_rows(self) -> np.ndarray:
+        """The union support vectors' scaled rows on the host (from the device model after a GPU fit)."""
+        if self._dev_model is not None:
+            dm = self._dev_model
+            return np.ascontiguousarray(dm["Xs"][:, : dm["d"]].cpu().numpy())
+        return np.ascontiguousarray(self.support_vectors_)
+
+    def save(self, directory) -> None:
+        """One directory per class with the reference's model files (``final_sv_ids.txt``,
+        ``final_sv_labels.txt``, ``final_sv_alphas.txt``, ``final_b.txt``: the class's nonzero dual
+        coefficients over the union of support vectors, ids = training rows), plus the union's scaled rows
+        (``sv_rows.npy``), the scaler (``scaler.npz``) and ``ovr.json`` -- pickle-free throughout."""
+        import json
+        from pathlib import Path
+
+        from .model_io import save_model
+
+        d = Path(directory)
+        d.mkdir(parents=True, exist_ok=True)
+        np.save(d / "sv_rows.npy", self._host_sv_rows(), allow_pickle=False)
+        np.save(d / "support.npy", np.ascontiguousarray(self.support_, dtype=np.int64), allow_pickle=False)
+        if self.scaler_ is not None:
+            np.savez(d / "scaler.npz", min=self.scaler_.min_, max=self.scaler_.max_)
+        for c, label in enumerate(self.classes_):
+            coef = self.dual_coef_[:, c]
+            nz = np.flatnonzero(coef != 0.0)
+            save_model(d / f"class_{label}", ids=self.support_[nz], labels=np.where(coef[nz] > 0, 1, -1),
+                       alphas=np.abs(coef[nz]), b=float(self.intercepts_b_[c]), params=self.params,
+                       meta={"class": int(label), "n_iter": int(self.n_iter_[c]), "stop_reason": self.stop_reasons_[c]})
+        (d / "ovr.json").write_text(json.dumps({"format": "svm355-ovr-v1", "classes": [int(x) for x in self.classes_],
+                                                "n_sv_union": int(len(self.support_)), "params": self.params.as_dict()},
+                                               indent=2))
+
+    @classmethod
+    def load(cls, directory, device: str = "cpu") -> "OneVsRestSVC":
+        """The model ``save`` wrote; ``device`` "cuda[:k]" keeps the SV rows on that GPU for prediction."""
+        import json
+        from pathlib import Path
+
+        from ..utils.config import SVMParams
+        from .model_io import load_model
+
+        d = Path(directory)
+        info = json.loads((d / "ovr.json").read_text())
+        p = SVMParams(**info["params"])
+        m = cls(C=p.C, gamma=p.gamma, tol=p.tau, eps=p.eps, sv_tol=p.sv_tol, max_iter=p.max_iter, device=device,
+                wss="second" if p.wss == 2 else "first")
+        m.classes_ = np.array(info["classes"])
+        m.support_ = np.load(d / "support.npy", allow_pickle=False)
+        m.support_vectors_ = np.load(d / "sv_rows.npy", allow_pickle=False)
+        m.scaler_ = None
+        if (d / "scaler.npz").exists():
+            z = np.load(d / "scaler.npz", allow_pickle=False)
+            m.scaler_ = MinMaxScaler(z["min"], z["max"])
+        coef = np.zeros((len(m.support_), len(m.classes_)))
+        bs, iters, stops = [], [], []
+        for c, label in enumerate(m.classes_):
+            mc = load_model(d / f"class_{label}")
+            pos = np.searchsorted(m.support_, mc["ids"])
+            if len(pos) and (pos.max() >= len(m.support_) or np.any(m.support_[pos] != mc["ids"])):
+                raise ValueError(f"class {label}: support vector ids outside the saved union")
+            coef[pos, c] = mc["alphas"] * mc["labels"]
+            bs.append(mc["b"])
+            meta = json.loads((d / f"class_{label}" / "model.json").read_text()).get("meta", {})
+            iters.append(int(meta.get("n_iter", 0)))
+            stops.append(meta.get("stop_reason", ""))
+        m.dual_coef_ = coef
+        m.intercepts_b_ = np.asarray(bs, dtype=np.float64)
+        m.n_iter_ = np.asarray(iters)
+        m.stop_reasons_ = stops
+        m._dev_model = None
+        if m._dev() != "cpu":
+            if m.scaler_ is None:
+                raise ValueError("a device model needs the saved scaler (scaler.npz)")
+            import torch
+
+            from ..ops import device as D
+
+            dev = torch.device(m._dev())
+            k, dd = m.support_vectors_.shape
+            Xs = D.upload_rows(m.support_vectors_, dev)
+            mm = np.concatenate([m.scaler_.min_, m.scaler_.max_]).astype(np.float64)
+            mmd = torch.from_numpy(mm).to(dev)
+            m._dev_model = {"Xs": Xs, "ns": D.row_norms(Xs, dd),
+                            "coef": torch.from_numpy(np.ascontiguousarray(coef)).to(dev),
+                            "b": torch.tensor(m.intercepts_b_, dtype=torch.float64, device=dev),
+                            "mn": mmd[:dd], "mx": mmd[dd:], "d": dd, "device": dev}
+        return m
+
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
         """(m, classes) decision values sum_k coef_kc K(x, sv_k) - b_c."""

@@ -757,6 +757,28 @@ def test_ovr_decomposition_equals_its_oracle_per_class(dev):
     assert float(np.mean(g.predict(te.compact().X) == p.predict(te.compact().X))) >= 0.995
 
 
+def test_ovr_device_model_save_load(dev, tmp_path):
+    """A GPU one-vs-rest fit saved and loaded back onto the GPU (and onto the CPU) predicts the same labels;
+    the coefficients, b and support ids survive the reference's text files bit for bit."""
+    from svm355 import OneVsRestSVC
+
+    tr = synthetic_mnist(2000, seed=37)
+    te = synthetic_mnist(400, seed=37, offset=2000)
+    X, Xt = tr.compact().X, te.compact().X
+    m = OneVsRestSVC(device="cuda:0").fit(X, tr.labels)
+    m.save(tmp_path / "ovr")
+    g = OneVsRestSVC.load(tmp_path / "ovr", device="cuda:0")
+    c = OneVsRestSVC.load(tmp_path / "ovr", device="cpu")
+    for r in (g, c):
+        np.testing.assert_array_equal(r.support_, m.support_)
+        np.testing.assert_array_equal(r.dual_coef_, m.dual_coef_)
+        np.testing.assert_array_equal(r.intercepts_b_, m.intercepts_b_)
+    p = m.predict(Xt)
+    np.testing.assert_array_equal(g.predict(Xt), p)
+    assert float(np.mean(c.predict(Xt) == p)) >= 0.999
+    np.testing.assert_allclose(g.decision_function(Xt), m.decision_function(Xt), rtol=0, atol=1e-12)
+
+
 def test_gram_epilogue_exp_is_bit_identical_to_libm(dev):
     """The Gram kernel's batched exp (SGPR-sourced FMAs, igram.hip exp_batch) must equal the device
     libm exp bit for bit, so the Gram -- and every SMO trajectory -- is unchanged by it."""

@@ -81,3 +81,22 @@ def test_ovr_distributed_gloo_two_processes():
         np.testing.assert_array_equal(coef, one.dual_coef_)
         np.testing.assert_array_equal(b, one.intercepts_b_)
         assert st == one.stop_reasons_
+
+
+def test_ovr_save_load_roundtrip(tmp_path):
+    """OneVsRestSVC.save writes the reference's four model files per class (pickle-free extras beside
+    them); load gives back the same decision values and predictions."""
+    tr = synthetic_mnist(700, seed=5)
+    te = synthetic_mnist(200, seed=5, offset=700)
+    m = OneVsRestSVC(device="cpu", n_threads=2).fit(tr.X, tr.labels)
+    m.save(tmp_path / "ovr")
+    for c in m.classes_:
+        for f in ("final_sv_ids.txt", "final_sv_labels.txt", "final_sv_alphas.txt", "final_b.txt"):
+            assert (tmp_path / "ovr" / f"class_{c}" / f).exists()
+    r = OneVsRestSVC.load(tmp_path / "ovr")
+    np.testing.assert_array_equal(r.classes_, m.classes_)
+    np.testing.assert_array_equal(r.support_, m.support_)
+    np.testing.assert_array_equal(r.dual_coef_, m.dual_coef_)
+    np.testing.assert_array_equal(r.intercepts_b_, m.intercepts_b_)
+    np.testing.assert_array_equal(r.decision_function(te.X), m.decision_function(te.X))
+    np.testing.assert_array_equal(r.predict(te.X), m.predict(te.X))
