@@ -397,6 +397,7 @@ def _multiclass(argv) -> int:
                          "decomposition solver per class with no Gram (decomp)")
     ap.add_argument("--gpus", type=int, default=0, help="launch torchrun with this many ranks (classes dealt over them)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--model-dir", default=None, help="save the model (one directory of reference model files per class)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
     if "RANK" not in os.environ and a.gpus > 1:
@@ -445,6 +446,8 @@ def _multiclass(argv) -> int:
         print(f"[rank 0] union SV count = {len(model.support_)}, iterations per class = {model.n_iter_.tolist()}")
         print(f"[rank 0] Test accuracy = {acc}")
         print(f"[rank 0] training time = {int((t1 - t0) * 1e3)} ms, prediction time = {int((t2 - t1) * 1e3)} ms")
+        if a.model_dir:
+            model.save(a.model_dir)
         if a.json:
             Path(a.json).write_text(json.dumps({
                 "program": "svm355 multiclass", "world": world, "n": tr.n, "classes": model.classes_.tolist(),

@@ -84,10 +84,14 @@ def test_native_cascade_rejects_non_power_of_two_tree():
 def test_cli_multiclass_two_ranks_gloo(tmp_path):
     js = tmp_path / "mc.json"
     out = _run(["multiclass", "--synthetic", "500,200", "--cpu", "--gpus", "2", "--backend", "gloo",
-                "--json", str(js)], tmp_path, timeout=600)
+                "--json", str(js), "--model-dir", str(tmp_path / "model")], tmp_path, timeout=600)
     assert "[rank 0] one-vs-rest over 10 classes on 2 rank(s)" in out
     s = json.loads(js.read_text())
     assert s["world"] == 2 and all(r == "converged" for r in s["stop_reasons"]) and s["accuracy"] > 0.8
+    from svm355 import OneVsRestSVC
+
+    m = OneVsRestSVC.load(tmp_path / "model")  # the distributed fit's model, saved by rank 0
+    assert len(m.classes_) == 10 and (tmp_path / "model" / "class_1" / "final_b.txt").exists()
 
 
 @pytest.mark.parametrize("topology", ["star", "tree"])
