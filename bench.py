@@ -290,7 +290,12 @@ def main(argv=None):
                 try:
                     m = DistributedDecompSVC(a.gpus, rank=crank).fit(pre.X, pre.y)
                     ref = SVC(device=str(dev), solver="decomp").fit(pre.X, pre.y)
-                    if not (m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)):
+                    if 8 % a.gpus == 0:  # the one-GPU block partition: the same trajectory bit for bit
+                        same = m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)
+                    else:  # another partition (a multiple of 8 x world blocks): another path to the same optimum
+                        same = (m.stop_reason_ == ref.stop_reason_ == "converged" and abs(m.b_ - ref.b_) <= 10 * ref.params.tau
+                                and abs(len(m.support_) - len(ref.support_)) <= max(2, len(ref.support_) // 100))
+                    if not same:
                         err = (f"preflight differs from the one-GPU solve (iterations {m.n_iter_} vs {ref.n_iter_}, "
                                f"b {m.b_!r} vs {ref.b_!r})")
                 except Exception as e:  # noqa: BLE001
@@ -641,6 +646,9 @@ def main(argv=None):
             if mode in ("smo", "decomp"):
                 extra["bit_identical_to_1gpu"] = bool(one.n_iter_ == model.n_iter_ and one.b_ == model.b_ and
                                                       np.array_equal(one.alpha_, model.alpha_))
+                if mode == "decomp" and 8 % a.gpus:  # a block partition of 8 x world blocks: another trajectory
+                    extra["bit_identity_expected"] = False
+                    extra["b_minus_1gpu_b"] = float(model.b_ - one.b_)
         if dist is not None:
             dist.barrier()
     if auto_selection is not None:

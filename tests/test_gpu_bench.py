@@ -119,6 +119,19 @@ def test_torchrun_processes_share_one_gpu_over_hostcomm(nproc, rows):
             assert abs(c["b_minus_headline_b"]) <= 10 * 1e-5
 
 
+def test_torchrun_world_not_dividing_8_converges_to_the_same_model():
+    """Three processes (a world that does not divide the 8-block grain): the selection's blocks are then
+    a multiple of 8 x world, another trajectory to the same optimum -- the preflight checks convergence,
+    b and the SV count instead of bit identity, and the line says so (bit_identity_expected false)."""
+    p, wall = _torchrun(3, "--parallel", "decomp", "--transport", "hostcomm", "--rows", "6000", "--test-rows", "500",
+                        "--steps", "1", "--warmup", "1", "--baseline-1gpu", "1", "--cascade-steps", "0")
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 3 and out["stop_reason"] == "converged" and out["bit_identity_expected"] is False
+    assert abs(out["b_minus_1gpu_b"]) <= 1e-4 and out["fallback_reason"] is None
+
+
 def test_torchrun_hostcomm_rank_failing_mid_solve_ends_every_process():
     """Rank 1 fails at outer iteration 3 of the distributed decomposition while rank 0 waits in its
     candidate all-gather: both processes exit non-zero and torchrun reports the failure, well within
