@@ -1,0 +1,67 @@
+"""Degenerate inputs on the GPU trainers (the default decomposition solver and the pairwise SMO): a single
+class, the smallest problems, constant and duplicate columns / rows, a single feature.  Each must end with
+a reported stop reason (never a fault or a hang) and, where the problem is well-posed, the stop test."""
+import numpy as np
+import pytest
+
+from svm355 import SVC
+
+pytestmark = pytest.mark.gpu
+
+
+def _gap(X, y, a, m):
+    Xs = m.scaler_.transform(X) if m.scaler_ is not None else X
+    sq = np.einsum("ij,ij->i", Xs, Xs)
+    K = np.exp(-m.params.gamma * np.maximum(sq[:, None] + sq[None, :] - 2.0 * Xs @ Xs.T, 0.0))
+    np.fill_diagonal(K, 1.0)
+    yf = y.astype(np.float64)
+    f = K @ (a * yf) - yf
+    C, eps = m.params.C, m.params.eps
+    hi = ((yf == 1) & (a < C - eps)) | ((yf == -1) & (a > eps))
+    lo = ((yf == 1) & (a > eps)) | ((yf == -1) & (a < C - eps))
+    return f[lo].max() - f[hi].min()
+
+
+@pytest.mark.parametrize("solver", ["decomp", "smo"])
+def test_single_class_reports_no_candidate(solver):
+    rng = np.random.default_rng(1)
+    X = rng.integers(0, 256, size=(300, 20)).astype(np.uint8)
+    y = -np.ones(300, dtype=np.int32)
+    m = SVC(device="cuda:0", solver=solver).fit(X, y)
+    assert m.stop_reason_ == "no_candidate"
+    assert np.all(m.alpha_ == 0.0)
+
+
+@pytest.mark.parametrize("solver", ["decomp", "smo"])
+@pytest.mark.parametrize("n", [2, 3, 17])
+def test_smallest_problems(solver, n):
+    rng = np.random.default_rng(n)
+    X = rng.integers(0, 256, size=(n, 5)).astype(np.uint8)
+    y = np.where(np.arange(n) % 2 == 0, 1, -1).astype(np.int32)
+    m = SVC(device="cuda:0", solver=solver).fit(X, y)
+    assert m.stop_reason_ == "converged"
+    assert _gap(X.astype(np.float64), y, m.alpha_, m) <= 2 * m.params.tau + 1e-9
+
+
+@pytest.mark.parametrize("solver", ["decomp", "smo"])
+def test_constant_and_duplicate_columns_and_rows(solver):
+    rng = np.random.default_rng(7)
+    X = rng.integers(0, 256, size=(1500, 40)).astype(np.uint8)
+    X[:, 3] = 17            # constant column (range 0: scaled to 0)
+    X[:, 9] = X[:, 8]       # duplicate column
+    X[100:200] = X[0:100]   # duplicate rows
+    y = np.where(X[:, 0].astype(int) + X[:, 1] > 255, 1, -1).astype(np.int32)
+    y[100:200] = y[0:100]
+    m = SVC(device="cuda:0", solver=solver).fit(X, y)
+    assert m.stop_reason_ == "converged"
+    assert _gap(X.astype(np.float64), y, m.alpha_, m) <= 2 * m.params.tau + 1e-9
+
+
+@pytest.mark.parametrize("solver", ["decomp", "smo"])
+def test_single_feature_real_valued(solver):
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((800, 1))
+    y = np.where(X[:, 0] + 0.3 * rng.standard_normal(800) > 0, 1, -1).astype(np.int32)
+    m = SVC(device="cuda:0", solver=solver, gamma=1.0, C=1.0).fit(X, y)
+    assert m.stop_reason_ == "converged"
+    assert _gap(X, y, m.alpha_, m) <= 2 * m.params.tau + 1e-8
