@@ -352,7 +352,8 @@ class Rank {
     Gathered g;
     g.counts = t_.allgather_i64(local.k);
     g.kmax = *std::max_element(g.counts.begin(), g.counts.end());
-    if (g.kmax == 0) return g;
+    if (t_.rank() == 0) g.ids.resize(size_t(t_.world()));  // one (possibly empty) id list per source
+    if (g.kmax == 0) return g;  // no rank has a support vector (e.g. every partition holds one class)
     pack_.ensure(g.kmax * w_ * 8);
     if (local.k) B_.pack(local, ld_, pack_.as<double>());
     const int64_t bytes = g.kmax * w_ * 8;
@@ -360,7 +361,6 @@ class Rank {
     if (root) recv_.ensure(bytes * t_.world());
     t_.gather(pack_.get(), bytes, root ? recv_.get() : nullptr, 0);
     if (root) {
-      g.ids.resize(size_t(t_.world()));
       std::vector<const double*> recs;
       std::vector<int64_t> ks;
       std::vector<int64_t*> outs;

@@ -185,3 +185,16 @@ def test_decomposition_solver_cascade(data, topology, world):
     assert abs(ra.b - rb.b) <= 10 * P2.tau
     assert len(set(ra.ids.tolist()) ^ set(rb.ids.tolist())) <= 2
     assert abs(a.score(te.X, te.y) - b.score(te.X, te.y)) <= 0.002
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+@pytest.mark.parametrize("solver", ["smo", "decomp"])
+def test_partitions_of_one_class_each(topology, solver):
+    """8 ranks on rows sorted by label: every partition holds one class, so no local solve finds a
+    violating pair and no rank has a support vector (the gather of empty sets once faulted on rank 0).
+    The cascade ends cleanly with an empty model, as the reference's rounds would."""
+    rng = np.random.default_rng(11)
+    X = rng.integers(0, 256, size=(24, 6)).astype(np.float64)
+    y = np.where(np.arange(24) < 12, 1, -1).astype(np.int32)
+    c = CascadeSVM(topology=topology, solver=solver).fit(X, y, world=8, device="cpu")
+    assert c.result.converged and len(c.result.ids) == 0 and c.result.b == 0.0

@@ -65,3 +65,30 @@ def test_single_feature_real_valued(solver):
     m = SVC(device="cuda:0", solver=solver, gamma=1.0, C=1.0).fit(X, y)
     assert m.stop_reason_ == "converged"
     assert _gap(X, y, m.alpha_, m) <= 2 * m.params.tau + 1e-8
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_cascade_with_tiny_single_class_partitions(topology):
+    """8 loopback ranks on 24 points sorted by label: every partition holds one class (no local solve
+    finds a violating pair, no rank has a support vector): the cascade ends cleanly with an empty model."""
+    from svm355.parallel.cascade import CascadeSVM
+
+    rng = np.random.default_rng(11)
+    X = rng.integers(0, 256, size=(24, 6)).astype(np.uint8)
+    y = np.where(np.arange(24) < 12, 1, -1).astype(np.int32)  # ranks 0-3 all +1, ranks 4-7 all -1
+    c = CascadeSVM(topology=topology).fit(X, y, world=8, device="cuda:0", transport="loopback")
+    assert c.result.converged and len(c.result.ids) == 0 and c.result.b == 0.0
+
+
+def test_distributed_decomposition_with_fewer_points_than_blocks():
+    """8 rehearsal ranks on 40 points (the 8-block grain leaves ranks with one small block each)."""
+    from svm355.parallel.decomp import DistributedDecompSVC
+
+    rng = np.random.default_rng(12)
+    X = rng.integers(0, 256, size=(40, 6)).astype(np.uint8)
+    y = np.where(rng.random(40) < 0.5, 1, -1).astype(np.int32)
+    y[0], y[1] = 1, -1
+    one = SVC(device="cuda:0", solver="decomp").fit(X, y)
+    m = DistributedDecompSVC(world=8, transport="loopback").fit(X, y)
+    assert m.stop_reason_ == one.stop_reason_ == "converged"
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
