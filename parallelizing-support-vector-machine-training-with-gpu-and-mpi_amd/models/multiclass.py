@@ -115,6 +115,7 @@ class OneVsRestSVC:
         X = np.ascontiguousarray(X, dtype=np.uint8 if (cuda and X.dtype == np.uint8) else np.float64)
         labels = np.asarray(labels)
         self.classes_ = np.array(sorted(set(labels.tolist())) if classes is None else classes)
+        self._n_pos = np.array([np.count_nonzero(labels == c) for c in self.classes_])  # per class
         t0 = time.perf_counter()
         if not cuda:
             self._fit_cpu(X, labels)
@@ -333,6 +334,14 @@ class OneVsRestSVC:
                          "smo_solver": "decomp"}
 
     def _finish(self, sup, coef_full, bs, iters, stops):
+        # a class absent from the labels (or covering them all) has no violating pair: its solve stops with
+        # no candidate and alpha = 0; make it the constant predictor -1 (or +1) instead of decision 0 - b = 0,
+        # which would outrank every real class whose decision values are negative
+        bs = list(bs)
+        n_rows = len(coef_full)
+        for c, pos in enumerate(self._n_pos):
+            if pos == 0 or pos == n_rows:
+                bs[c] = 1.0 if pos == 0 else -1.0
         self.support_ = sup
         self.dual_coef_ = np.ascontiguousarray(coef_full[sup])  # (n_sv_union, classes)
         self.intercepts_b_ = np.asarray(bs, dtype=np.float64)  # per-class b (decision = K coef - b)

@@ -100,3 +100,14 @@ def test_ovr_save_load_roundtrip(tmp_path):
     np.testing.assert_array_equal(r.intercepts_b_, m.intercepts_b_)
     np.testing.assert_array_equal(r.decision_function(te.X), m.decision_function(te.X))
     np.testing.assert_array_equal(r.predict(te.X), m.predict(te.X))
+
+
+def test_ovr_class_absent_from_the_labels_is_never_predicted():
+    """An explicitly requested class with no training rows: its solve stops with no candidate (alpha = 0)
+    and it becomes the constant predictor -1, so it never outranks the real classes."""
+    tr = synthetic_mnist(400, seed=9)
+    labels = np.where(tr.labels < 3, tr.labels, 2)  # classes 0, 1, 2 only
+    m = OneVsRestSVC(device="cpu", n_threads=2).fit(tr.X, labels, classes=[0, 1, 2, 7])
+    assert m.stop_reasons_[3] == "no_candidate" and m.intercepts_b_[3] == 1.0
+    assert np.all(m.decision_function(tr.X)[:, 3] == -1.0)
+    assert 7 not in set(m.predict(tr.X).tolist())
