@@ -10,6 +10,7 @@
 // split into lines, and parsed in parallel with std::from_chars (same values as std::stod for
 // decimal input).
 #include <charconv>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -66,7 +67,7 @@ bool parse_double(const char* s, const char* e, double& v) {
   s = skip_ws(s, e);
   if (s < e && *s == '+') ++s;
   auto r = std::from_chars(s, e, v);
-  return r.ec == std::errc();
+  return r.ec == std::errc() && std::isfinite(v);  // "nan" / "inf" cells: rejected, not trained on
 }
 
 bool parse_int(const char* s, const char* e, int32_t& v) {
@@ -229,7 +230,7 @@ SVM_API void* svm_csv_load(const char* path, int64_t limit, int32_t positive_lab
   }
   for (int32_t w = 0; w < nt; ++w) {
     if (err_line[size_t(w)] >= 0) {
-      set_error("Error: malformed CSV line %lld in %s (expected %lld features + label)",
+      set_error("Error: malformed CSV line %lld in %s (expected %lld finite features + label)",
                 (long long)err_line[size_t(w)], path, (long long)d);
       return nullptr;
     }

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <string>
+#include <vector>
 #include <sys/stat.h>
 
 #include "internal.h"
@@ -26,13 +27,17 @@ SVM_API int svm_minmax(const double* X, int64_t n, int64_t d, double* mn, double
     mx[j] = X[j];
   }
   // Row-outer order (cache friendly); min/max are order independent so results are identical.
+  std::vector<char> nan(static_cast<size_t>(d), 0);  // std::min / max drop a NaN that is not the seed
   for (int64_t i = 0; i < n; ++i) {
     const double* r = X + i * d;
     for (int64_t j = 0; j < d; ++j) {
       mn[j] = std::min(mn[j], r[j]);
       mx[j] = std::max(mx[j], r[j]);
+      nan[size_t(j)] |= r[j] != r[j];
     }
   }
+  for (int64_t j = 0; j < d; ++j)  // a NaN anywhere in a column: both bounds NaN (callers reject them)
+    if (nan[size_t(j)]) mn[j] = mx[j] = std::nan("");
   return SVM_OK;
 }
 

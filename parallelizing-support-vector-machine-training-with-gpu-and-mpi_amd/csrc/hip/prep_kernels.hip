@@ -22,13 +22,16 @@ __global__ __launch_bounds__(256) void minmax_partial_kernel(const double* __res
   const int64_t c = int64_t(blockIdx.x) * kColsPerBlock + lane;
   const int64_t rstride = int64_t(gridDim.y) * kRowLanes;
   double lo = __builtin_inf(), hi = -__builtin_inf();
+  bool nan = false;  // fmin / fmax drop NaN: a NaN anywhere in the column makes both of its bounds NaN
   if (c < d) {
     for (int64_t r = int64_t(blockIdx.y) * kRowLanes + wv; r < n; r += rstride) {
       const double v = X[r * ld + c];
       lo = fmin(lo, v);
       hi = fmax(hi, v);
+      nan |= v != v;
     }
   }
+  if (nan) lo = hi = __builtin_nan("");
   __shared__ double smin[kRowLanes][kColsPerBlock], smax[kRowLanes][kColsPerBlock];
   smin[wv][lane] = lo;
   smax[wv][lane] = hi;
@@ -36,9 +39,11 @@ __global__ __launch_bounds__(256) void minmax_partial_kernel(const double* __res
   if (wv == 0 && c < d) {
 #pragma unroll
     for (int w = 1; w < kRowLanes; ++w) {
+      nan |= smin[w][lane] != smin[w][lane] || lo != lo;
       lo = fmin(lo, smin[w][lane]);
       hi = fmax(hi, smax[w][lane]);
     }
+    if (nan) lo = hi = __builtin_nan("");
     pmin[int64_t(blockIdx.y) * d + c] = lo;
     pmax[int64_t(blockIdx.y) * d + c] = hi;
   }
@@ -51,6 +56,7 @@ __global__ __launch_bounds__(256) void minmax_final_kernel(const double* __restr
   const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= d) return;
   double lo = pmin[c], hi = pmax[c];
+  bool nan = lo != lo;  // a NaN partial (a NaN in the column) stays NaN: fmin / fmax would drop it
   // 8 partials' loads in flight ahead of the in-order folds (same order, same result)
   int p = 1;
   for (; p + 8 <= parts; p += 8) {
@@ -62,16 +68,19 @@ __global__ __launch_bounds__(256) void minmax_final_kernel(const double* __restr
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
+      nan |= a[u] != a[u];
       lo = fmin(lo, a[u]);
       hi = fmax(hi, z[u]);
     }
   }
   for (; p < parts; ++p) {
-    lo = fmin(lo, pmin[int64_t(p) * d + c]);
+    const double a = pmin[int64_t(p) * d + c];
+    nan |= a != a;
+    lo = fmin(lo, a);
     hi = fmax(hi, pmax[int64_t(p) * d + c]);
   }
-  mn[c] = lo;
-  mx[c] = hi;
+  mn[c] = nan ? __builtin_nan("") : lo;
+  mx[c] = nan ? __builtin_nan("") : hi;
 }
 
 // One wave per row.  mn == nullptr -> norms only.

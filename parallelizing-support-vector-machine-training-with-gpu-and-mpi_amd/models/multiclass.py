@@ -36,7 +36,7 @@ from typing import List, Optional
 import numpy as np
 
 from ..utils.config import SVMParams, default_threads
-from ..utils.data import MinMaxScaler
+from ..utils.data import MinMaxScaler, check_finite_bounds
 from ..utils.trace import trace_range
 
 
@@ -156,6 +156,7 @@ class OneVsRestSVC:
         from ..ops import cpu as C
 
         self.scaler_ = MinMaxScaler().fit(X)
+        check_finite_bounds(self.scaler_.min_, self.scaler_.max_)
         Xs = self.scaler_.transform(X)
         K = C.rbf_matrix(Xs, Xs, self.params.gamma, self.params.n_threads)
         ys = self._ys(labels)
@@ -199,7 +200,7 @@ class OneVsRestSVC:
             t0 = time.perf_counter()
             Xd = D.upload_rows(X, device)
             mn, mx, sqn = D.minmax_scale_(Xd, d)
-            torch.cuda.synchronize(device)
+            check_finite_bounds(mn.cpu().numpy(), mx.cpu().numpy())
             t1 = time.perf_counter()
             K, path = D.rbf_gram_sym(Xd, sqn, self.params.gamma, mn=mn, mx=mx, gram=self.gram,
                                      out=D.gram_buffer(X.shape[0], device))
@@ -280,6 +281,7 @@ class OneVsRestSVC:
         else:
             Xd = D.upload_rows(X, device)
             mn, mx, sqn = D.minmax_scale_(Xd, d)
+            check_finite_bounds(mn.cpu().numpy(), mx.cpu().numpy())
             rows = Xd
         mm = torch.cat([mn, mx]).cpu().numpy()
         mn_h, mx_h = mm[:d].copy(), mm[d:].copy()

@@ -25,7 +25,7 @@ from typing import Optional
 import numpy as np
 
 from ..utils.config import SVMParams, default_threads
-from ..utils.data import MinMaxScaler
+from ..utils.data import MinMaxScaler, check_finite_bounds
 
 
 def _resolve_device(device: str) -> str:
@@ -105,8 +105,11 @@ class SVC:
             raise ValueError("solver='decomp' runs on the GPU (device='cuda'); the CPU oracle is the pairwise SMO")
         if self.scale:
             self.scaler_ = MinMaxScaler().fit(X)
+            check_finite_bounds(self.scaler_.min_, self.scaler_.max_)
             Xs = self.scaler_.transform(X)
         else:
+            if not np.all(np.isfinite(X)):
+                raise ValueError("X holds NaN or infinite values")
             self.scaler_ = None
             Xs = X
         alpha, res, _ = C.smo_train(Xs, y, self.params, alpha=alpha0, warm=alpha0 is not None)
@@ -145,9 +148,13 @@ class SVC:
         d = X.shape[1]
         if self.scale:
             mn, mx, sqn = D.minmax_scale_(Xd, d)
+            mm_h = mn.as_strided((2 * d,), (1,)).cpu().numpy()  # both bounds (one buffer), one copy
+            check_finite_bounds(mm_h[:d], mm_h[d:])
         else:
             mn = mx = None
             sqn = D.row_norms(Xd, d)
+            if not np.all(np.isfinite(sqn.cpu().numpy())):  # a NaN / inf anywhere makes its row's norm one
+                raise ValueError("X holds NaN or infinite values")
         if alpha0 is not None:
             alpha = torch.from_numpy(np.ascontiguousarray(alpha0, dtype=np.float64)).to(device)
         else:
@@ -156,7 +163,7 @@ class SVC:
         t1 = time.perf_counter()
         out = None
         if decomp:
-            out = D.train_decomp_rows(Xd, yd, alpha, self.params, mn, mx, working_set=self.working_set,
+            out = D.train_decomp_rows(Xd, yd, alpha, self.params, mm_h[:d], mm_h[d:], working_set=self.working_set,
                                       warm=alpha0 is not None)
             if out is None and self.solver == "decomp":
                 raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16, n is beyond the "
@@ -180,7 +187,7 @@ class SVC:
             "device": device,
         }
         if self.scale:
-            self.scaler_ = MinMaxScaler(mn.cpu().numpy(), mx.cpu().numpy())
+            self.scaler_ = MinMaxScaler(mm_h[:d].copy(), mm_h[d:].copy())
         else:
             self.scaler_ = None
         self._sv_host = None  # scaled SV rows stay on the device; copied to the host on first access

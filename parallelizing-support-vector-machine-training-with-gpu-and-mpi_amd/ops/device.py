@@ -164,9 +164,9 @@ def minmax_scale_(X: torch.Tensor, d: int, mn: Optional[torch.Tensor] = None,
     ctx = _ctx_for(X)
     n = X.shape[0]
     use_given = mn is not None
-    if not use_given:
-        mn = torch.empty(d, dtype=torch.float64, device=X.device)
-        mx = torch.empty(d, dtype=torch.float64, device=X.device)
+    if not use_given:  # one buffer: the caller reads both bounds back with one copy (torch.cat-free)
+        mm = torch.empty(2 * d, dtype=torch.float64, device=X.device)
+        mn, mx = mm[:d], mm[d:]
     sqn = torch.empty(n, dtype=torch.float64, device=X.device)
     N.check(ctx.lib.svmd_preprocess(ctx.bind(), N.ptr(X), n, d, X.shape[1], N.ptr(mn), N.ptr(mx), N.ptr(sqn),
                                     int(use_given)), "svmd_preprocess")

@@ -74,6 +74,17 @@ def check_labels(y, n: int) -> np.ndarray:
     return y.astype(np.int32, copy=False)
 
 
+def check_finite_bounds(mn, mx) -> None:
+    """ValueError when a column's min / max is NaN or infinite, i.e. the rows hold a NaN or an infinity
+    (numpy's and the device's column bounds propagate NaN): a fit would otherwise find no violating pair
+    and return an empty model without saying why."""
+    bounds = np.concatenate([np.asarray(mn, dtype=np.float64).ravel(), np.asarray(mx, dtype=np.float64).ravel()])
+    if not np.all(np.isfinite(bounds)):
+        d = np.asarray(mn).size
+        bad = sorted({int(j) for j in np.flatnonzero(~np.isfinite(bounds)) % max(d, 1)})[:8]
+        raise ValueError(f"X holds NaN or infinite values (columns {bad}{' ...' if len(bad) == 8 else ''})")
+
+
 def pixel_rows(X, what: str) -> np.ndarray:
     """X as C-contiguous uint8 (n, d) when every value is an integer in [0, 255]; ValueError naming
     `what` otherwise (never a silent cast: 3.7 or 300 would be truncated or wrapped)."""

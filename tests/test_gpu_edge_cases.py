@@ -92,3 +92,22 @@ def test_distributed_decomposition_with_fewer_points_than_blocks():
     m = DistributedDecompSVC(world=8, transport="loopback").fit(X, y)
     assert m.stop_reason_ == one.stop_reason_ == "converged"
     np.testing.assert_array_equal(m.alpha_, one.alpha_)
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf])
+def test_non_finite_rows_are_rejected_on_the_gpu(bad):
+    """FP64 rows with a NaN or an infinity: the device column bounds propagate NaN (fmin / fmax alone
+    would drop it), and the fit raises instead of returning an empty model."""
+    from svm355 import OneVsRestSVC
+
+    rng = np.random.default_rng(5)
+    X = rng.random((3000, 12))
+    X[1234, 7] = bad
+    y = np.where(rng.random(3000) < 0.5, 1, -1).astype(np.int32)
+    for solver in ("decomp", "smo"):
+        with pytest.raises(ValueError, match="NaN or infinite"):
+            SVC(device="cuda:0", solver=solver).fit(X, y)
+    with pytest.raises(ValueError, match="NaN or infinite"):
+        OneVsRestSVC(device="cuda:0").fit(X, rng.integers(0, 3, size=3000))
+    with pytest.raises(ValueError, match="NaN or infinite"):
+        OneVsRestSVC(device="cuda:0", solver="batched").fit(X, rng.integers(0, 3, size=3000))

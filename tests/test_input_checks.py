@@ -72,3 +72,29 @@ def test_dsmo_rank_agrees_on_a_bad_input_before_any_solve():
     finally:
         dist.destroy_process_group()
 
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
+def test_non_finite_rows_are_rejected_on_the_cpu(bad):
+    """A NaN or an infinity in X: a clear error, not an empty model (the column bounds propagate NaN)."""
+    from svm355 import SVC, OneVsRestSVC
+
+    rng = np.random.default_rng(2)
+    X = rng.random((120, 6))
+    X[37, 4] = bad
+    y = np.where(rng.random(120) < 0.5, 1, -1).astype(np.int32)
+    with pytest.raises(ValueError, match="NaN or infinite"):
+        SVC(device="cpu").fit(X, y)
+    with pytest.raises(ValueError, match="NaN or infinite"):
+        SVC(device="cpu", scale=False).fit(X, y)
+    with pytest.raises(ValueError, match="NaN or infinite"):
+        OneVsRestSVC(device="cpu").fit(X, rng.integers(0, 3, size=120))
+
+
+def test_non_finite_csv_cell_is_a_malformed_line(tmp_path):
+    from svm355.utils.data import load_csv
+
+    p = tmp_path / "d.csv"
+    p.write_text("f0,f1,label\n0.5,1.0,1\n0.25,nan,0\n")
+    with pytest.raises(FileNotFoundError, match="malformed CSV line 3"):  # load_csv's error type (test_data.py)
+        load_csv(p)
