@@ -443,6 +443,10 @@ class OneVsRestSVC:
     # ------------------------------------------------------------------ inference
     def decision_function(self, X: np.ndarray) -> np.ndarray:
         """(m, classes) decision values sum_k coef_kc K(x, sv_k) - b_c."""
+        d = (int(self._dev_model["d"]) if self._dev_model is not None else
+             int(np.size(self.scaler_.min_)) if self.scaler_ is not None else int(np.shape(self.support_vectors_)[1]))
+        if np.ndim(X) != 2 or np.shape(X)[1] != d:
+            raise ValueError(f"X must be (m, {d}) like the training rows, got shape {np.shape(X)}")
         X = np.ascontiguousarray(X, dtype=np.uint8 if (self._dev_model is not None and X.dtype == np.uint8)
                                  else np.float64)
         if self._dev_model is not None:

@@ -250,7 +250,21 @@ class SVC:
         self._sv_host = value
 
     # ------------------------------------------------------------------ inference
+    def _n_features(self) -> Optional[int]:
+        if self._dev is not None:
+            return int(self._dev["d"])
+        if self.scaler_ is not None and self.scaler_.min_ is not None:
+            return int(np.size(self.scaler_.min_))
+        sv = self.support_vectors_
+        return int(sv.shape[1]) if sv is not None and np.ndim(sv) == 2 else None
+
+    def _check_X(self, X) -> None:
+        d = self._n_features()
+        if np.ndim(X) != 2 or (d is not None and np.shape(X)[1] != d):
+            raise ValueError(f"X must be (m, {d}) like the training rows, got shape {np.shape(X)}")
+
     def decision_function(self, X: np.ndarray) -> np.ndarray:
+        self._check_X(X)
         if self._dev is not None:
             return self._device_decision(X).cpu().numpy()
         return self._host_decision(X)
@@ -287,6 +301,7 @@ class SVC:
         if self._dev is not None and len(y):
             from ..ops import device as D
 
+            self._check_X(X)
             return D.count_correct(self._device_decision(X), y, self.zero_is_positive) / len(y)
         return float(np.mean(self.predict(X) == y))
 

@@ -98,3 +98,17 @@ def test_non_finite_csv_cell_is_a_malformed_line(tmp_path):
     p.write_text("f0,f1,label\n0.5,1.0,1\n0.25,nan,0\n")
     with pytest.raises(FileNotFoundError, match="malformed CSV line 3"):  # load_csv's error type (test_data.py)
         load_csv(p)
+
+
+def test_prediction_rows_must_have_the_training_width():
+    from svm355 import SVC, OneVsRestSVC
+
+    rng = np.random.default_rng(4)
+    X = rng.random((150, 5))
+    y = np.where(rng.random(150) < 0.5, 1, -1).astype(np.int32)
+    for m in (SVC(device="cpu").fit(X, y), OneVsRestSVC(device="cpu", n_threads=2).fit(X, rng.integers(0, 3, 150))):
+        with pytest.raises(ValueError, match=r"\(m, 5\)"):
+            m.predict(rng.random((10, 4)))
+        with pytest.raises(ValueError, match=r"\(m, 5\)"):
+            m.decision_function(rng.random(5))
+        assert m.predict(np.empty((0, 5))).shape == (0,)
