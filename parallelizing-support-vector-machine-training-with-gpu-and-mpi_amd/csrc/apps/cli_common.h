@@ -15,6 +15,7 @@
 //                    second-order choice of the second index (Fan, Chen & Lin 2005)
 #pragma once
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -113,6 +114,12 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
       usage(argv[0]);
       return false;
     }
+  }
+  const svm_params& q = o.p;  // as SVMParams.__post_init__: a well-posed problem or an error
+  if (!(q.C > 0) || !(q.gamma > 0) || !(q.tau > 0) || !(q.eps >= 0) || !(q.sv_tol >= 0) || q.max_iter < 1 ||
+      !std::isfinite(q.C) || !std::isfinite(q.gamma) || !std::isfinite(q.tau)) {
+    fprintf(stderr, "parameters out of range: C, gamma, tau > 0; eps, sv-tol >= 0; max-iter >= 1\n");
+    return false;
   }
   if (o.train.empty()) o.train = o.dataset + "_train_data.csv";
   if (o.test.empty()) o.test = o.dataset + "_test_data.csv";

@@ -16,6 +16,8 @@ import dataclasses
 import os
 from dataclasses import dataclass
 
+import numpy as np
+
 from .._native import params_struct
 
 
@@ -43,6 +45,20 @@ class SVMParams:
     # working-set selection: 1 = first order (the reference, Keerthi et al.), 2 = second-order choice
     # of the second index (Fan, Chen & Lin 2005; opt-in, not the reference's trajectory)
     wss: int = 1
+
+    def __post_init__(self):
+        # the reference hard-codes these; as parameters they must keep the problem well posed:
+        # C <= 0 empties the box, gamma <= 0 makes the kernel constant (eta = 0), tau <= 0 never stops
+        bad = [f"{k}={v!r}" for k, v, ok in (("C", self.C, self.C > 0), ("gamma", self.gamma, self.gamma > 0),
+                                              ("tau", self.tau, self.tau > 0), ("eps", self.eps, self.eps >= 0),
+                                              ("sv_tol", self.sv_tol, self.sv_tol >= 0),
+                                              ("max_iter", self.max_iter, self.max_iter >= 1),
+                                              ("n_threads", self.n_threads, self.n_threads >= 0),
+                                              ("wss", self.wss, self.wss in (1, 2)))
+               if not (ok and np.isfinite(v))]
+        if bad:
+            raise ValueError("SVM parameters out of range: " + ", ".join(bad) +
+                             " (C, gamma, tau > 0; eps, sv_tol >= 0; max_iter >= 1; wss 1 or 2)")
 
     def to_struct(self, verbose: int = 0):
         return params_struct(self.C, self.gamma, self.tau, self.eps, self.sv_tol, self.max_iter,

@@ -112,3 +112,27 @@ def test_prediction_rows_must_have_the_training_width():
         with pytest.raises(ValueError, match=r"\(m, 5\)"):
             m.decision_function(rng.random(5))
         assert m.predict(np.empty((0, 5))).shape == (0,)
+
+
+@pytest.mark.parametrize("kw", [dict(C=0.0), dict(C=-1.0), dict(gamma=0.0), dict(tau=0.0), dict(max_iter=0),
+                                dict(eps=-1e-12), dict(C=float("nan")), dict(wss=3)])
+def test_parameters_out_of_range_are_rejected(kw):
+    from svm355 import SVC
+
+    with pytest.raises(ValueError, match="out of range"):
+        SVMParams(**kw)
+    key = {"tau": "tol"}.get(next(iter(kw)), next(iter(kw)))
+    if key != "wss":
+        with pytest.raises(ValueError, match="out of range"):
+            SVC(**{key: kw[next(iter(kw))]})
+
+
+def test_native_cli_rejects_parameters_out_of_range(tmp_path):
+    import subprocess
+    from pathlib import Path
+
+    exe = Path(__file__).resolve().parents[1] / "svm355" / "bin" / "svm_serial"
+    for args in (["--C", "-1"], ["--gamma", "0"], ["--max-iter", "0"]):
+        r = subprocess.run([str(exe), "--synthetic", "20,5", *args], cwd=tmp_path, capture_output=True, text=True,
+                           timeout=60)
+        assert r.returncode == 2 and "out of range" in r.stderr, (args, r.stdout, r.stderr)
