@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/r5al
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_edge_cases.py tests/test_gpu_kernels.py -m gpu -x -q --timeout 300 \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_decomp.py tests/test_gpu_properties.py tests/test_gpu_decomp_oracle.py -m gpu -x -q --timeout 300 \
   --timeout-method thread > gpurun_out/r5al/pytest.txt 2>&1
 rc=$?; tail -n 3 gpurun_out/r5al/pytest.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r5al/bench.json 2> gpurun_out/r5al/bench.err
