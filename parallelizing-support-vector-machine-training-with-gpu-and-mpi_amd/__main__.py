@@ -470,16 +470,15 @@ def main(argv=None) -> int:
         return _native("svm_serial", rest)
     if cmd == "gpu":
         return _native("svm_gpu", rest)
-    if cmd == "sweep":
-        return _sweep(rest)
-    if cmd == "cascade":
-        return _cascade(rest)
-    if cmd == "multiclass":
-        return _multiclass(rest)
-    if cmd == "scale":
-        return _scale(rest)
-    print(f"unknown command {cmd!r}\n\n{__doc__}", file=sys.stderr)
-    return 2
+    fn = {"sweep": _sweep, "cascade": _cascade, "multiclass": _multiclass, "scale": _scale}.get(cmd)
+    if fn is None:
+        print(f"unknown command {cmd!r}\n\n{__doc__}", file=sys.stderr)
+        return 2
+    try:
+        return fn(rest)
+    except ValueError as e:  # a bad input or configuration (the reference MPI_Aborts with a message): no traceback
+        print(f"svm355 {cmd}: {e}", file=sys.stderr)
+        return 2
 
 
 if __name__ == "__main__":

@@ -119,3 +119,12 @@ def test_cli_scale_decomp_needs_a_gpu(tmp_path):
     r = subprocess.run([sys.executable, "-m", "svm355", "scale", "--cpu", "--synthetic", "400,100"], cwd=ROOT,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "--trainer cascade" in r.stderr
+
+
+def test_cli_configuration_errors_exit_2_without_a_traceback(tmp_path):
+    """A bad configuration (the tree cascade on 3 ranks; the reference MPI_Aborts, mpi_svm_main3.cpp:420-428)
+    ends the CLI with exit status 2 and one line naming the problem."""
+    r = subprocess.run([sys.executable, "-m", "svm355", "cascade", "--synthetic", "600,100", "--cpu", "--gpus", "3",
+                        "--topology", "tree"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=str(ROOT)))
+    assert r.returncode == 2 and "power-of-2" in r.stderr and "Traceback" not in r.stderr, r.stderr[-2000:]
