@@ -25,7 +25,7 @@ from typing import Optional
 import numpy as np
 
 from ..utils.config import SVMParams, default_threads
-from ..utils.data import MinMaxScaler, check_finite_bounds
+from ..utils.data import MinMaxScaler, check_finite_bounds, check_warm_start
 
 
 def _resolve_device(device: str) -> str:
@@ -79,6 +79,8 @@ class SVC:
             raise ValueError("X must be (n, d) and y (n,)")
         if not np.all(np.abs(y) == 1):
             raise ValueError("labels must be +1/-1 (use svm355.utils.data.one_vs_rest)")
+        if alpha0 is not None:
+            alpha0 = check_warm_start(alpha0, y, self.params.C)
         t0 = time.perf_counter()
         if dev == "cpu":
             self._fit_cpu(X, y, alpha0)

@@ -24,6 +24,21 @@ def _c32(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
+def _start(alpha, n: int) -> np.ndarray:
+    """The solver's alpha buffer: zeros, or a copy of the warm start, which must have n entries (the native
+    solvers read n of them)."""
+    if alpha is None:
+        return np.zeros(n)
+    if np.shape(alpha) != (n,):
+        raise ValueError(f"alpha must have shape ({n},), got {np.shape(alpha)}")
+    return np.array(alpha, dtype=np.float64, copy=True)
+
+
+def _gram_shape(K: np.ndarray, n: int) -> None:
+    if K.ndim != 2 or K.shape[0] < n or K.shape[1] < n:
+        raise ValueError(f"K must be at least ({n}, {n}) for {n} labels, got {K.shape}")
+
+
 def smo_train(X: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[np.ndarray] = None,
               warm: bool = False, trace_cap: int = 0, verbose: int = 0
               ) -> Tuple[np.ndarray, SMOResult, Optional[np.ndarray]]:
@@ -31,7 +46,9 @@ def smo_train(X: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optional[n
     X = _c64(X)
     y = _c32(y)
     n, d = X.shape
-    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    if y.shape != (n,):
+        raise ValueError(f"y must have shape ({n},), got {y.shape}")
+    a = _start(alpha, n)
     r = N.SvmResult()
     trace = np.zeros((trace_cap, 2), dtype=np.int64) if trace_cap > 0 else None
     p = params.to_struct(verbose)
@@ -48,7 +65,8 @@ def smo_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Optio
     K = _c64(K)
     y = _c32(y)
     n = y.shape[0]
-    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    _gram_shape(K, n)
+    a = _start(alpha, n)
     r = N.SvmResult()
     trace = np.zeros((trace_cap, 2), dtype=np.int64) if trace_cap > 0 else None
     p = params.to_struct()
@@ -69,7 +87,8 @@ def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Op
     K = _c64(K)
     y = _c32(y)
     n = y.shape[0]
-    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    _gram_shape(K, n)
+    a = _start(alpha, n)
     r = N.SvmResult()
     st = (ctypes.c_int64 * 8)()
     tr = N.DecompTrace(trace_cap, n if snapshots else 0) if trace_cap > 0 else None
@@ -99,7 +118,8 @@ def decomp_train_gram_dist(K: np.ndarray, y: np.ndarray, params: SVMParams, worl
     K = _c64(K)
     y = _c32(y)
     n = y.shape[0]
-    a = np.zeros(n) if alpha is None else np.array(alpha, dtype=np.float64, copy=True)
+    _gram_shape(K, n)
+    a = _start(alpha, n)
     r = N.SvmResult()
     st = (ctypes.c_int64 * 8)()
     p = params.to_struct()

@@ -74,6 +74,22 @@ def check_labels(y, n: int) -> np.ndarray:
     return y.astype(np.int32, copy=False)
 
 
+def check_warm_start(alpha0, y: np.ndarray, C: float) -> np.ndarray:
+    """alpha0 as float64 (n,) that is a feasible point of the dual: finite, inside the box [0, C] and on
+    the equality constraint sum(alpha y) = 0 (to rounding).  ValueError otherwise: the solvers assume a
+    feasible start, and from an infeasible one they stop on a "converged" model that is not a solution."""
+    a = np.ascontiguousarray(alpha0, dtype=np.float64)
+    n = y.shape[0]
+    if a.shape != (n,):
+        raise ValueError(f"alpha0 must have shape ({n},), got {a.shape}")
+    if not np.all(np.isfinite(a)) or a.min(initial=0.0) < 0.0 or a.max(initial=0.0) > C:
+        raise ValueError(f"alpha0 must be finite and inside [0, C = {C}]")
+    s = float(np.dot(a, y.astype(np.float64)))
+    if abs(s) > 1e-9 * max(1.0, float(a.sum())):
+        raise ValueError(f"alpha0 must satisfy sum(alpha0 * y) = 0 (the dual's equality constraint), got {s:.3g}")
+    return a
+
+
 def check_finite_bounds(mn, mx) -> None:
     """ValueError when a column's min / max is NaN or infinite, i.e. the rows hold a NaN or an infinity
     (numpy's and the device's column bounds propagate NaN): a fit would otherwise find no violating pair

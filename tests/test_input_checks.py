@@ -136,3 +136,28 @@ def test_native_cli_rejects_parameters_out_of_range(tmp_path):
         r = subprocess.run([str(exe), "--synthetic", "20,5", *args], cwd=tmp_path, capture_output=True, text=True,
                            timeout=60)
         assert r.returncode == 2 and "out of range" in r.stderr, (args, r.stdout, r.stderr)
+
+
+def test_warm_starts_must_be_feasible():
+    """SVC.fit(alpha0=...) and the oracles' alpha: the right length (the native solvers read n entries),
+    finite, inside [0, C] and on sum(alpha y) = 0 -- from an infeasible start a solver stops on a
+    'converged' model that is not a solution."""
+    from svm355 import SVC
+    from svm355.ops import cpu as C
+
+    rng = np.random.default_rng(6)
+    X = rng.random((100, 4))
+    y = np.where(rng.random(100) < 0.5, 1, -1).astype(np.int32)
+    for a0, msg in ((np.zeros(10), "shape"), (np.full(100, 20.0), r"\[0, C"), (-np.ones(100), r"\[0, C"),
+                    (np.where(y > 0, 1.0, 0.0), "sum"), (np.full(100, np.nan), r"\[0, C")):
+        with pytest.raises(ValueError, match=msg):
+            SVC(device="cpu").fit(X, y, alpha0=a0)
+    K = C.rbf_matrix(X, X, 0.5)
+    with pytest.raises(ValueError, match="shape"):
+        C.smo_train_gram(K, y, SVMParams(gamma=0.5), alpha=np.zeros(10), warm=True)
+    with pytest.raises(ValueError, match="at least"):
+        C.decomp_train_gram(K[:50, :50], y, SVMParams(gamma=0.5))
+    feasible = np.zeros(100)
+    i, j = int(np.flatnonzero(y > 0)[0]), int(np.flatnonzero(y < 0)[0])
+    feasible[i] = feasible[j] = 0.5
+    assert SVC(device="cpu").fit(X, y, alpha0=feasible).stop_reason_ == "converged"
