@@ -122,6 +122,8 @@ def main(argv=None):
                          "plumbing; N > 1 under torchrun exchanges over gloo); not a benchmark")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
+    if a.steps < 1 or a.warmup < 0 or a.gpus < 1:
+        ap.error("--steps must be >= 1, --warmup >= 0 and --gpus >= 1")
 
     import torch
 
