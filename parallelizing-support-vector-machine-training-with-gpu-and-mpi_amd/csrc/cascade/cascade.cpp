@@ -265,6 +265,20 @@ class Rank {
     B_.d2h(mn_h.data(), mn.get(), d_ * 8);
     B_.d2h(mx_h.data(), mx.get(), d_ * 8);
   }
+  // The training set a checkpoint belongs to: FNV-1a over n and the global column bounds (a resume on
+  // other data would otherwise warm-start from another problem's support vectors without a word).
+  uint64_t data_fingerprint(int64_t n_total) const {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](const void* p, size_t bytes) {
+      const auto* c = static_cast<const unsigned char*>(p);
+      for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    };
+    mix(&n_total, 8);
+    mix(mn_h.data(), mn_h.size() * 8);
+    mix(mx_h.data(), mx_h.size() * 8);
+    return h;
+  }
+  uint64_t fingerprint = 0;  // set by run_cascade after the global scaling
 
   // warm (alphas kept) U rows of extra whose id is not in warm (alpha = 0), extra order kept
   // (the seen_ids loops of mpi_svm_main3.cpp:629-655 / mpi_svm_main2.cpp:474-502).
@@ -429,6 +443,7 @@ class Rank {
       f.write(reinterpret_cast<const char*>(&b), 8);
       f.write(reinterpret_cast<const char*>(&d), 8);
       f.write(reinterpret_cast<const char*>(&k), 8);
+      f.write(reinterpret_cast<const char*>(&fingerprint), 8);
       f.write(reinterpret_cast<const char*>(recs.data()), std::streamsize(recs.size() * 8));
       if (!f) throw CascadeError("short write on checkpoint " + tmp);
     }
@@ -441,6 +456,7 @@ class Rank {
     char magic[8];
     int32_t topo = 0, reserved = 0;
     int64_t d = 0, k = 0;
+    uint64_t fp = 0;
     f.read(magic, 8);
     f.read(reinterpret_cast<char*>(&topo), 4);
     f.read(reinterpret_cast<char*>(&reserved), 4);
@@ -448,9 +464,12 @@ class Rank {
     f.read(reinterpret_cast<char*>(b), 8);
     f.read(reinterpret_cast<char*>(&d), 8);
     f.read(reinterpret_cast<char*>(&k), 8);
+    f.read(reinterpret_cast<char*>(&fp), 8);
     if (!f || std::memcmp(magic, kCheckpointMagic, 8) != 0) throw CascadeError("not a cascade checkpoint");
     if (topo != (tree ? 1 : 0) || d != d_ || k < 0 || *next_round < 0)
       throw CascadeError("checkpoint does not match this cascade configuration");
+    if (fp != fingerprint)
+      throw CascadeError("checkpoint belongs to another training set (row count or column ranges differ)");
     std::vector<double> recs(size_t(k) * size_t(d_ + 3));
     f.read(reinterpret_cast<char*>(recs.data()), std::streamsize(recs.size() * 8));
     if (!f) throw CascadeError("truncated cascade checkpoint");
@@ -520,6 +539,7 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
   const auto t0 = Clock::now();
   R.phase[kPhSetup] = ms_between(t_entry, t0) - R.phase[kPhUpload];
   R.scale_global(part);
+  R.fingerprint = R.data_fingerprint(n_total);
   DSet G = R.make(0);  // global SV set (meaningful on rank 0; broadcast each round)
   std::unordered_set<int64_t> global_ids;
   double b = 0.0;

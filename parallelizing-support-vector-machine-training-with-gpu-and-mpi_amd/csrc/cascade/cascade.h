@@ -380,7 +380,7 @@ inline int cascade_solver_for(int solver, int64_t k, int64_t warm_rows) {
 // cascade_state.bin layout (little-endian): char magic[8] = "SVM355C2"; int32 topology (0 star,
 // 1 tree); int32 reserved; int64 next_round; double b; int64 d; int64 k; then k records of d + 3
 // doubles [scaled row (d) | y | alpha | global id] (backend independent).
-constexpr char kCheckpointMagic[9] = "SVM355C2";
+constexpr char kCheckpointMagic[9] = "SVM355C3";  // C3: + training-set fingerprint
 
 struct SolveLog {
   int rank = 0, round = 0;

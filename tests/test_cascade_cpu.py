@@ -152,6 +152,19 @@ def test_checkpoint_of_other_topology_is_rejected(tmp_path, data):
         CascadeSVM(P2, topology="tree", checkpoint_dir=str(tmp_path), resume=True).fit(tr.X, tr.y, world=2)
 
 
+def test_checkpoint_of_other_training_set_is_rejected(tmp_path, data):
+    """A resume on other rows (another row count or other column ranges) is refused: the checkpoint
+    carries a fingerprint of n and the global column bounds."""
+    tr, _ = data
+    CascadeSVM(P2, topology="star", max_rounds=1, checkpoint_dir=str(tmp_path)).fit(tr.X, tr.y, world=2)
+    with pytest.raises(NativeError, match="another training set"):
+        CascadeSVM(P2, topology="star", checkpoint_dir=str(tmp_path), resume=True).fit(tr.X[:-7], tr.y[:-7], world=2)
+    X2 = tr.X.copy()
+    X2[:, 300] = X2[:, 300] * 0.5  # one column's range changes
+    with pytest.raises(NativeError, match="another training set"):
+        CascadeSVM(P2, topology="star", checkpoint_dir=str(tmp_path), resume=True).fit(X2, tr.y, world=2)
+
+
 @pytest.mark.parametrize("world,fail_rank,fail_round", [(2, 1, 1), (3, 0, 0), (4, 2, 1)])
 def test_failing_rank_ends_every_rank(data, world, fail_rank, fail_round):
     """One rank throws mid-run: the others leave their exchanges and the call reports that rank."""
