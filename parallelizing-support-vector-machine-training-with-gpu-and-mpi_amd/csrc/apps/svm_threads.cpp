@@ -211,6 +211,41 @@ void resume(const Data& D) {
          res.ok ? "" : res.err);
 }
 
+// Degenerate partitions: rows sorted by label, 8 ranks, so every partition holds one class and no rank
+// has a support vector (rank 0's gather of the empty sets once read past its id lists), and more ranks
+// than rows (empty partitions); a resume on other rows is refused.
+void degenerate(const Data& D) {
+  Data S;
+  S.n = 24;
+  S.d = D.d;
+  S.X.assign(D.X.begin(), D.X.begin() + S.n * S.d);
+  S.y.resize(size_t(S.n));
+  for (int64_t i = 0; i < S.n; ++i) S.y[size_t(i)] = i < S.n / 2 ? 1 : -1;
+  for (bool tree : {false, true}) {
+    const svm_cascade_cfg c = base_cfg(tree);
+    const Fit f = take(svm_cascade_fit_cpu(S.X.data(), S.y.data(), S.n, S.d, 8, &c));
+    report(tree ? "cascade tree P=8, one class per partition" : "cascade star P=8, one class per partition",
+           f.ok && f.ids.empty(), f.ok ? "" : f.err);
+    const Fit g = take(svm_cascade_fit_cpu(S.X.data(), S.y.data(), 5, S.d, 8, &c));
+    report(tree ? "cascade tree P=8 on 5 rows (empty partitions)" : "cascade star P=8 on 5 rows (empty partitions)",
+           g.ok, g.ok ? "" : g.err);
+  }
+  namespace fs = std::filesystem;
+  const fs::path dir = fs::temp_directory_path() / ("svm_threads_fp_" + std::to_string(::getpid()));
+  const std::string ds = dir.string();
+  svm_cascade_cfg c = base_cfg(false);
+  c.checkpoint_dir = ds.c_str();
+  c.max_rounds = 1;
+  const Fit part = take(svm_cascade_fit_cpu(D.X.data(), D.y.data(), D.n, D.d, 2, &c));
+  c.max_rounds = 50;
+  c.resume = 1;
+  const Fit other = take(svm_cascade_fit_cpu(D.X.data(), D.y.data(), D.n - 5, D.d, 2, &c));
+  fs::remove_all(dir);
+  report("cascade resume on other rows is refused", part.ok && !other.ok &&
+                                                       other.err.find("another training set") != std::string::npos,
+         other.err.substr(0, 90));
+}
+
 void decomp(int64_t n) {
   Data D = make_data(n, 11);
   std::vector<double> mn(size_t(D.d)), mx(size_t(D.d));
@@ -287,6 +322,7 @@ int main(int argc, char** argv) {
   cascades(D, quick);
   abort_mid_round(D);
   resume(D);
+  degenerate(D);
   decomp(std::max<int64_t>(n, 600));
   std::printf("%s\n", g_fail ? "SOME SCENARIOS FAILED" : "ALL SCENARIOS OK");
   return g_fail ? 1 : 0;
