@@ -111,3 +111,27 @@ def test_non_finite_rows_are_rejected_on_the_gpu(bad):
         OneVsRestSVC(device="cuda:0").fit(X, rng.integers(0, 3, size=3000))
     with pytest.raises(ValueError, match="NaN or infinite"):
         OneVsRestSVC(device="cuda:0", solver="batched").fit(X, rng.integers(0, 3, size=3000))
+
+
+@pytest.mark.parametrize("topology", ["star", "tree"])
+def test_cascade_with_more_ranks_than_rows(topology):
+    """8 loopback ranks on 5 rows: three partitions are empty (no upload, no min/max, no solve)."""
+    from svm355.parallel.cascade import CascadeSVM
+
+    rng = np.random.default_rng(13)
+    X = rng.integers(0, 256, size=(5, 6)).astype(np.uint8)
+    y = np.array([1, -1, 1, -1, 1], dtype=np.int32)
+    c = CascadeSVM(topology=topology).fit(X, y, world=8, device="cuda:0", transport="loopback")
+    assert c.result.converged
+
+
+def test_distributed_decomposition_with_more_ranks_than_rows():
+    from svm355.parallel.decomp import DistributedDecompSVC
+
+    rng = np.random.default_rng(14)
+    X = rng.integers(0, 256, size=(5, 6)).astype(np.uint8)
+    y = np.array([1, -1, 1, -1, 1], dtype=np.int32)
+    one = SVC(device="cuda:0", solver="decomp").fit(X, y)
+    m = DistributedDecompSVC(world=8, transport="loopback").fit(X, y)
+    assert m.stop_reason_ == one.stop_reason_ == "converged"
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
