@@ -135,3 +135,27 @@ def test_distributed_decomposition_with_more_ranks_than_rows():
     m = DistributedDecompSVC(world=8, transport="loopback").fit(X, y)
     assert m.stop_reason_ == one.stop_reason_ == "converged"
     np.testing.assert_array_equal(m.alpha_, one.alpha_)
+
+
+@pytest.mark.parametrize("d", [1, 3, 17, 129, 1023, 3000])
+@pytest.mark.parametrize("kind", ["u8", "f64"])
+def test_feature_counts_from_1_to_3000(d, kind):
+    """Odd and large feature counts (row strides padded to 16 doubles, k-steps of 32 / 128 int8 columns,
+    the exact plan's step cap): the default GPU solver ends on the stop test, with the pairwise solver's
+    support vectors."""
+    rng = np.random.default_rng(d)
+    n = 1500
+    if kind == "u8":
+        X = rng.integers(0, 256, size=(n, d)).astype(np.uint8)
+        Xf = X.astype(np.float64)
+    else:
+        Xf = X = rng.standard_normal((n, d))
+    w = rng.standard_normal(d)
+    y = np.where(Xf @ w > np.median(Xf @ w), 1, -1).astype(np.int32)
+    gamma = 1.0 / d  # the rows are min-max scaled to [0, 1] either way
+    m = SVC(device="cuda:0", gamma=gamma).fit(X, y)
+    p = SVC(device="cuda:0", gamma=gamma, solver="smo").fit(X, y)
+    assert m.stop_reason_ == "converged" and p.stop_reason_ in ("converged", "max_iter")
+    assert _gap(Xf, y, m.alpha_, m) <= 2 * m.params.tau + 1e-8
+    if p.stop_reason_ == "converged":
+        assert abs(len(m.support_) - len(p.support_)) <= max(2, len(p.support_) // 100)
