@@ -159,3 +159,18 @@ def test_feature_counts_from_1_to_3000(d, kind):
     assert _gap(Xf, y, m.alpha_, m) <= 2 * m.params.tau + 1e-8
     if p.stop_reason_ == "converged":
         assert abs(len(m.support_) - len(p.support_)) <= max(2, len(p.support_) // 100)
+
+
+@pytest.mark.parametrize("n", [2047, 2049, 16383, 16385, 65535, 65537])
+def test_pairwise_solver_shape_boundaries(n):
+    """The pairwise solver changes shape with n (one workgroup up to 2,048 points, 256- then 512-thread
+    XCD-local teams up to 64k, the device-wide solver above): on both sides of each boundary it reaches the
+    stop test with the decomposition solver's support vectors and b within 10 tau."""
+    from svm355.utils.data import synthetic_mnist
+
+    tr = synthetic_mnist(n, seed=n % 97).compact()
+    p = SVC(device="cuda:0", solver="smo").fit(tr.X, tr.y)
+    m = SVC(device="cuda:0").fit(tr.X, tr.y)
+    assert p.stop_reason_ == m.stop_reason_ == "converged"
+    np.testing.assert_array_equal(p.support_, m.support_)
+    assert abs(p.b_ - m.b_) <= 10 * p.params.tau
