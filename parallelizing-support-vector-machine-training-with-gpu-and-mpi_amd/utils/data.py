@@ -75,14 +75,17 @@ def check_labels(y, n: int) -> np.ndarray:
 
 
 def check_warm_start(alpha0, y: np.ndarray, C: float) -> np.ndarray:
-    """alpha0 as float64 (n,) that is a feasible point of the dual: finite, inside the box [0, C] and on
+    """alpha0 as float64 (n,) that is a feasible point of the dual: finite, inside the box [0, C] (to rounding) and on
     the equality constraint sum(alpha y) = 0 (to rounding).  ValueError otherwise: the solvers assume a
     feasible start, and from an infeasible one they stop on a "converged" model that is not a solution."""
     a = np.ascontiguousarray(alpha0, dtype=np.float64)
     n = y.shape[0]
     if a.shape != (n,):
         raise ValueError(f"alpha0 must have shape ({n},), got {a.shape}")
-    if not np.all(np.isfinite(a)) or a.min(initial=0.0) < 0.0 or a.max(initial=0.0) > C:
+    # the solvers' own alphas may sit a few ulps outside the box (a_i moves by the rounded step of a_j,
+    # as in the reference's update, gpu_svm_main3.cu:441-448): a previous solution must stay a valid start
+    tol = 1e-9 * max(1.0, C)
+    if not np.all(np.isfinite(a)) or a.min(initial=0.0) < -tol or a.max(initial=0.0) > C + tol:
         raise ValueError(f"alpha0 must be finite and inside [0, C = {C}]")
     s = float(np.dot(a, y.astype(np.float64)))
     if abs(s) > 1e-9 * max(1.0, float(a.sum())):

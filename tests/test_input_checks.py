@@ -161,3 +161,10 @@ def test_warm_starts_must_be_feasible():
     i, j = int(np.flatnonzero(y > 0)[0]), int(np.flatnonzero(y < 0)[0])
     feasible[i] = feasible[j] = 0.5
     assert SVC(device="cpu").fit(X, y, alpha0=feasible).stop_reason_ == "converged"
+    # a solver's own solution sits a few ulps outside the box (a_i moves by the rounded step of a_j): it
+    # stays a valid warm start
+    m = SVC(device="cpu", C=1.0, gamma=0.5).fit(X, y)
+    a = m.alpha_.copy()
+    a[np.argmax(a)] = 1.0 + 2e-15
+    a[np.argmin(a)] = -1e-15
+    assert SVC(device="cpu", C=1.0, gamma=0.5).fit(X, y, alpha0=a).stop_reason_ == "converged"
