@@ -51,6 +51,28 @@ inline void usage(const char* prog) {
           prog);
 }
 
+// Numeric option values parse whole or the run ends (exit 2), as argparse does: atof("1e-5x") would be
+// 1e-5 and atoll("abc") a silent 0 (--synthetic abc read the default CSVs instead).
+inline double parse_num(const char* what, const char* v) {
+  char* end = nullptr;
+  const double x = strtod(v, &end);
+  if (end == v || *end != '\0') {
+    fprintf(stderr, "invalid number for %s: '%s'\n", what, v);
+    exit(2);
+  }
+  return x;
+}
+
+inline long long parse_int(const char* what, const char* v, bool until_comma = false) {
+  char* end = nullptr;
+  const long long x = strtoll(v, &end, 10);
+  if (end == v || (*end != '\0' && !(until_comma && *end == ','))) {
+    fprintf(stderr, "invalid integer for %s: '%s'\n", what, v);
+    exit(2);
+  }
+  return x;
+}
+
 inline bool parse(int argc, char** argv, Options& o, int default_threads) {
   svm_default_params(&o.p);
   o.p.n_threads = default_threads;
@@ -63,31 +85,43 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
       }
       return argv[++i];
     };
+    auto num = [&](const char* what) { return parse_num(what, next(what)); };
+    auto count = [&](const char* what, const char* v, bool until_comma = false) {
+      return parse_int(what, v, until_comma);
+    };
     if (a == "--dataset") o.dataset = next("--dataset");
     else if (a == "--train") o.train = next("--train");
     else if (a == "--test") o.test = next("--test");
     else if (a == "--synthetic") {
       const char* v = next("--synthetic");
-      o.synth_train = atoll(v);
+      o.synth_train = count("--synthetic", v, true);
       const char* c = strchr(v, ',');
-      o.synth_test = c ? atoll(c + 1) : 10000;
-    } else if (a == "--seed") o.seed = strtoull(next("--seed"), nullptr, 10);
-    else if (a == "--n-limit") o.n_limit = atoll(next("--n-limit"));
-    else if (a == "--test-limit") o.test_limit = atoll(next("--test-limit"));
-    else if (a == "--C") o.p.C = atof(next("--C"));
-    else if (a == "--gamma") o.p.gamma = atof(next("--gamma"));
-    else if (a == "--tau") o.p.tau = atof(next("--tau"));
-    else if (a == "--eps") o.p.eps = atof(next("--eps"));
-    else if (a == "--sv-tol") o.p.sv_tol = atof(next("--sv-tol"));
-    else if (a == "--max-iter") o.p.max_iter = atoll(next("--max-iter"));
-    else if (a == "--positive-label") o.positive_label = atoi(next("--positive-label"));
-    else if (a == "--threads") o.p.n_threads = atoi(next("--threads"));
+      o.synth_test = c ? count("--synthetic", c + 1) : 10000;
+      if (o.synth_train < 1 || o.synth_test < 0) {
+        fprintf(stderr, "--synthetic N[,M] needs N >= 1, M >= 0\n");
+        return false;
+      }
+    } else if (a == "--seed") o.seed = (unsigned long long)count("--seed", next("--seed"));
+    else if (a == "--n-limit") o.n_limit = count("--n-limit", next("--n-limit"));
+    else if (a == "--test-limit") o.test_limit = count("--test-limit", next("--test-limit"));
+    else if (a == "--C") o.p.C = num("--C");
+    else if (a == "--gamma") o.p.gamma = num("--gamma");
+    else if (a == "--tau") o.p.tau = num("--tau");
+    else if (a == "--eps") o.p.eps = num("--eps");
+    else if (a == "--sv-tol") o.p.sv_tol = num("--sv-tol");
+    else if (a == "--max-iter") o.p.max_iter = count("--max-iter", next("--max-iter"));
+    else if (a == "--positive-label") o.positive_label = (int)count("--positive-label", next("--positive-label"));
+    else if (a == "--threads") o.p.n_threads = (int)count("--threads", next("--threads"));
     else if (a == "--model-dir") o.model_dir = next("--model-dir");
     else if (a == "--json") o.json = next("--json");
     else if (a == "--quiet") o.quiet = true;
-    else if (a == "--warmup") o.warmup = atoi(next("--warmup"));
+    else if (a == "--warmup") o.warmup = (int)count("--warmup", next("--warmup"));
     else if (a == "--gram") {
       const std::string g = next("--gram");
+      if (g != "auto" && g != "fp64" && g != "int") {
+        fprintf(stderr, "--gram must be auto, fp64 or int\n");
+        return false;
+      }
       o.gram_mode = g == "fp64" ? 1 : g == "int" ? 2 : 0;
     } else if (a == "--solver") {
       const std::string v = next("--solver");
@@ -108,7 +142,7 @@ inline bool parse(int argc, char** argv, Options& o, int default_threads) {
       usage(argv[0]);
       exit(0);
     } else if (a.size() && a[0] != '-' && o.n_limit < 0) {
-      o.n_limit = atoll(a.c_str());  // gpu_svm4 positional form: ./gpu_svm4 <n_limit>
+      o.n_limit = count("n_limit", a.c_str());  // gpu_svm4 positional form: ./gpu_svm4 <n_limit>
     } else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       usage(argv[0]);

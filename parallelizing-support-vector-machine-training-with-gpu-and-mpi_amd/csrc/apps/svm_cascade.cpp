@@ -61,14 +61,14 @@ int main(int argc, char** argv) {
       return argv[++i];
     };
     if (a == "--topology") topology = val();
-    else if (a == "--gpus") P = atoi(val().c_str());
+    else if (a == "--gpus") P = int(cli::parse_int("--gpus", val().c_str()));
     else if (a == "--transport") transport = val();
-    else if (a == "--max-rounds") max_rounds = atoi(val().c_str());
+    else if (a == "--max-rounds") max_rounds = int(cli::parse_int("--max-rounds", val().c_str()));
     else if (a == "--checkpoint-dir") checkpoint_dir = val();
     else if (a == "--resume") resume = true;
-    else if (a == "--comm-timeout") timeout = atof(val().c_str());
-    else if (a == "--fail-rank") fail_rank = atoi(val().c_str());
-    else if (a == "--fail-round") fail_round = atoi(val().c_str());
+    else if (a == "--comm-timeout") timeout = cli::parse_num("--comm-timeout", val().c_str());
+    else if (a == "--fail-rank") fail_rank = int(cli::parse_int("--fail-rank", val().c_str()));
+    else if (a == "--fail-round") fail_round = int(cli::parse_int("--fail-round", val().c_str()));
     else if (a == "-h" || a == "--help") {
       usage(argv[0]);
       cli::usage(argv[0]);
@@ -77,7 +77,7 @@ int main(int argc, char** argv) {
   }
   cli::Options o;
   if (!cli::parse(int(rest.size()), rest.data(), o, 0)) return 2;
-  if ((topology != "star" && topology != "tree") || P < 1 ||
+  if ((topology != "star" && topology != "tree") || P < 1 || max_rounds < 1 || !(timeout > 0) ||
       (transport != "auto" && transport != "rccl" && transport != "loopback")) {
     usage(argv[0]);
     return 2;

@@ -136,6 +136,19 @@ def test_native_cli_rejects_parameters_out_of_range(tmp_path):
         r = subprocess.run([str(exe), "--synthetic", "20,5", *args], cwd=tmp_path, capture_output=True, text=True,
                            timeout=60)
         assert r.returncode == 2 and "out of range" in r.stderr, (args, r.stdout, r.stderr)
+    # values parse whole: no silent 0 from atoll("abc") (which read the default CSVs) or 1e-5 from "1e-5x"
+    bad = ((["--synthetic", "abc"], "invalid integer"), (["--synthetic", "20,x"], "invalid integer"),
+           (["--synthetic", "0,5"], "N >= 1"), (["--synthetic", "20,5", "--C", "1e-5x"], "invalid number"),
+           (["--synthetic", "20,5", "--n-limit", "10,5"], "invalid integer"),
+           (["--synthetic", "20,5", "--gram", "bogus"], "--gram must be"))
+    for args, msg in bad:
+        r = subprocess.run([str(exe), *args], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2 and msg in r.stderr, (args, r.stdout, r.stderr)
+    casc = exe.parent / "svm_cascade"
+    for args in (["--gpus", "two"], ["--max-rounds", "0"], ["--comm-timeout", "0"]):
+        r = subprocess.run([str(casc), "--synthetic", "40,10", *args], cwd=tmp_path, capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode == 2, (args, r.stdout, r.stderr)
 
 
 def test_warm_starts_must_be_feasible():
