@@ -30,7 +30,7 @@ using namespace svm355;
 namespace {
 
 constexpr int kMaxWS = SVM_DECOMP_MAX_WS;
-constexpr int64_t kSelPts = 256 * 16;  // points per selection block at most (ws_select_kernel)
+constexpr int64_t kSelPts = 256 * 16;  // points per selection block below the block cap (ws_select_kernel)
 constexpr int kInnerNT = 256;           // the device's inner workgroup (ws_inner_kernel<256, 4>)
 
 struct Shape {
@@ -47,10 +47,11 @@ Shape shape(int64_t n, int qws, int world) {
   const int64_t nb0 = std::max<int64_t>((n + kSelPts - 1) / kSelPts, std::min<int64_t>(64, (n + 63) / 64));
   const int64_t mult = (8 % world == 0) ? 8 : int64_t(8) * world;
   d.NB = (nb0 + mult - 1) / mult * mult;
-  d.per = (n + d.NB - 1) / d.NB;
-  d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
+  d.NB = std::min<int64_t>(d.NB, int64_t(kMaxWS / 2) / mult * mult);  // past 2,097,152 rows: wider blocks
+  d.per = d.NB > 0 ? (n + d.NB - 1) / d.NB : 0;
+  d.T = d.NB > 0 ? int(std::max<int64_t>(1, d.q / (2 * d.NB))) : 0;
   d.L = 2 * d.NB * d.T;
-  d.ok = n >= 2 && n < int64_t(UINT32_MAX) && d.L <= kMaxWS && d.per <= kSelPts && world >= 1;
+  d.ok = n >= 2 && n < int64_t(INT32_MAX) && d.NB >= 1 && d.L <= kMaxWS && world >= 1;
   return d;
 }
 

@@ -163,6 +163,70 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
   }
 }
 
+// ws_select_kernel's picks for blocks of any size, streamed from memory: past 2,097,152 rows the block
+// count is capped at kMaxWS / 2 (the candidates must fit one working set, so T = 1) and a block holds
+// more than the kSelNT x kSelE points the register-resident kernel takes (SVM355_DECOMP_WIDE_SELECT=1
+// runs it at any n, for the equivalence tests).  Round k takes, per side, the best point strictly after
+// round k - 1's block pick in (value, lowest index) order: the keys are distinct, so that is the next
+// entry of the sorted list the T arg-reductions of ws_select_kernel (and the CPU oracle) produce.  One
+// pass over the block per round; every thread merges the four wave winners itself.
+__global__ __launch_bounds__(kSelNT) void ws_select_wide_kernel(const double* __restrict__ f,
+                                                                const double* __restrict__ alpha,
+                                                                const int32_t* __restrict__ y, int64_t lo,
+                                                                int64_t nloc, int64_t per, int T, double C, double eps,
+                                                                CandRec* __restrict__ cand_h,
+                                                                CandRec* __restrict__ cand_l,
+                                                                const DecompCtl* __restrict__ ctl) {
+  if (ctl->stop != SVM_STOP_RUNNING) return;
+  constexpr int NW = kSelNT / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t b0 = int64_t(blockIdx.x) * per, b1 = std::min<int64_t>(nloc, b0 + per);
+  const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
+  __shared__ double wv[2][NW];
+  __shared__ uint32_t wi[2][NW];
+  VI ph{-inf, 0}, pl{inf, 0};  // the previous round's block picks (round 0: nothing excluded)
+  for (int k = 0; k < T; ++k) {
+    VI mn{inf, kSentinel}, mx{-inf, kSentinel};
+    for (int64_t i = b0 + t; i < b1; i += kSelNT) {  // ascending index within a thread
+      const double a = alpha[lo + i], fi = f[i];
+      const int32_t yi = y[lo + i];
+      const uint32_t gi = uint32_t(lo + i);
+      const bool up = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
+      const bool dn = (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi);
+      const bool eh = k == 0 || fi > ph.v || (fi == ph.v && gi > ph.i);
+      const bool el = k == 0 || fi < pl.v || (fi == pl.v && gi > pl.i);
+      if (up && eh && fi < mn.v) mn = VI{fi, gi};
+      if (dn && el && fi > mx.v) mx = VI{fi, gi};
+    }
+    VIL a, b;
+    wave_arg_pair(mn, mx, a, b);
+    if (lane == 0) {
+      wv[0][w] = a.v;
+      wi[0][w] = a.i;
+      wv[1][w] = b.v;
+      wi[1][w] = b.i;
+    }
+    __syncthreads();
+    VI bh{wv[0][0], wi[0][0]}, bl{wv[1][0], wi[1][0]};
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      const VI ch{wv[0][q], wi[0][q]}, cl{wv[1][q], wi[1][q]};
+      if (beats<true>(ch, bh)) bh = ch;
+      if (beats<false>(cl, bl)) bl = cl;
+    }
+    __syncthreads();  // every thread has read the wave winners before the next round writes them
+    if (t == 0) {
+      const bool ok = bh.i != kSentinel && bh.v < inf;
+      cand_h[int64_t(blockIdx.x) * T + k] = CandRec{ok ? bh.v : 0.0, ok ? int32_t(bh.i) : -1, 0};
+    } else if (t == 64) {
+      const bool ok = bl.i != kSentinel && bl.v > -inf;
+      cand_l[int64_t(blockIdx.x) * T + k] = CandRec{ok ? bl.v : 0.0, ok ? int32_t(bl.i) : -1, 0};
+    }
+    ph = bh;
+    pl = bl;
+  }
+}
+
 // One workgroup over the L gathered candidates (Lr per GPU, GPU-major; the first Lh of each GPU's
 // are I_high picks, T per selection block, the rest I_low): b_high = min f over the I_high
 // candidates, b_low = max f over the I_low ones (the global extremes: every block's first pick is its
@@ -839,50 +903,125 @@ __global__ __launch_bounds__(256) void ws_rowsum_f64_kernel(const double* __rest
 }
 
 // Column cache bookkeeping of one f update (one 1024-thread workgroup): the moved columns cols[0..*count)
-// the cache lacks get slots -- persistent ones in moved order while the cache has room (slot_of keeps
-// them for the rest of the fit), then scratch slots cap + position -- and are listed for the column
-// store (miss_ids / miss_slots, state[1] of them); rd_slot[k] = every moved column's slot.  state[0] =
-// the next free persistent slot; state[2] = 1 when the narrow column store takes the misses (at most
-// 64: the tiled store's gate).
+// the cache lacks get slots -- free persistent ones in moved order while the cache has room (slot_of
+// keeps them for the rest of the fit), then, with `meta`, slots evicted by a CLOCK sweep, then scratch
+// slots cap + position -- and are listed for the column store (miss_ids / miss_slots, state[1] of them);
+// rd_slot[k] = every moved column's slot.  state[0] = the next free persistent slot; state[2] = 1 when
+// the narrow column store takes the misses (at most 64: the tiled store's gate); state[3] = the clock
+// hand, state[4] = the update's stamp.  meta (nullptr: fill-only) = owner[cap] (point id, -1 none),
+// last[cap] (stamp of the last update that used the slot), ref[cap] (the CLOCK bit, set on every use):
+// past ~2M rows the distinct moved columns outnumber the slots a quarter of the HBM holds, and the
+// columns the solve moves late are not the ones it moved first.  A victim is a slot this update does not
+// read whose bit the hand finds clear (the hand clears the bits it passes); a cached column is the
+// recomputed one bit for bit, so the policy never changes a result.
+__device__ __forceinline__ int block_excl_scan_1024(bool v, int32_t* wsum, int& total) {
+  const int k = threadIdx.x, lane = k & 63, w = k >> 6;
+  const unsigned long long bal = __ballot(v);
+  if (lane == 0) wsum[w] = __popcll(bal);
+  __syncthreads();
+  int r = __popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+  for (int q = 0; q < 16; ++q) {
+    if (q < w) r += wsum[q];
+    tot += wsum[q];
+  }
+  __syncthreads();  // wsum is reused by the next scan
+  total = tot;
+  return r;
+}
+
 __global__ __launch_bounds__(1024) void ws_cache_plan_kernel(const int32_t* __restrict__ cols,
                                                              const int32_t* __restrict__ count,
                                                              int32_t* __restrict__ slot_of, int32_t cap,
                                                              int32_t* __restrict__ state, int32_t* __restrict__ rd_slot,
                                                              int32_t* __restrict__ miss_ids,
-                                                             int32_t* __restrict__ miss_slots) {
-  constexpr int NW = 1024 / 64;
-  __shared__ int32_t wsum[NW];
-  const int k = threadIdx.x, lane = k & 63, w = k >> 6;
+                                                             int32_t* __restrict__ miss_slots,
+                                                             int32_t* __restrict__ meta) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t vict[kMaxWS];
+  __shared__ int32_t s_nv, s_hand, s_stop;
+  const int k = threadIdx.x;
   const int cnt = *count;
   const bool valid = k < cnt;
   const int32_t id = valid ? cols[k] : -1;
   int32_t sl = valid ? slot_of[id] : 0;
   const bool miss = valid && sl < 0;
-  const unsigned long long bal = __ballot(miss);
-  if (lane == 0) wsum[w] = __popcll(bal);
-  __syncthreads();
-  int r = __popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
-  for (int q = 0; q < NW; ++q) {
-    if (q < w) r += wsum[q];
-    tot += wsum[q];
+  int32_t* owner = meta;
+  int32_t* last = meta ? meta + cap : nullptr;
+  int32_t* ref = meta ? meta + 2 * int64_t(cap) : nullptr;
+  const int32_t E = state[4] + 1;
+  if (meta && valid && !miss) {  // hits: read by this update (never a victim now) and referenced
+    last[sl] = E;
+    ref[sl] = 1;
   }
+  int tot = 0;
+  const int r = block_excl_scan_1024(miss, wsum, tot);  // its barriers publish the hits' stamps
   const int32_t next = state[0];
+  const int fresh = max(0, min(tot, cap - next));
+  const int need = meta ? tot - fresh : 0;
+  if (k == 0) {
+    s_nv = 0;
+    s_hand = state[3];
+  }
+  __syncthreads();
+  if (need > 0) {
+    const int win = min(cap, kMaxWS);
+    const int max_sweeps = 2 * ((cap + win - 1) / win) + 1;  // one full turn clears every unpinned bit
+    for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+      const int have = s_nv, hand = s_hand;
+      if (have >= need) break;  // uniform: read after a barrier
+      const int32_t sx = int32_t((int64_t(hand) + k) % cap);
+      // slots from `next` on are this update's fresh fills (the cache fills up in this very update)
+      const bool cand = k < win && sx < next && last[sx] != E && ref[sx] == 0;
+      int vtot = 0;
+      const int vr = block_excl_scan_1024(cand, wsum, vtot);
+      const bool take = cand && have + vr < need;
+      if (take) {
+        vict[have + vr] = sx;
+        last[sx] = E;  // taken: not a candidate again when a small cache's next window wraps onto it
+      }
+      if (take && have + vr == need - 1) s_stop = k;  // the hand stops after the last victim it needs
+      __syncthreads();
+      const bool done = have + vtot >= need;
+      const int passed = done ? s_stop + 1 : win;
+      if (k < passed && !take && last[sx] != E) ref[sx] = 0;  // second chance used up
+      __syncthreads();
+      if (k == 0) {
+        s_nv = min(need, have + vtot);
+        s_hand = int32_t((int64_t(hand) + passed) % cap);
+      }
+      __syncthreads();
+    }
+  }
+  const int nv = s_nv;
   if (miss) {
-    if (next + r < cap) {
+    if (r < fresh) {
       sl = next + r;
-      slot_of[id] = sl;
+    } else if (r - fresh < nv) {
+      sl = vict[r - fresh];
+      const int32_t old = owner[sl];
+      if (old >= 0) slot_of[old] = -1;  // not a column of this update: its slot would be pinned
     } else {
-      sl = cap + k;  // cache full: a scratch slot for this update only
+      sl = cap + k;  // no slot free or evictable: a scratch slot for this update only
+    }
+    if (sl < cap) {
+      slot_of[id] = sl;
+      if (meta) {
+        owner[sl] = id;
+        last[sl] = E;
+        ref[sl] = 1;
+      }
     }
     miss_ids[r] = id;
     miss_slots[r] = sl;
   }
   if (valid) rd_slot[k] = sl;
-  __syncthreads();  // every thread has read state[0]
+  __syncthreads();  // every thread has read state[0] / state[3] / state[4]
   if (k == 0) {
-    state[0] = min(cap, next + tot);
+    state[0] = next + fresh;
     state[1] = tot;
     state[2] = tot <= 64 ? 1 : 0;
+    state[3] = s_hand;
+    state[4] = E;
   }
 }
 
@@ -1063,13 +1202,16 @@ DecompShape decomp_shape(int64_t n, int qws, int world) {
   const int64_t nb0 = std::max<int64_t>((n + kSelNT * kSelE - 1) / (kSelNT * kSelE), std::min<int64_t>(64, (n + 63) / 64));
   const int64_t mult = (8 % world == 0) ? 8 : int64_t(8) * world;
   d.NB = (nb0 + mult - 1) / mult * mult;
-  d.per = (n + d.NB - 1) / d.NB;
+  // at most kMaxWS / 2 blocks (past 2,097,152 rows): their extreme pairs fill one working set, and the
+  // blocks grow beyond kSelNT x kSelE points (ws_select_wide_kernel)
+  d.NB = std::min<int64_t>(d.NB, int64_t(kMaxWS / 2) / mult * mult);
+  d.per = d.NB > 0 ? (n + d.NB - 1) / d.NB : 0;
   // T picks per block and side; at least one, so the working-set capacity L = 2 NB T is the
   // requested q rounded down to the blocks, or 2 NB when q < 2 NB (every block contributes its extreme
   // pair: the union must hold the globally maximal violating pair).  stats[2] reports L.
-  d.T = int(std::max<int64_t>(1, d.q / (2 * d.NB)));
+  d.T = d.NB > 0 ? int(std::max<int64_t>(1, d.q / (2 * d.NB))) : 0;
   d.L = 2 * d.NB * d.T;
-  d.ok = n >= 2 && n < int64_t(kSentinel) && d.L <= kMaxWS && d.per <= int64_t(kSelNT) * kSelE && world >= 1;
+  d.ok = n >= 2 && n < int64_t(kSentinel) && d.NB >= 1 && d.L <= kMaxWS && world >= 1;
   return d;
 }
 
@@ -1110,8 +1252,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   }
   const DecompShape sh = decomp_shape(n, qws, world);
   if (!sh.ok) {
-    set_error("decomposition SMO: n = %lld is outside the solver's shapes (2 <= n, %lld candidates <= %d, blocks "
-              "of <= %d points)", (long long)n, (long long)sh.L, kMaxWS, kSelNT * kSelE);
+    set_error("decomposition SMO: n = %lld is outside the solver's shapes (2 <= n < 2^31 - 1, %lld candidates <= %d, "
+              "world <= 64)", (long long)n, (long long)sh.L, kMaxWS);
     return SVM_ERR_ARG;
   }
   const int64_t NBr = sh.NB / world, b0 = rank * NBr;
@@ -1119,6 +1261,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const int64_t nloc = hi - lo;
   const int T = sh.T;
   const int64_t Lr = 2 * NBr * T;  // this GPU's candidate records (I_high picks, then I_low)
+  const char* wide_env = getenv("SVM355_DECOMP_WIDE_SELECT");
+  const bool wide_select = sh.per > int64_t(kSelNT) * kSelE || T > 64 || (wide_env && atoi(wide_env) == 1);
   // inner workgroup: NT threads x PER points (NT * PER = 1024); SVM355_DECOMP_NT = 64 | 128 | 256 | 512
   int inner_nt = 256;
   if (const char* v = getenv("SVM355_DECOMP_NT")) inner_nt = atoi(v);
@@ -1166,6 +1310,9 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // HBM (192 MiB: 60k MNIST rows, 46 MB, are 4 % faster without the cache, 250k rows 2 % with it).
   bool use_cache = false;
   int32_t cache_cap = 0;
+  // evict by CLOCK once the slots are taken (SVM355_DECOMP_CCACHE_EVICT=0: fill-only, the round-4 cache)
+  const char* ev_env = getenv("SVM355_DECOMP_CCACHE_EVICT");
+  const bool cache_evict = !(ev_env && atoi(ev_env) == 0);
   int64_t ldc_cache = 0;
   double* cache = nullptr;
   if (!f64 && nloc > 0) {
@@ -1216,7 +1363,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // column cache state: slot per point (-1 = none), the update's slots, its misses, {next free, misses}
   const size_t o_cslot = use_cache ? take(size_t(n) * 4) : 0, o_crd = use_cache ? take(kMaxWS * 4) : 0,
                o_cmid = use_cache ? take(kMaxWS * 4) : 0, o_cmsl = use_cache ? take(kMaxWS * 4) : 0,
-               o_cst = use_cache ? take(64) : 0;
+               o_cst = use_cache ? take(64) : 0,
+               o_cmeta = use_cache && cache_evict ? take(size_t(cache_cap) * 12) : 0;
   // K(W, W) through the narrow column store: the identity ids 0 .. kMaxWS - 1 and the column count
   const size_t o_wid = f64 ? 0 : take(kMaxWS * 4 + 64);
   // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
@@ -1251,6 +1399,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   auto* cmid = reinterpret_cast<int32_t*>(ws + o_cmid);
   auto* cmsl = reinterpret_cast<int32_t*>(ws + o_cmsl);
   auto* cst = reinterpret_cast<int32_t*>(ws + o_cst);
+  auto* cmeta = use_cache && cache_evict ? reinterpret_cast<int32_t*>(ws + o_cmeta) : nullptr;
   auto* wid = reinterpret_cast<int32_t*>(ws + o_wid);  // [kMaxWS] identity, then the count kMaxWS
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
   // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
@@ -1262,7 +1411,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     if (nloc <= 0) return SVM_OK;
     if (use_cache) {  // plan the slots, compute and store the missing columns, sum every column from the cache
       hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cl, cnt, cslot, cache_cap, cst, crd, cmid,
-                         cmsl);
+                         cmsl, cmeta);
       SVMD_LAUNCH_CHECK();
       const int rc2 = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid,
                                             cmsl, cst + 1, kMaxWS, P, p.gamma, cache, ldc_cache, cst + 2, tiled);
@@ -1311,6 +1460,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   if (use_cache) {  // a fresh cache per fit: no point has a slot, the first free slot is 0
     SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
     SVMD_CHECK(hipMemsetAsync(cst, 0, 64, s));
+    if (cmeta) {  // owners and stamps -1, CLOCK bits clear
+      SVMD_CHECK(hipMemsetAsync(cmeta, 0xFF, size_t(cache_cap) * 8, s));
+      SVMD_CHECK(hipMemsetAsync(cmeta + 2 * int64_t(cache_cap), 0, size_t(cache_cap) * 4, s));
+    }
   }
   hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n,
                      int(o.warm));
@@ -1427,8 +1580,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       }
       if ((rc = solo_begin(0))) return rc;
       if (NBr > 0)
-        hipLaunchKernelGGL(ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT), 0, s, f, alpha, y, lo, nloc, sh.per,
-                           T, p.C, p.eps, cown, cown + NBr * T, ctl);
+        hipLaunchKernelGGL(wide_select ? ws_select_wide_kernel : ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT),
+                           0, s, f, alpha, y, lo, nloc, sh.per, T, p.C, p.eps, cown, cown + NBr * T, ctl);
       SVMD_LAUNCH_CHECK();
       if ((rc = solo_end(0))) return rc;
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
@@ -1931,7 +2084,8 @@ SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t
     SVMD_CHECK(hipMemsetAsync(f, 0, size_t(nloc) * 8, s));
     SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
     SVMD_CHECK(hipMemsetAsync(cst, 0, 256, s));
-    hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cols, cnt, cslot, m, cst, crd, cmid, cmsl);
+    hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cols, cnt, cslot, m, cst, crd, cmid, cmsl,
+                       nullptr);
     SVMD_LAUNCH_CHECK();
     rc = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid, cmsl,
                                cst + 1, kMaxWS, P, gamma, cache, ldc, cst + 2);

@@ -140,13 +140,17 @@ def test_warm_start_equals_the_oracle_and_meets_the_stop_test():
     np.testing.assert_array_equal(warm.alpha_, a)
 
 
-@pytest.mark.parametrize("slots", [None, "300"])
-def test_column_cache_trajectory_equals_the_oracle(monkeypatch, slots):
-    """The f update served from the column cache (forced on at 6k; with 300 slots the cache fills and
-    later misses take scratch slots) keeps the oracle's trajectory bit for bit, cold and warm."""
+@pytest.mark.parametrize("slots,evict", [(None, None), ("300", None), ("8", None), ("300", "0")])
+def test_column_cache_trajectory_equals_the_oracle(monkeypatch, slots, evict):
+    """The f update served from the column cache (forced on at 6k) keeps the oracle's trajectory bit for
+    bit, cold and warm: with every column cached; with 300 slots (the cache fills, then the CLOCK sweep
+    evicts slots the update does not read); with 8 (fewer slots than a sweep's window: the hand wraps,
+    most misses take scratch slots); and with 300 fill-only slots (SVM355_DECOMP_CCACHE_EVICT=0)."""
     monkeypatch.setenv("SVM355_DECOMP_CCACHE", "1")
     if slots:
         monkeypatch.setenv("SVM355_DECOMP_CCACHE_SLOTS", slots)
+    if evict:
+        monkeypatch.setenv("SVM355_DECOMP_CCACHE_EVICT", evict)
     n = 6000
     tr = synthetic_mnist(n, seed=61).compact()
     Xu, mn, mx = _dev_rows(tr)
@@ -167,10 +171,13 @@ def test_column_cache_trajectory_equals_the_oracle(monkeypatch, slots):
         assert res.stop_reason == r_o.stop_reason == "converged" and res.b == r_o.b
 
 
-@pytest.mark.parametrize("n", [60000, 250000])
-def test_column_cache_is_bit_identical_at_large_n(monkeypatch, n):
+@pytest.mark.parametrize("n,slots", [(60000, None), (250000, None), (250000, "1500")])
+def test_column_cache_is_bit_identical_at_large_n(monkeypatch, n, slots):
     """The cache (SVM355_DECOMP_CCACHE=1; the default from ~200k rows) against the GEMV path
-    (SVM355_DECOMP_CCACHE=0): the same alpha, b and iteration counts."""
+    (SVM355_DECOMP_CCACHE=0): the same alpha, b and iteration counts -- also with 1,500 slots for the
+    ~3,000 distinct columns of the 250k solve (eviction in most late updates)."""
+    if slots:
+        monkeypatch.setenv("SVM355_DECOMP_CCACHE_SLOTS", slots)
     tr = synthetic_mnist(n, seed=2024).compact()
     Xu, mn, mx = _dev_rows(tr)
     yd = torch.from_numpy(tr.y).to(DEV)
@@ -211,3 +218,23 @@ def test_kww_paths_equal_the_oracle(monkeypatch, d, kww):
     _compare(dt, ot)
     np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
     assert res.b == r_o.b and res.stop_reason == r_o.stop_reason
+
+
+@pytest.mark.parametrize("n,q", [(2000, 1024), (6000, 64), (6000, 1024)])
+def test_streamed_selection_equals_the_cpu_oracle(n, q, monkeypatch):
+    """ws_select_wide_kernel, the selection past 2,097,152 rows (blocks of more than 4,096 points), forced
+    at any n by SVM355_DECOMP_WIDE_SELECT=1: its T rounds of 'the best point after the previous pick'
+    (T = 16 / 1 / 8 here) give the oracle's picks, so the whole trajectory stays the oracle's bit for bit."""
+    monkeypatch.setenv("SVM355_DECOMP_WIDE_SELECT", "1")
+    tr = synthetic_mnist(n, seed=77 + q).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    K = _exact_gram_host(Xu, mn, mx, n)
+    yd = torch.from_numpy(tr.y).to(DEV)
+    alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+    dt = N.DecompTrace(400, n)
+    res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx, working_set=q, trace=dt)
+    a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), q=q, trace_cap=400, snapshots=True)
+    _compare(dt, ot)
+    assert res.stop_reason == r_o.stop_reason == "converged"
+    assert res.iterations == r_o.iterations and res.b == r_o.b
+    np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)

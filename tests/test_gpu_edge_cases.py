@@ -174,3 +174,35 @@ def test_pairwise_solver_shape_boundaries(n):
     assert p.stop_reason_ == m.stop_reason_ == "converged"
     np.testing.assert_array_equal(p.support_, m.support_)
     assert abs(p.b_ - m.b_) <= 10 * p.params.tau
+
+
+def test_decomposition_beyond_2097152_rows():
+    """Past 2,097,152 rows the selection keeps 512 blocks (their extreme pairs fill one working set) of more
+    than 4,096 points each (ws_select_wide_kernel); the solve ends on the stop test, recomputed here from
+    the exact-integer kernel values over all rows (two overlapping 8-dimensional pixel clusters)."""
+    import torch
+
+    from svm355.ops import device as D
+
+    DEV = torch.device("cuda:0")
+    n, d = 2_200_000, 8
+    rng = np.random.default_rng(3)
+    y = np.where(rng.random(n) < 0.5, 1, -1).astype(np.int32)
+    X = np.clip(np.rint(np.where(y[:, None] > 0, 156.0, 100.0) + 25.0 * rng.standard_normal((n, d))), 0, 255)
+    X = X.astype(np.uint8)
+    m = SVC(device="cuda:0", solver="decomp", gamma=1.0 / d).fit(X, y)
+    assert m.stop_reason_ == "converged" and m.timings_["solver"] == "decomp"
+    assert m.support_.size > 100
+    Xu = D.upload_u8(X, DEV)
+    mmd = torch.empty(2 * d, dtype=torch.float64, device=DEV)
+    D.minmax_u8(Xu, out=mmd)
+    mm = mmd.cpu().numpy()
+    f = -y.astype(np.float64)
+    sv = np.flatnonzero(m.alpha_ > 0).astype(np.int32)  # every nonzero alpha, not only those above sv_tol
+    coef = m.alpha_[sv] * y[sv]
+    for k in range(0, sv.size, 1024):
+        f += D.decomp_gemv_u8(Xu, mm[:d].copy(), mm[d:].copy(), 1.0 / d, sv[k:k + 1024], coef[k:k + 1024])
+    a, p = m.alpha_, m.params
+    hi = ((y == 1) & (a < p.C - p.eps)) | ((y == -1) & (a > p.eps))
+    lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < p.C - p.eps))
+    assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-9
