@@ -169,7 +169,7 @@ class SVC:
                                       warm=alpha0 is not None)
             if out is None and self.solver == "decomp":
                 raise ValueError("solver='decomp': the device rows' stride is not a multiple of 16, n is beyond the "
-                                 "solver's 2,097,152 rows, or the FP64-row solve's workspace (n x 1024 doubles) does "
+                                 "solver's 2^31 - 1 rows, or the FP64-row solve's workspace (n x 1024 doubles) does "
                                  "not fit the device")
         if out is not None:
             res, tm = out
