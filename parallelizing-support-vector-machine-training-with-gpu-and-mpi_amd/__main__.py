@@ -239,6 +239,8 @@ def _scale(argv) -> int:
     ap.add_argument("--repeats", type=int, default=3, help="timed fits per P (median reported)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--comm-timeout", type=float, default=120.0)
+    ap.add_argument("--max-iter", type=int, default=100000,
+                    help="pair-update cap of every solve (the reference's 100,000; large n needs more)")
     ap.add_argument("--json", default=None, help="write the per-size, per-P rows to this file")
     a = ap.parse_args(argv)
     ranks = [int(v) for v in a.ranks.split(",")]
@@ -292,7 +294,7 @@ def _scale(argv) -> int:
         X = tr.X if a.cpu else tr.compact().X  # pixels travel as uint8, widened on the device
         # the single-device baseline: the GPU trainer (cuda:0) or the serial oracle
         base_dev = "cpu" if a.cpu else "cuda:0"
-        single = SVC(device=base_dev)
+        single = SVC(device=base_dev, max_iter=a.max_iter)
         t_single = timed(lambda: single.fit(X, tr.y))
         rows = []
         for P in ranks:
@@ -306,7 +308,7 @@ def _scale(argv) -> int:
             group = None if a.cpu else DeviceGroup(P, a.transport, a.comm_timeout)
             try:
                 if a.trainer == "decomp":
-                    model = DistributedDecompSVC(P, group=group)
+                    model = DistributedDecompSVC(P, group=group, max_iter=a.max_iter)
                     t = timed(lambda: model.fit(X, tr.y))
                     solo = model.solo_
                     row = {"P": P, "train_s": round(t, 6), "outer_iterations": model.stats_["outer_iterations"],
@@ -319,7 +321,7 @@ def _scale(argv) -> int:
                            "transport": group.transport if group is not None else "cpu"}
                 else:
                     threads = max(1, default_threads() // P) if a.cpu else default_threads()
-                    model = CascadeSVM(SVMParams(n_threads=threads), topology=a.topology,
+                    model = CascadeSVM(SVMParams(n_threads=threads, max_iter=a.max_iter), topology=a.topology,
                                        comm_timeout_s=a.comm_timeout)
                     t = timed(lambda: model.fit(X, tr.y, world=P, device="cpu" if a.cpu else "cuda", group=group))
                     r = model.result

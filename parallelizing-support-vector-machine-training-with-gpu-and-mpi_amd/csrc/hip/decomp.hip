@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "decomp.h"
@@ -1310,6 +1311,11 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   // HBM (192 MiB: 60k MNIST rows, 46 MB, are 4 % faster without the cache, 250k rows 2 % with it).
   bool use_cache = false;
   int32_t cache_cap = 0;
+  // Sizing and allocating the cache and the workspace is one step per process: thread ranks sharing a
+  // GPU (the loopback rehearsal) would otherwise read the same free memory, each take half of it, and
+  // leave a later rank without room for its workspace.
+  static std::mutex alloc_mu;
+  std::unique_lock<std::mutex> alloc_lock(alloc_mu);
   // evict by CLOCK once the slots are taken (SVM355_DECOMP_CCACHE_EVICT=0: fill-only, the round-4 cache)
   const char* ev_env = getenv("SVM355_DECOMP_CCACHE_EVICT");
   const bool cache_evict = !(ev_env && atoi(ev_env) == 0);
@@ -1328,7 +1334,12 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     SVMD_CHECK(hipMemGetInfo(&free_b, &total_b));
     ldc_cache = (nloc + 3) & ~int64_t(3);  // a multiple of 4: 16-byte row pairs (or quads) in the reader
     const size_t slot_b = size_t(ldc_cache) * 8;
-    cap = std::min<int64_t>(cap, int64_t((free_b + ctx->rc_cache_bytes) / 2 / slot_b) - kMaxWS);
+    // the workspace allocated below (f, the GEMV partials, the per-point slot map, a warm start's columns
+    // and ~64 MB of fixed parts) comes out of the same free memory
+    const size_t ws_need = size_t(nloc + 1) * 8 * size_t(1 + ldp) + size_t(n) * (o.warm ? 16 : 4) + (size_t(64) << 20);
+    const size_t ws_grow = ws_need > ctx->ws_bytes ? ws_need - ctx->ws_bytes : 0;
+    const size_t avail = free_b + ctx->rc_cache_bytes > ws_grow ? free_b + ctx->rc_cache_bytes - ws_grow : 0;
+    cap = std::min<int64_t>(cap, int64_t(avail / 2 / slot_b) - kMaxWS);
     // and at most a quarter of the GPU's HBM (SVM355_DECOMP_CCACHE_FRAC): the slab is a grow-only
     // buffer of the context, kept for the next fit, that PyTorch's allocator cannot see -- it must leave
     // room for the caller's tensors and other contexts on the device.  At 1M rows that is
@@ -1375,6 +1386,7 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   if (rc) return rc;
   rc = ctx->ensure_pinned(sizeof(DecompHost) * 2 + 2 * sizeof(DecompCtl) + 64);
   if (rc) return rc;
+  alloc_lock.unlock();
   char* ws = static_cast<char*>(ctx->ws);
   auto* f = reinterpret_cast<double*>(ws + o_f);
   auto* cown = reinterpret_cast<CandRec*>(ws + o_own);
