@@ -108,6 +108,8 @@ def main(argv=None):
                     help="the working-set decomposition SMO (decomp; default on GPUs: same stop test on all n points, "
                          "same SVs; N > 1: --parallel auto runs it distributed) or the reference's pairwise first-order "
                          "trajectory (smo; the CPU oracle's, the default with --device cpu)")
+    ap.add_argument("--max-iter", type=int, default=100000,
+                    help="pair-update cap of every solve (the reference's 100,000; --rows beyond ~2M needs more)")
     ap.add_argument("--decomp-fits", "--other-solver-fits", dest="decomp_fits", type=int, default=3,
                     help="N = 1: fits of the OTHER solver (pairwise when the headline is decomp, and vice versa) timed "
                          "after the run and reported next to the headline (0 = skip)")
@@ -188,7 +190,7 @@ def main(argv=None):
 
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))  # bootstrap store + timing max
 
-    params = SVMParams(wss=2 if a.wss == "second" else 1)
+    params = SVMParams(wss=2 if a.wss == "second" else 1, max_iter=a.max_iter)
     te = synthetic_mnist(a.m, seed=a.seed, offset=a.n) if rank == 0 else None
     full = synthetic_mnist(a.n, seed=a.seed)  # every rank: the distributed SMO holds all rows on every GPU
     lo, hi = partition_bounds(a.n, world_env, rank) if multiproc else (0, a.n)
@@ -241,8 +243,8 @@ def main(argv=None):
         else:
             pre = full.subset(0, min(PREFLIGHT_ROWS, a.n))
             try:
-                m = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(pre.X, pre.y)
-                ref = SVC(device=str(dev), solver="smo").fit(pre.X, pre.y)
+                m = DistributedSVC(a.gpus, group=dgroup, rank=drank, max_iter=a.max_iter).fit(pre.X, pre.y)
+                ref = SVC(max_iter=a.max_iter, device=str(dev), solver="smo").fit(pre.X, pre.y)
                 if not (m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)):
                     err = (f"preflight differs from the single-GPU solve (iterations {m.n_iter_} vs {ref.n_iter_}, "
                            f"b {m.b_!r} vs {ref.b_!r})")
@@ -290,8 +292,8 @@ def main(argv=None):
             if agree(not err) and not cpu:
                 pre = full.subset(0, min(PREFLIGHT_ROWS, a.n))
                 try:
-                    m = DistributedDecompSVC(a.gpus, rank=crank).fit(pre.X, pre.y)
-                    ref = SVC(device=str(dev), solver="decomp").fit(pre.X, pre.y)
+                    m = DistributedDecompSVC(a.gpus, rank=crank, max_iter=a.max_iter).fit(pre.X, pre.y)
+                    ref = SVC(max_iter=a.max_iter, device=str(dev), solver="decomp").fit(pre.X, pre.y)
                     if 8 % a.gpus == 0:  # the one-GPU block partition: the same trajectory bit for bit
                         same = m.n_iter_ == ref.n_iter_ and m.b_ == ref.b_ and np.array_equal(m.alpha_, ref.alpha_)
                     else:  # another partition (a multiple of 8 x world blocks): another path to the same optimum
@@ -349,11 +351,11 @@ def main(argv=None):
     def step():
         nonlocal model
         if mode == "single":
-            model = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(full.X, full.y)
+            model = SVC(max_iter=a.max_iter, device=str(dev), wss=a.wss, solver=a.solver).fit(full.X, full.y)
         elif mode == "smo":
-            model = DistributedSVC(a.gpus, group=dgroup, rank=drank).fit(full.X, full.y)
+            model = DistributedSVC(a.gpus, group=dgroup, rank=drank, max_iter=a.max_iter).fit(full.X, full.y)
         elif mode == "decomp":
-            model = DistributedDecompSVC(a.gpus, group=group, rank=crank,
+            model = DistributedDecompSVC(a.gpus, group=group, rank=crank, max_iter=a.max_iter,
                                          transport="cpu" if cpu else "auto").fit(full.X, full.y)
         else:
             model = cascade_fit(a.topology)
@@ -512,11 +514,11 @@ def main(argv=None):
         f64_ms = []
         if a.f64_fits > 0 and not cpu and a.input == "u8":  # the reference's FP64 host rows, same model
             X64 = full.X.astype(np.float64)
-            m64 = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
+            m64 = SVC(max_iter=a.max_iter, device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
             for _ in range(a.f64_fits):
                 sync()
                 tf = time.perf_counter()
-                m64 = SVC(device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
+                m64 = SVC(max_iter=a.max_iter, device=str(dev), wss=a.wss, solver=a.solver).fit(X64, full.y)
                 sync()
                 f64_ms.append((time.perf_counter() - tf) * 1e3)
             extra["f64_input_fit_ms"] = round(float(np.median(f64_ms)), 3)
@@ -526,12 +528,12 @@ def main(argv=None):
             # the other solver on the same rows (outside the timed region): the same stop test on all n
             # points by a different pair sequence; the same SV set expected, b within a few tau
             other = "smo" if a.solver == "decomp" else "decomp"
-            dm = SVC(device=str(dev), solver=other).fit(full.X, full.y)
+            dm = SVC(max_iter=a.max_iter, device=str(dev), solver=other).fit(full.X, full.y)
             d_ms = []
             for _ in range(a.decomp_fits):
                 sync()
                 tf = time.perf_counter()
-                dm = SVC(device=str(dev), solver=other).fit(full.X, full.y)
+                dm = SVC(max_iter=a.max_iter, device=str(dev), solver=other).fit(full.X, full.y)
                 sync()
                 d_ms.append((time.perf_counter() - tf) * 1e3)
             rec = {"fit_ms": round(float(np.median(d_ms)), 3), "fit_ms_all": [round(x, 3) for x in d_ms],
@@ -631,8 +633,8 @@ def main(argv=None):
 
             def one_fit():
                 if cpu and mode == "decomp":  # the one-rank CPU oracle of the decomposition
-                    return DistributedDecompSVC(1, transport="cpu").fit(full.X, full.y)
-                return SVC(device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)
+                    return DistributedDecompSVC(1, transport="cpu", max_iter=a.max_iter).fit(full.X, full.y)
+                return SVC(max_iter=a.max_iter, device=str(dev), wss=a.wss, solver=one_solver).fit(full.X, full.y)
 
             one = one_fit()  # warm
             ts = []
