@@ -114,6 +114,16 @@ def test_cli_scale_sweeps_rank_counts(tmp_path, topology):
     assert "efficiency" in out and "single CPU oracle" in out
 
 
+def test_cli_scale_max_iter_caps_every_solve(tmp_path):
+    """--max-iter reaches the single-device baseline and the cascade's solves (large n needs more than
+    the reference's 100,000)."""
+    js = tmp_path / "scale.json"
+    _run(["scale", "--cpu", "--trainer", "cascade", "--synthetic", "500,100", "--ranks", "1", "--repeats", "1",
+          "--warmup", "0", "--max-iter", "7", "--json", str(js)], tmp_path)
+    sz = json.loads(js.read_text())["sizes"][0]
+    assert sz["single_iterations"] <= 8  # the oracle counts the iteration that finds the cap reached
+
+
 def test_cli_scale_decomp_needs_a_gpu(tmp_path):
     """The default trainer is the distributed decomposition, which runs on GPUs: --cpu asks for the cascade."""
     r = subprocess.run([sys.executable, "-m", "svm355", "scale", "--cpu", "--synthetic", "400,100"], cwd=ROOT,
