@@ -1192,6 +1192,7 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, igram_colstore_narrow_kernel<true>, 256, lds);
     else
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, igram_colstore_narrow_kernel<false>, 256, lds);
+    if (const char* v = getenv("SVM355_NARROW_WGS_PER_CU")) per_cu = std::max(1, atoi(v));  // A/B: grid size
     const unsigned nwg = unsigned(std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, int64_t(cus) * std::max(per_cu, 1))));
     if (P.main0 > 0)
       hipLaunchKernelGGL(igram_colstore_narrow_kernel<true>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
