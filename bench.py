@@ -524,10 +524,13 @@ def main(argv=None):
             extra["f64_input_fit_ms"] = round(float(np.median(f64_ms)), 3)
             extra["f64_input_same_model"] = bool(m64.b_ == model.b_ and m64.n_iter_ == model.n_iter_ and
                                                  np.array_equal(m64.alpha_, model.alpha_))
-        if a.decomp_fits > 0 and not cpu and a.input == "u8":
+        other = "smo" if a.solver == "decomp" else "decomp"
+        if a.decomp_fits > 0 and not cpu and a.input == "u8" and other == "smo" and a.n > 1048576:
+            # beyond the pairwise solver's HBM row cache its fit replays kernels per iteration (minutes)
+            extra["pairwise_solver"] = {"skipped": "n beyond the pairwise row cache (1,048,576 rows)"}
+        elif a.decomp_fits > 0 and not cpu and a.input == "u8":
             # the other solver on the same rows (outside the timed region): the same stop test on all n
             # points by a different pair sequence; the same SV set expected, b within a few tau
-            other = "smo" if a.solver == "decomp" else "decomp"
             dm = SVC(max_iter=a.max_iter, device=str(dev), solver=other).fit(full.X, full.y)
             d_ms = []
             for _ in range(a.decomp_fits):
