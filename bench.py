@@ -491,8 +491,8 @@ def main(argv=None):
                    "n_sv": int(len(r.ids)), "sv_ids_digest": ids_digest(r.ids), "b": r.b,
                    "sv_history": r.sv_history, "solver": cm.solver_used,
                    "transport": r.transport, "per_round_critical_path": crit, "critical_path_solve_ms": crit_ms,
-                   "speedup_vs_ref_cascade_same_P": round(ref / cel, 2) if ref else None,
-                   "speedup_vs_serial": round(REF_SERIAL_S / cel, 2),
+                   "speedup_vs_ref_cascade_same_P": round(ref / cel, 2) if ref and a.n == 60000 else None,
+                   "speedup_vs_serial": round(REF_SERIAL_S / cel, 2) if a.n == 60000 else None,
                    "b_minus_headline_b": float(r.b - model.b_)}
             if topo == "star":
                 rec["merged_history"] = r.merged_history
@@ -704,8 +704,8 @@ def main(argv=None):
             **({"device": "cpu (C++ oracle; launch-path check, not a benchmark)"} if cpu else {}),
             "host_rows": "uint8 (the device reads the bytes; only the SVs are widened to fp64)" if a.input == "u8"
                          else "fp64",
-            "speedup_vs_serial": round(REF_SERIAL_S / value, 2),
-            "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2),
+            "speedup_vs_serial": round(REF_SERIAL_S / value, 2) if a.n == 60000 else None,
+            "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2) if a.n == 60000 else None,
             "step_ms": step_ms,
             ("step_upload_alloc_gram_smo_fit_ms" if mode != "smo" else "step_upload_slab_smo_fit_ms"): parts,
             **extra,
