@@ -118,3 +118,14 @@ def test_bench_parallel_decomp_cpu_twin_thread_ranks(capsys):
 def test_bench_hostcomm_needs_torchrun(capsys):
     assert bench.main(["--gpus", "2", "--transport", "hostcomm", "--parallel", "decomp", "--rows", "600"]) == 2
     assert "--transport hostcomm is a per-process transport" in capsys.readouterr().err
+
+
+def test_bench_max_iter_and_rows_away_from_60k(capsys):
+    """--max-iter reaches the timed solve (here the CPU oracle ends on the cap), and a row count other
+    than the reference's 60k names itself in the config with no reference-relative figures."""
+    assert bench.main(["--device", "cpu", "--rows", "900", "--test-rows", "100", "--steps", "1", "--warmup", "0",
+                       "--max-iter", "20"]) == 0
+    out = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert out["stop_reason"] == "max_iter" and out["iterations"] <= 21
+    assert "900 rows" in out["config"]["model"] and out["config"]["global_batch"] == 900
+    assert out["vs_baseline"] is None and out["speedup_vs_serial"] is None
