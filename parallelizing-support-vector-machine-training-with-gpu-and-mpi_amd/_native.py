@@ -246,6 +246,7 @@ _HIP_SIGS = {
                            POINTER(SvmResult), _P, c_int64]),
     "svmd_release_cache": (c_int32, [c_void_p]),
     "svmd_release_slab": (c_int32, [c_void_p]),
+    "svmd_set_ccache_frac": (c_int32, [c_void_p, c_double]),
     "svmd_cache_bytes": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),
     "svmd_selftest_exp": (c_int32, [c_void_p, _P, c_int64, _P, _P]),
     "svmd_smo_multi": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, c_int32, _P, POINTER(SvmParams),

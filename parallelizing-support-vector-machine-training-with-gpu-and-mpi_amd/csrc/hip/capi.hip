@@ -216,6 +216,12 @@ SVM_API int svmd_cache_bytes(void* h, int64_t* gram, int64_t* slab) {
   return SVM_OK;
 }
 
+SVM_API int svmd_set_ccache_frac(void* h, double frac) {  // < 0: the default quarter of the HBM
+  SVMD_CTX(h);
+  ctx->ccache_frac = frac < 0.0 ? -1.0 : std::min(0.9, frac);
+  return SVM_OK;
+}
+
 SVM_API int svmd_release_slab(void* h) {  // the row-cache slab only (the resident Gram stays)
   SVMD_CTX(h);
   if (ctx->rc_cache) {

@@ -41,6 +41,7 @@ struct DeviceCtx {
   // GB per call, and the default cache size does not depend on what the last free left unmapped.
   double* rc_cache = nullptr;
   size_t rc_cache_bytes = 0;
+  double ccache_frac = -1.0;  // decomposition column cache cap as a fraction of the HBM (< 0: the default)
   unsigned long long* count_d = nullptr;  // device counter for count_sv
   // Cached SMO iteration graph (smo.hip) and the argument key it was captured for.
   hipGraphExec_t smo_exec = nullptr;

@@ -1344,7 +1344,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     // buffer of the context, kept for the next fit, that PyTorch's allocator cannot see -- it must leave
     // room for the caller's tensors and other contexts on the device.  At 1M rows that is
     // ~8,000 slots of 8 MB for ~6,100 distinct columns a fit moves, so no fit of n <= 1M loses a hit.
-    double frac = 0.25;
+    // (a context's own share when several solve side by side, svmd_set_ccache_frac; the env var overrides)
+    double frac = ctx->ccache_frac >= 0.0 ? ctx->ccache_frac : 0.25;
     if (const char* v = getenv("SVM355_DECOMP_CCACHE_FRAC")) frac = std::min(0.9, std::max(0.0, atof(v)));
     cap = std::min<int64_t>(cap, int64_t(double(total_b) * frac / double(slot_b)) - kMaxWS);
     int64_t min_cap = 256;

@@ -56,6 +56,32 @@ def _pool(workers: int) -> ThreadPoolExecutor:
         return _POOLS[workers]
 
 
+def release_solver_caches(timeout_s: float = 5.0) -> bool:
+    """Hand back the device memory the one-vs-rest decomposition solves keep between fits -- each pool
+    thread's column-cache slab (large n; at most half the HBM over a pool), invisible to PyTorch's
+    allocator -- on every thread of every pool (``ops.device.release_gram_buffers`` acts on the calling
+    thread only): one task per thread, all held at a barrier so that no thread takes two.  Call it with no
+    fit running; False when a pool's barrier timed out (a fit was using it) and its slabs were kept."""
+    from ..ops import device as D
+
+    with _POOL_LOCK:
+        pools = dict(_POOLS)
+    ok = True
+    for workers, pool in pools.items():
+        barrier = threading.Barrier(workers)
+
+        def release(_, barrier=barrier):
+            try:
+                barrier.wait(timeout_s)
+            except threading.BrokenBarrierError:
+                return False
+            D.release_gram_buffers()
+            return True
+
+        ok = all(list(pool.map(release, range(workers)))) and ok
+    return ok
+
+
 def _thread_stream(device):
     import torch
 
@@ -78,8 +104,8 @@ class OneVsRestSVC:
         of workgroups per XCD pulling classes from a queue; "streams" runs one persistent solve per
         class on ``concurrent_solves`` streams (default 8).  Results are identical either way.  "decomp":
         the working-set decomposition solver per class with no Gram, ``concurrent_solves`` classes at a time
-        (default: all).  ``wss="second"``:
-        the opt-in second-order working-set selection (as ``SVC(wss="second")``) in every class solve."""
+        (default: all, or 2 past 192 MiB of pixel rows, where the solves are bound by passes over the rows).
+        ``wss="second"``: the opt-in second-order working-set selection (as ``SVC(wss="second")``) in every class solve."""
         if solver not in ("auto", "batched", "streams", "decomp"):
             raise ValueError("solver must be auto, batched, streams or decomp")
         if solver == "decomp" and wss == "second":
@@ -293,16 +319,26 @@ class OneVsRestSVC:
         torch.cuda.synchronize(device)
         mine = [k for k in range(len(ys)) if self._mine(k)]
 
+        # all classes side by side while the rows sit in the last-level cache (the solves are bound by their
+        # one-CU inner chains); past 192 MiB of pixel rows (where the column cache turns on) they are bound
+        # by HBM passes over the rows and two at a time is fastest (1M: 5.7 s against 7.6 s one at a time
+        # and 9-14 s all ten, profiles/r5_ovr_large_n.txt)
+        big = X.shape[0] * X.shape[1] > (192 << 20)
+        workers = self.concurrent_solves or (2 if big else len(mine))
+        width = min(workers, max(1, len(mine)))
+        # Large n: every solving thread's context keeps one column-cache slab for all its classes and for the
+        # next fit -- freeing and re-allocating a tens-of-GB slab made the later solves' caches 2-7x slower
+        # per outer iteration (per class, and again per fit: profiles/r5_ovr_large_n.txt) -- the slabs of a
+        # pool together capped at half the HBM; release_solver_caches() hands them back.
+        frac = min(0.25, 0.5 / width)
+
         def solve(k):
             s = _thread_stream(device)
-            try:
-                with torch.cuda.stream(s):
-                    out = D.train_decomp(rows, ys_d[k], alphas[k], self.params, mn_h, mx_h)
-                s.synchronize()
-            finally:
-                # the pool thread's context keeps no column-cache slab between fits (large n: up to a
-                # quarter of the HBM per context, invisible to PyTorch's allocator)
-                D.release_gram_buffers()
+            ctx = D.DeviceContext.get(device)
+            N.check(ctx.lib.svmd_set_ccache_frac(ctx.handle, frac), "svmd_set_ccache_frac")
+            with torch.cuda.stream(s):
+                out = D.train_decomp(rows, ys_d[k], alphas[k], self.params, mn_h, mx_h)
+            s.synchronize()
             if out is None:
                 raise N.NativeError(f"class {self.classes_[k]}: the decomposition solver declined these rows "
                                     "(no exact-integer plan for uint8 rows, or beyond its shapes); use "
@@ -310,8 +346,7 @@ class OneVsRestSVC:
             return out
 
         with trace_range(f"svm355.ovr.decomp classes={len(mine)}"):
-            workers = self.concurrent_solves or len(mine)
-            outs = dict(zip(mine, _pool(min(workers, max(1, len(mine)))).map(solve, mine))) if mine else {}
+            outs = dict(zip(mine, _pool(width).map(solve, mine))) if mine else {}
             torch.cuda.synchronize(device)
         bs = [outs[k][0].b if k in outs else 0.0 for k in range(len(ys))]
         iters = [outs[k][0].iterations if k in outs else 0 for k in range(len(ys))]
