@@ -93,6 +93,10 @@ def main(argv=None):
                          "torchrun: RCCL (auto / rccl) or hostcomm = the same per-process ranks exchanging over the "
                          "gloo group with host-staged device buffers, so N processes may share one GPU (the "
                          "per-process N-GPU path rehearsed on one device; decomp and cascade)")
+    ap.add_argument("--allow-transport-fallback", action="store_true",
+                    help="under torchrun: when the RCCL rank cannot be set up or fails its preflight on any rank, time "
+                         "the same ranks over host-staged gloo exchanges (config.parallelism then ends in -gloo) "
+                         "instead of exiting non-zero with the failing rank and step")
     ap.add_argument("--input", choices=["u8", "f64"], default="u8",
                     help="host row format: uint8 pixels (default) or FP64 as in the reference")
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
@@ -227,6 +231,9 @@ def main(argv=None):
 
     # ---- distributed SMO set-up + preflight: a 4096-row solve must equal the single-GPU solve
     group = crank = dgroup = drank = None
+    # the exchanges' transport when it is not RCCL between GPUs: "gloo" (host-staged: --transport hostcomm, or the
+    # opt-in fallback), "loopback" (a one-GPU rehearsal); the line's config.parallelism ends with it
+    transport_label = "gloo" if hostcomm else "loopback" if a.transport == "loopback" else ""
     if mode == "smo":
         from svm355.parallel.dsmo import DistributedSVC, DsmoGroup, DsmoRank
 
@@ -309,7 +316,17 @@ def main(argv=None):
                     print(f"bench.py rank {rank}: distributed decomposition unavailable: {err or 'another rank'}",
                           file=sys.stderr, flush=True)
                     os._exit(1)
-                fallback_reason = f"RCCL: {err or 'failed on another rank'}; exchanges over gloo (host-staged)"
+                errs = [None] * world_env  # every rank's reason, so the line names the failing rank and step
+                dist.all_gather_object(errs, err)
+                failed = "; ".join(f"rank {r}: {e}" for r, e in enumerate(errs) if e)
+                if not a.allow_transport_fallback:
+                    if rank == 0:
+                        print(f"bench.py: the RCCL transport failed ({failed}); not timing another transport under "
+                              "the RCCL label (--allow-transport-fallback times host-staged gloo exchanges, labelled "
+                              "-gloo)", file=sys.stderr, flush=True)
+                    os._exit(1)
+                transport_label = "gloo"
+                fallback_reason = f"RCCL: {failed}; exchanges over gloo (host-staged)"
                 if rank == 0:
                     print(f"bench.py: {fallback_reason}", file=sys.stderr, flush=True)
                 if crank is not None:
@@ -672,11 +689,11 @@ def main(argv=None):
         if mode == "single":
             parallelism = "single-gpu"
         elif mode == "smo":
-            parallelism = f"distributed-smo-dp{a.gpus}"
+            parallelism = f"distributed-smo-dp{a.gpus}" + (f"-{transport_label}" if transport_label else "")
         elif mode == "decomp":
-            parallelism = f"distributed-decomp-dp{a.gpus}"
+            parallelism = f"distributed-decomp-dp{a.gpus}" + (f"-{transport_label}" if transport_label else "")
         else:
-            parallelism = f"cascade-{a.topology}-dp{a.gpus}"
+            parallelism = f"cascade-{a.topology}-dp{a.gpus}" + (f"-{transport_label}" if transport_label else "")
         line = {
             "metric": METRIC,
             "value": round(value, 6),

@@ -45,7 +45,7 @@ class SvmParams(ctypes.Structure):
         ("n_threads", c_int32),
         ("verbose", c_int32),
         ("wss", c_int32),
-        ("reserved", c_int32),
+        ("shrink", c_int32),
     ]
 
 
@@ -206,6 +206,7 @@ _CORE_SIGS = {
                                         c_int32, POINTER(SvmResult), POINTER(c_int64), POINTER(SvmDecompTrace)]),
     "svm_crash_handler_install": (c_int32, [c_char_p]),
     "svm_decomp_gemv_ref": (c_int32, [_P, c_int64, c_int64, _P, _P, c_int64, _P]),
+    "svm_decomp_newton_step": (c_int32, [_P, c_int64, _P, c_int32, _P, _P, c_double, c_double, c_int32, POINTER(c_int32)]),
     "svm_decomp_rank_train_gram": (c_int32, [_P, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams), c_int32,
                                              c_double, c_int32, POINTER(SvmResult), POINTER(c_int64)]),
     "svm_decomp_group_train_gram": (c_int32, [c_int32, _P, c_int64, _P, c_int64, _P, c_int32, POINTER(SvmParams),
@@ -276,6 +277,8 @@ _HIP_SIGS = {
     "svmd_train_decomp": (c_int32, [c_void_p, _P, c_int32, c_int64, c_int64, c_int64, _P, _P, _P, _P,
                                     POINTER(SvmParams), c_int32, c_int32, POINTER(SvmResult), POINTER(SvmdTiming),
                                     POINTER(c_int64), POINTER(c_int32), POINTER(SvmDecompTrace)]),
+    "svmd_decomp_newton_probe": (c_int32, [c_void_p, _P, _P, c_int32, _P, _P, c_double, c_double, c_int32, c_int32,
+                                            POINTER(c_int32), _P, POINTER(c_double)]),
     "svmd_decomp_gemv_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, c_double, c_int64, c_int64, _P, _P,
                                       c_int32, _P, POINTER(c_int32)]),
     "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
@@ -390,7 +393,29 @@ def ptr(a) -> int:
     return a.ctypes.data
 
 
+def newton_step_probe(Kw, y, a, f, C=10.0, eps=1e-12, max_free=1024):
+    """One Newton polish step (decomp_newton.h newton_step_ref) on a working set: Kw (m x m), labels,
+    alpha, f by position.  Returns (alpha, f, code: 0 none, 1 full step, 2 cut at a bound)."""
+    import numpy as np
+
+    Kw = np.ascontiguousarray(Kw, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.int32)
+    a = np.array(a, dtype=np.float64)
+    f = np.array(f, dtype=np.float64)
+    code = c_int32(0)
+    check(core().svm_decomp_newton_step(ptr(Kw), Kw.shape[1], ptr(y), len(y), ptr(a), ptr(f), float(C), float(eps),
+                                        int(max_free), code), "svm_decomp_newton_step")
+    return a, f, int(code.value)
+
+
+def shrink_stats(st) -> dict:
+    """The decomposition solver's shrinking and Newton-polish counters (stats[8:13] of a solve,
+    decomp_shrink.h / decomp_newton.h)."""
+    return {"unshrinks": int(st[8]), "shrink_passes": int(st[9]), "min_active": int(st[10]),
+            "repacks": int(st[11]), "newton_steps": int(st[12])}
+
+
 def params_struct(C=10.0, gamma=0.00125, tau=1e-5, eps=1e-12, sv_tol=1e-8, max_iter=100000,
-                  n_threads=1, verbose=0, wss=1) -> SvmParams:
+                  n_threads=1, verbose=0, wss=1, shrink=0) -> SvmParams:
     return SvmParams(float(C), float(gamma), float(tau), float(eps), float(sv_tol), int(max_iter),
-                     int(n_threads), int(verbose), int(wss), 0)
+                     int(n_threads), int(verbose), int(wss), int(shrink))

@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
     CK(svmd_memcpy_d2h(dev.ctx, mxh.data(), mx, d * 8));
     if (o.solver != 0) {  // working-set decomposition (the default, auto; no stored Gram)
       int32_t used = 0;
-      int64_t st[8] = {};
+      int64_t st[SVM_DECOMP_STATS] = {};
       CK(svmd_train_decomp_rows(dev.ctx, Xd, n, ld, d, mnh.data(), mxh.data(), yd, alpha, &o.p, 1024, &r, &tm, st,
                                 &used));
       if (!used) {

@@ -258,7 +258,7 @@ void decomp(int64_t n) {
   p.n_threads = 8;
   std::vector<double> a1(size_t(D.n)), a8(size_t(D.n)), ah(size_t(D.n));
   svm_result r1{}, r8{};
-  int64_t st[8];
+  int64_t st[SVM_DECOMP_STATS];
   const int rc1 = svm_decomp_train_gram(K.data(), D.n, D.y.data(), D.n, a1.data(), 0, &p, 1024, 0.1, 3, &r1, st, nullptr);
   report("decomp oracle, 8-thread worker team", rc1 == SVM_OK && r1.stop_reason == SVM_STOP_CONVERGED,
          rc1 ? svm_last_error() : "iterations " + std::to_string(r1.iterations));

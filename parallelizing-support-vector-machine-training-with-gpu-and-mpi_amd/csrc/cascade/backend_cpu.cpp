@@ -104,7 +104,7 @@ class CpuBackend final : public Backend {
       }
       check(svm_rbf_matrix(S.X.as<double>(), S.k, S.X.as<double>(), S.k, d, p.gamma, K.data(), p.n_threads),
             "svm_rbf_matrix");
-      int64_t ds[8] = {};
+      int64_t ds[SVM_DECOMP_STATS] = {};
       check(svm_decomp_train_gram(K.data(), S.k, S.y.as<int32_t>(), S.k, S.a.as<double>(), 1, &p, 1024, 0.1, 3, &r, ds,
                                   nullptr),
             "svm_decomp_train_gram");

@@ -104,7 +104,7 @@ SVM_API void svm_default_params(svm_params* p) {
   p->n_threads = 1;
   p->verbose = 0;
   p->wss = 1;
-  p->reserved = 0;
+  p->shrink = 0;
 }
 
 SVM_API const char* svm_stop_message(int32_t reason) {

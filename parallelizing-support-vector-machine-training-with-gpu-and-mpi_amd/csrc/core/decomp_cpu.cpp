@@ -15,14 +15,21 @@
 //   * f update (igram GEMV epilogue + ws_fsum_count_kernel): per row, per 64-column half, lane l's
 //     two terms (columns l and 32 + l) summed from 0, a 32-lane xor butterfly (16, 8, 4, 2, 1), and
 //     the halves added in index order before the one add into f.
+//   * shrinking (decomp_shrink.h): the same schedule, rule and unshrink (f recomputed from alpha with
+//     the warm start's chunked GEMV) -- which points are active is part of the trajectory; which rows the
+//     device also keeps updating (its packed list lags the flags) is not, so the trace shows f only
+//     for active points (NaN elsewhere).
 // The kernel values themselves come from the caller (the device Gram on the exact-integer path).
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <limits>
 #include <vector>
 
 #include "../cascade/cascade_capi.h"
+#include "decomp_newton.h"
+#include "decomp_shrink.h"
 #include "internal.h"
 
 using namespace svm355;
@@ -145,10 +152,10 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
   // rank's rows [lo, hi) only
   std::vector<double> f(static_cast<size_t>(std::max<int64_t>(nloc, 1)));
   int64_t warm_cols = 0;
-  for (int64_t i = lo; i < hi; ++i) f[size_t(i - lo)] = -static_cast<double>(y[i]);
-  if (!warm) {
-    for (int64_t i = 0; i < n; ++i) alpha[i] = 0.0;
-  } else {
+  // f = -y + K (alpha y) over the nonzero alphas (ascending ids, chunks of kMaxWS columns): the warm
+  // start, and the recomputation when the solve unshrinks
+  auto f_from_alpha = [&]() -> int64_t {
+    for (int64_t i = lo; i < hi; ++i) f[size_t(i - lo)] = -static_cast<double>(y[i]);
     std::vector<int32_t> nzc;
     std::vector<double> nzv;
     for (int64_t j = 0; j < n; ++j)
@@ -156,13 +163,27 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
         nzc.push_back(int32_t(j));
         nzv.push_back(alpha[j] * double(y[j]));
       }
-    warm_cols = int64_t(nzc.size());
     for (size_t c0 = 0; c0 < nzc.size(); c0 += kMaxWS)
       gemv_update(K + lo * ldk, ldk, nloc, nzc.data() + c0, nzv.data() + c0,
                   int64_t(std::min<size_t>(kMaxWS, nzc.size() - c0)), f.data(), team);
+    return int64_t(nzc.size());
+  };
+  if (!warm) {
+    for (int64_t i = lo; i < hi; ++i) f[size_t(i - lo)] = -static_cast<double>(y[i]);
+    for (int64_t i = 0; i < n; ++i) alpha[i] = 0.0;
+  } else {
+    warm_cols = f_from_alpha();
   }
+  // shrinking: shr[i - lo] = 1 while row i is out of the active set
+  const ShrinkCfg shc = shrink_cfg(p);
+  std::vector<uint8_t> shr(size_t(std::max<int64_t>(nloc, 1)), 0);
+  bool shrunk = false;  // a shrink pass has run since the start / the last unshrink
+  int64_t origin = 0, unshrinks = 0, passes = 0, min_active = nloc, n_active = nloc;
 
-  int64_t outer = 0, inner_total = 0, changed_total = 0, last_inner_it = 0;
+  int64_t outer = 0, inner_total = 0, changed_total = 0, last_inner_it = 0, newton_steps = 0;
+  int last_m = 0;
+  NewtonCfg nwc = newton_cfg(p);
+  nwc.on = nwc.on && inner_wss == 3;  // the device polishes in its default inner solve (second order + second pair)
   int32_t last_reason = SVM_STOP_CONVERGED, stop = SVM_STOP_RUNNING;
   double bh = inf, bl = -inf;
   std::vector<Cand> cown(size_t(std::max<int64_t>(Lr, 1))), call(size_t(sh.L));
@@ -189,6 +210,7 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
           double mv = inf, xv = -inf;
           int64_t mi = -1, xi = -1;
           for (int64_t i = b0; i < b1; ++i) {
+            if (shr[size_t(i - lo)]) continue;
             const double ai = alpha[i], fi = f[size_t(i - lo)];
             if (!th[size_t(i - b0)] && in_high(y[i], ai) && fi < mv) {
               mv = fi;
@@ -246,6 +268,20 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
       set_error("svm_decomp_train_gram: working set outside [2, %d]", kMaxWS);
       return SVM_ERR_INTERNAL;
     }
+    if (stop != SVM_STOP_RUNNING && stop != SVM_STOP_MAX_ITER && shrunk) {
+      // the ACTIVE problem stopped: every point active again, f recomputed from alpha, and the stop
+      // test again on all n points (the next selection)
+      stop = SVM_STOP_RUNNING;
+      f_from_alpha();
+      std::fill(shr.begin(), shr.end(), uint8_t(0));
+      n_active = nloc;
+      shrunk = false;
+      origin = outer;
+      last_inner_it = -1;  // the no-progress test looks at the next working set, not the last one
+      last_m = 0;          // and the Newton polish waits for a long inner solve on the full problem
+      ++unshrinks;
+      continue;
+    }
     if (stop != SVM_STOP_RUNNING) break;
     const double tau_in = std::fmax(tau, tau_frac * (bl - bh));
     const int64_t max_inner = std::min<int64_t>(int64_t(20) * m, p.max_iter - inner_total);
@@ -263,6 +299,9 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
     kl.assign(size_t(m), 0.0);
     int64_t it = 0;
     int32_t reason = SVM_STOP_CONVERGED;
+    // the Newton polish of W's free variables (decomp_newton.h): `since` counts chain iterations with no
+    // bound-status change, and starts at `every` after a long inner solve
+    int32_t since = newton_since0(nwc, last_inner_it, last_m), ntrig = 0;
     for (;;) {
       double hv = inf, lv = -inf;
       int ih = -1, il = -1;
@@ -284,6 +323,23 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
       if (it >= max_inner) {
         reason = SVM_STOP_MAX_ITER;
         break;
+      }
+      if (nwc.on && since >= nwc.every && ntrig < nwc.per_solve) {
+        ++ntrig;
+        since = 0;
+        int code = 0, steps = 0;
+        while (steps < nwc.repeat &&
+               (code = newton_step_ref(m, a.data(), ft.data(), yw.data(),
+                                       [&](int q, int k) { return K[int64_t(W[size_t(q)]) * ldk + W[size_t(k)]]; },
+                                       C, eps, nwc.max_free)) != 0) {
+          ++steps;
+          if (code == 1) break;
+        }
+        if (steps > 0) {
+          it += steps;  // a step counts as an iteration of the inner solve
+          newton_steps += steps;
+          continue;  // select again
+        }
       }
       // inner_wss 3: the second pair from the same selection (ws_inner_kernel DP): i2 = the best I_high
       // point outside i_high's wave of the 256-thread inner workgroup (position k lies in wave
@@ -373,6 +429,8 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
       const double ch = (ah_new - ah) * double(yh);
       const double cl = (al_new - al) * double(yl);
       for (int k = 0; k < m; ++k) ft[size_t(k)] += ch * kh[size_t(k)] + cl * kl[size_t(k)];
+      bool moved_status = bound_status(ah_new, C, eps) != bound_status(ah, C, eps) ||
+                          bound_status(al_new, C, eps) != bound_status(al, C, eps);
       a[size_t(ih)] = ah_new;
       a[size_t(il)] = al_new;
       ++it;
@@ -400,11 +458,14 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
           const double* Ki2 = K + int64_t(W[size_t(i2)]) * ldk;
           const double* Kj2 = K + int64_t(W[size_t(j2)]) * ldk;
           for (int k = 0; k < m; ++k) ft[size_t(k)] += ch2 * Ki2[W[size_t(k)]] + cl2 * Kj2[W[size_t(k)]];
+          moved_status = moved_status || bound_status(ah2, C, eps) != bound_status(a2h, C, eps) ||
+                         bound_status(al2, C, eps) != bound_status(a2l, C, eps);
           a[size_t(i2)] = ah2;
           a[size_t(j2)] = al2;
           ++it;
         }
       }
+      since = moved_status ? 0 : since + 1;
     }
     // ---- moved columns (ascending position = ascending id), alpha written back
     cols.clear();
@@ -419,8 +480,26 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
     inner_total += it;
     changed_total += int64_t(cols.size());
     last_inner_it = it;
+    last_m = m;
     last_reason = reason;
     gemv_update(K + lo * ldk, ldk, nloc, cols.data(), coef.data(), int64_t(cols.size()), f.data(), team);
+    if (shc.pass_after(outer, origin)) {  // shrink pass with this outer iteration's bounds
+      int64_t drop = 0;
+      double hc, lc;
+      shrink_cuts(bh, bl, shc.margin, &hc, &lc);
+      for (int64_t i = lo; i < hi; ++i)
+        if (!shr[size_t(i - lo)] && shrinkable(y[i], alpha[i], f[size_t(i - lo)], C, eps, hc, lc)) {
+          shr[size_t(i - lo)] = 1;
+          ++drop;
+        }
+      n_active -= drop;
+      min_active = std::min(min_active, n_active);
+      shrunk = true;
+      ++passes;
+      if (getenv("SVM355_DECOMP_SHRINK_LOG"))
+        fprintf(stderr, "decomp oracle: rank %d outer %lld shrink pass: %lld active of %lld\n", rank,
+                (long long)outer, (long long)n_active, (long long)nloc);
+    }
     if (tr && tr->count < tr->cap) {
       const int64_t o = tr->count++;
       if (tr->m) tr->m[o] = m;
@@ -438,7 +517,9 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
         tr->bounds[2 * o + 1] = bl;
       }
       if (tr->n == n && tr->alpha) std::copy(alpha, alpha + n, tr->alpha + o * n);
-      if (tr->n == n && tr->f) std::copy(f.begin(), f.end(), tr->f + o * n);
+      if (tr->n == n && tr->f)
+        for (int64_t i = 0; i < n; ++i)
+          tr->f[o * n + i] = shr[size_t(i)] ? std::numeric_limits<double>::quiet_NaN() : f[size_t(i)];
     }
   }
   if (stats) {
@@ -450,6 +531,11 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
     stats[5] = 0;
     stats[6] = 0;
     stats[7] = warm_cols;
+    stats[8] = unshrinks;
+    stats[9] = passes;
+    stats[10] = min_active;
+    stats[11] = 0;
+    stats[12] = newton_steps;
   }
   if (res) {
     res->iterations = inner_total + 1;
@@ -540,6 +626,18 @@ extern "C" SVM_API int svm_decomp_group_train_gram(int32_t world, const double* 
       set_error("decomposition SMO: rank %d's alpha replica differs from rank 0's", r);
       return SVM_ERR_INTERNAL;
     }
+  return SVM_OK;
+}
+
+// One Newton polish step on a working set of m points (tests): Kw (m x m, row stride ldk), labels,
+// alpha and f by position (updated in place); *code = 0 (no step), 1 (full), 2 (cut at a bound).
+extern "C" SVM_API int svm_decomp_newton_step(const double* Kw, int64_t ldk, const int32_t* y, int32_t m, double* a,
+                                              double* f, double C, double eps, int32_t max_free, int32_t* code) {
+  if (!Kw || !y || !a || !f || !code || m < 1 || ldk < m) {
+    set_error("svm_decomp_newton_step: bad arguments");
+    return SVM_ERR_ARG;
+  }
+  *code = newton_step_ref(m, a, f, y, [&](int q, int k) { return Kw[int64_t(q) * ldk + k]; }, C, eps, max_free);
   return SVM_OK;
 }
 

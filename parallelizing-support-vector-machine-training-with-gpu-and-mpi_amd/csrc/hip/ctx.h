@@ -173,7 +173,7 @@ int launch_igram_slab(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
 int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                       int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                       const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m, const QuantPlan& P,
-                      double gamma, double* part, int64_t ldp);
+                      double gamma, double* part, int64_t ldp, const int32_t* diag = nullptr);
 // K(W, W) through the narrow column store; *launched = false (SVM_OK) when its shape limits do not apply.
 int launch_igram_ww(hipStream_t s, const int8_t* Qw, const int32_t* N0w, const double* WNw, const double* stw,
                     int64_t n, const int32_t* ids, const int32_t* count, const QuantPlan& P, double gamma, double* K,
@@ -182,7 +182,7 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
                           int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                           const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,
                           const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate,
-                          bool tiled = true);
+                          bool tiled = true, const int32_t* diag = nullptr);
 int run_igram_u8(hipStream_t s, const uint8_t* Xu, int64_t n, int64_t d, const double* mn_h, const double* mx_h,
                  const QuantPlan& P, double gamma, double* K, int64_t ldk, void* ws, bool* used);
 size_t igram_u8_workspace(int64_t n, const QuantPlan& P);

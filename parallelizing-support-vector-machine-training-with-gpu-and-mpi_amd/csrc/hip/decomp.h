@@ -69,7 +69,7 @@ struct DecompRows {
 };
 
 // stats: SVM_DECOMP_STATS int64 (see run_decomp).
-constexpr int kDecompStats = 8;
+constexpr int kDecompStats = SVM_DECOMP_STATS;
 int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* alpha, int64_t n, const svm_params& p,
                int qws, svm_result* r, int64_t* stats, const DecompOpts& o = {});
 

@@ -33,6 +33,8 @@
 #include <vector>
 
 #include "decomp.h"
+#include "decomp_newton.h"
+#include "decomp_shrink.h"
 #include "persist.h"
 #include "svm355_device.h"
 #include "trace.h"
@@ -58,7 +60,18 @@ struct DecompCtl {
   double tau_in;             // the next inner solve's stop tolerance
   int64_t max_inner;         // and its iteration cap
   int64_t outer, inner_total, changed_total, last_inner_it;
-  int32_t last_inner_reason, pad;
+  int32_t last_inner_reason;
+  int32_t shrunk;            // a shrink pass has run since the start or the last unshrink
+  int64_t n_active;          // this GPU's points not shrunk
+  int64_t passes;            // shrink passes run
+  int32_t last_m, pad2;      // the last inner solve's working-set size (the Newton polish's arming)
+  int64_t newton_steps;      // Newton polish steps applied (decomp_newton.h)
+};
+
+// The Newton polish's knobs on the device (NewtonCfg).
+struct NwDev {
+  int32_t on, every, per_solve, repeat, max_free, pad;
+  double frac;
 };
 constexpr int32_t kStopInternal = -100;
 
@@ -84,24 +97,35 @@ struct CandRec {
 // order (value, then lowest index): every wave's own T best by T wave arg-reductions (the winner
 // masked out by its owner after each), then a 4-way merge of the sorted wave lists.  f is the slice's
 // (local index); alpha and y are global.
+// Shrinking (decomp_shrink.h): shr[i] = 1 excludes local row i; with a packed list (act: the rows in
+// the active order, boff: selection block b's rows are act[boff[b] .. boff[b + 1])) the block walks its
+// packed rows instead of [b per, (b + 1) per) -- the same points in the same ascending order, so the picks
+// are those of the masked full block.
 __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restrict__ f,
                                                            const double* __restrict__ alpha,
                                                            const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
                                                            int64_t per, int T, double C, double eps,
                                                            CandRec* __restrict__ cand_h, CandRec* __restrict__ cand_l,
-                                                           const DecompCtl* __restrict__ ctl) {
+                                                           const DecompCtl* __restrict__ ctl,
+                                                           const int32_t* __restrict__ act,
+                                                           const int32_t* __restrict__ boff,
+                                                           const uint8_t* __restrict__ shr) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   constexpr int NW = kSelNT / 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t b0 = int64_t(blockIdx.x) * per, b1 = std::min<int64_t>(nloc, b0 + per);
+  const int64_t b0 = act ? int64_t(boff[blockIdx.x]) : int64_t(blockIdx.x) * per;
+  const int64_t b1 = act ? int64_t(boff[blockIdx.x + 1]) : std::min<int64_t>(nloc, b0 + per);
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
   double fh[kSelE], fl[kSelE];
+  uint32_t gi[kSelE];  // global ids, ascending in e
 #pragma unroll
   for (int e = 0; e < kSelE; ++e) {
-    const int64_t i = b0 + t + int64_t(kSelNT) * e;
+    const int64_t k = b0 + t + int64_t(kSelNT) * e;
     fh[e] = inf;
     fl[e] = -inf;
-    if (i < b1) {
+    const int64_t i = k < b1 ? (act ? int64_t(act[k]) : k) : k;
+    gi[e] = uint32_t(lo + i);
+    if (k < b1 && !(shr && shr[i])) {
       const double a = alpha[lo + i], fi = f[i];
       const int32_t yi = y[lo + i];
       if ((yi == 1 && a < c_hi) || (yi == -1 && a > c_lo)) fh[e] = fi;
@@ -118,7 +142,7 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
     VI mn{inf, kSentinel}, mx{-inf, kSentinel};
 #pragma unroll
     for (int e = 0; e < kSelE; ++e) {  // ascending index within a thread: strict compares keep the lowest
-      const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
+      const uint32_t i = gi[e];
       const bool ch = fh[e] < mn.v, cl = fl[e] > mx.v;
       mn = ch ? VI{fh[e], i} : mn;
       mx = cl ? VI{fl[e], i} : mx;
@@ -133,9 +157,8 @@ __global__ __launch_bounds__(kSelNT) void ws_select_kernel(const double* __restr
     }
 #pragma unroll
     for (int e = 0; e < kSelE; ++e) {
-      const uint32_t i = uint32_t(lo + b0 + t + int64_t(kSelNT) * e);
-      if (i == a.i) fh[e] = inf;
-      if (i == b.i) fl[e] = -inf;
+      if (gi[e] == a.i) fh[e] = inf;
+      if (gi[e] == b.i) fl[e] = -inf;
     }
   }
   __syncthreads();
@@ -177,18 +200,24 @@ __global__ __launch_bounds__(kSelNT) void ws_select_wide_kernel(const double* __
                                                                 int64_t nloc, int64_t per, int T, double C, double eps,
                                                                 CandRec* __restrict__ cand_h,
                                                                 CandRec* __restrict__ cand_l,
-                                                                const DecompCtl* __restrict__ ctl) {
+                                                                const DecompCtl* __restrict__ ctl,
+                                                                const int32_t* __restrict__ act,
+                                                                const int32_t* __restrict__ boff,
+                                                                const uint8_t* __restrict__ shr) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   constexpr int NW = kSelNT / 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t b0 = int64_t(blockIdx.x) * per, b1 = std::min<int64_t>(nloc, b0 + per);
+  const int64_t b0 = act ? int64_t(boff[blockIdx.x]) : int64_t(blockIdx.x) * per;
+  const int64_t b1 = act ? int64_t(boff[blockIdx.x + 1]) : std::min<int64_t>(nloc, b0 + per);
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
   __shared__ double wv[2][NW];
   __shared__ uint32_t wi[2][NW];
   VI ph{-inf, 0}, pl{inf, 0};  // the previous round's block picks (round 0: nothing excluded)
   for (int k = 0; k < T; ++k) {
     VI mn{inf, kSentinel}, mx{-inf, kSentinel};
-    for (int64_t i = b0 + t; i < b1; i += kSelNT) {  // ascending index within a thread
+    for (int64_t kk = b0 + t; kk < b1; kk += kSelNT) {  // ascending index within a thread
+      const int64_t i = act ? int64_t(act[kk]) : kk;
+      if (shr && shr[i]) continue;
       const double a = alpha[lo + i], fi = f[i];
       const int32_t yi = y[lo + i];
       const uint32_t gi = uint32_t(lo + i);
@@ -321,6 +350,9 @@ __global__ __launch_bounds__(kMaxWS) void ws_build_kernel(const CandRec* __restr
       st = SVM_STOP_MAX_ITER;
     else if (m < 2 || m > kMaxWS)
       st = kStopInternal;
+    // the ACTIVE problem stopped while points are shrunk: not a stop -- the host unshrinks (f recomputed
+    // from alpha, every point active) and the next build tests all n points (decomp_shrink.h)
+    if (st != SVM_STOP_RUNNING && st != SVM_STOP_MAX_ITER && st != kStopInternal && ctl->shrunk) st = kStopUnshrink;
     if (st != SVM_STOP_RUNNING) {
       ctl->stop = st;
       *mcount = 0;  // the rest of the batch's f updates are no-ops
@@ -351,6 +383,358 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
   }
 }
 
+// ---- Newton polish of the working set's free variables (decomp_newton.h) ---------------------------------
+// The inner workgroup's step on W's free set F (positions with c_lo < alpha < c_hi): the Cholesky of
+// K_FF with the right-hand sides f_F and 1 as two extra rows, the back substitution, b and u, the step
+// cut at the first bound, alpha and f of every position of W updated.  gA / gF: W's alpha and f by
+// position (the caller's registers spilled there around the call); Amat: (|F| + 2) x ldA scratch.
+// Every entry's arithmetic is newton_step_ref's, in its order (decomp_newton.h):
+//   * the factorisation is left-looking in panels of kNwPW columns: a row's panel entries first take the
+//     terms of every earlier column (ascending j, from the panel's own rows staged in LDS), then wave 0
+//     factors the panel in LDS column by column (the diagonal's sqrt, the divisions, the updates of the
+//     panel's later columns) with no workgroup barrier;
+//   * the back substitution goes by blocks of 64 columns from the last: wave 0 solves the block's
+//     triangle (staged in LDS) one column at a time, then every thread applies the block's 64 x to its
+//     entries below, in descending column order;
+//   * sums and the step's arg-min in the sequential order (thread 0; wave_arg's value-then-lowest-index).
+// Returns 0 (nothing changed), 1 (full step) or 2 (cut at a bound), the same in every thread.
+constexpr int kNwPW = 16;      // panel width
+constexpr int kNwMax = 512;    // |F| bound of the LDS buffers (NewtonCfg::max_free is clamped to it)
+__device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, int64_t ldw, const int8_t* __restrict__ sy,
+                                      double* __restrict__ gA, double* __restrict__ gF, double* __restrict__ Amat,
+                                      double C, double eps, int max_free, int64_t* __restrict__ prof = nullptr) {
+  constexpr int64_t ldA = kMaxWS;
+  __shared__ int32_t fidx[kMaxWS];
+  __shared__ __attribute__((aligned(16))) double pb[(kNwMax + 2) * kNwPW];  // the panel's rows; later x1, x2, u
+  __shared__ __attribute__((aligned(16))) double lp[kNwMax * kNwPW];        // the panel's own rows of L (as [j][c]); later s1, s2, the diagonal blocks
+  __shared__ int32_t s_wc[16];
+  __shared__ int32_t s_fail, s_blk;
+  __shared__ double s_t, s_b;
+  __shared__ double s_wv[16];
+  __shared__ uint32_t s_wi[16];
+  const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, w = t >> 6, nw = nt >> 6;
+  const double c_hi = C - eps, c_lo = 0.0 + eps;
+  if (prof && t == 0) prof[7] = wall_clock64();
+  // 1. the free positions in ascending order
+  int base = 0;
+  for (int c0 = 0; c0 < m; c0 += nt) {
+    const int k = c0 + t;
+    const double ak = k < m ? gA[k] : 0.0;
+    const bool fr = k < m && ak > c_lo && ak < c_hi;
+    const unsigned long long bal = __ballot(fr);
+    if (lane == 0) s_wc[w] = __popcll(bal);
+    __syncthreads();
+    int r = __popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+    for (int q = 0; q < nw; ++q) {
+      if (q < w) r += s_wc[q];
+      tot += s_wc[q];
+    }
+    if (fr) fidx[base + r] = k;
+    base += tot;
+    __syncthreads();
+  }
+  const int nf = base;
+  if (nf < 2 || nf > min(max_free, kNwMax)) return 0;
+  if (prof && threadIdx.x == 0) prof[0] = wall_clock64();
+  // 2. A = K_FF (lower) and the right-hand sides f_F, 1 (rows nf, nf + 1); the lower triangle as one flat
+  // range of nf (nf + 1) / 2 entries (row i starts at i (i + 1) / 2), 16 independent gathers per thread
+  {
+    constexpr int U = 16;
+    const int64_t ne = int64_t(nf) * (nf + 1) / 2;
+    for (int64_t e0 = t; e0 < ne; e0 += U * int64_t(nt)) {
+      double v[U];
+      int64_t dst[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + int64_t(u) * nt;
+        dst[u] = -1;
+        v[u] = 0.0;
+        if (e < ne) {
+          int i = int((__builtin_sqrt(8.0 * double(e) + 1.0) - 1.0) * 0.5);
+          i = int64_t(i) * (i + 1) / 2 > e ? i - 1 : int64_t(i + 1) * (i + 2) / 2 <= e ? i + 1 : i;
+          const int k = int(e - int64_t(i) * (i + 1) / 2);
+          v[u] = Kw[int64_t(fidx[i]) * ldw + fidx[k]];
+          dst[u] = int64_t(i) * ldA + k;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (dst[u] >= 0) Amat[dst[u]] = v[u];
+    }
+  }
+  for (int k = t; k < nf; k += nt) {
+    Amat[int64_t(nf) * ldA + k] = gF[fidx[k]];
+    Amat[int64_t(nf + 1) * ldA + k] = 1.0;
+  }
+  if (t == 0) s_fail = 0;
+  __threadfence_block();
+  __syncthreads();
+  if (prof && threadIdx.x == 0) prof[1] = wall_clock64();
+  // 3. the factorisation, a panel of kNwPW columns at a time.  Every thread holds up to kNwRows rows of
+  // the panel in registers (rows p0 + t + nt q): it applies the earlier columns (ascending j; the panel's
+  // own rows of L staged in LDS as lp[j][c], shared by the thread's rows), wave 0 factors the panel's
+  // diagonal block in registers (a lane per row, readlane broadcasts), and every thread then solves its
+  // rows below the block against it (ascending kk, no barrier).
+  constexpr int kNwRows = (kNwMax + 2 + 255) / 256;  // rows per thread (nt = 256)
+  double* dblk = pb;  // the panel's diagonal block, kNwPW x kNwPW
+  for (int p0 = 0; p0 < nf; p0 += kNwPW) {
+    const int pw = min(kNwPW, nf - p0);
+    for (int e = t; e < kNwPW * p0; e += nt) {  // lp[j][c] = L[p0 + c][j], j < p0
+      const int j = e / kNwPW, c = e - j * kNwPW;
+      lp[e] = c < pw ? Amat[int64_t(p0 + c) * ldA + j] : 0.0;
+    }
+    __syncthreads();
+    double sv[kNwRows][kNwPW];
+    const double* ar[kNwRows];
+    bool rv[kNwRows];
+#pragma unroll
+    for (int q = 0; q < kNwRows; ++q) {
+      const int i = p0 + t + nt * q;
+      rv[q] = i < nf + 2;
+      ar[q] = Amat + int64_t(rv[q] ? i : 0) * ldA;
+#pragma unroll
+      for (int c = 0; c < kNwPW; ++c) sv[q][c] = rv[q] && c < pw && (i >= nf || p0 + c <= i) ? ar[q][p0 + c] : 0.0;
+    }
+    const bool any = rv[0];
+    if (any) {
+      for (int j = 0; j < p0; j += 4) {  // p0 is a multiple of 16
+        double lij[kNwRows][4];
+#pragma unroll
+        for (int q = 0; q < kNwRows; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; u += 2) {
+            const f64x2 v = rv[q] ? *reinterpret_cast<const f64x2*>(ar[q] + j + u) : f64x2{0.0, 0.0};
+            lij[q][u] = v[0];
+            lij[q][u + 1] = v[1];
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f64x2* lr = reinterpret_cast<const f64x2*>(lp + (j + u) * kNwPW);
+#pragma unroll
+          for (int c2 = 0; c2 < kNwPW / 2; ++c2) {
+            const f64x2 l2 = lr[c2];
+#pragma unroll
+            for (int q = 0; q < kNwRows; ++q) {
+              sv[q][2 * c2] = __builtin_fma(-lij[q][u], l2[0], sv[q][2 * c2]);
+              sv[q][2 * c2 + 1] = __builtin_fma(-lij[q][u], l2[1], sv[q][2 * c2 + 1]);
+            }
+          }
+        }
+      }
+    }
+    // the diagonal block's rows (p0 .. p0 + pw - 1, held by threads 0 .. pw - 1 as q = 0) to LDS
+    if (t < pw)
+#pragma unroll
+      for (int c = 0; c < kNwPW; ++c) dblk[t * kNwPW + c] = sv[0][c];
+    __syncthreads();
+    if (w == 0) {  // the diagonal block in wave 0's registers: lane r = row p0 + r
+      double dr[kNwPW];
+#pragma unroll
+      for (int c = 0; c < kNwPW; ++c) dr[c] = lane < pw ? dblk[lane * kNwPW + c] : 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int kk = 0; kk < kNwPW; ++kk) {
+        if (kk < pw) {
+          const double d = read_lane64(dr[kk], kk);  // row kk's updated diagonal
+          bad = bad || !(d > 1e-12);
+          const double lkk = d > 1e-12 ? __builtin_sqrt(d) : 1.0;
+          if (lane == kk) dr[kk] = lkk;
+          if (lane > kk) dr[kk] = dr[kk] / lkk;
+#pragma unroll
+          for (int k2 = kk + 1; k2 < kNwPW; ++k2)
+            if (k2 < pw) {
+              const double lk2 = read_lane64(dr[kk], k2);  // L[p0 + k2][p0 + kk]
+              if (lane >= k2) dr[k2] = __builtin_fma(-dr[kk], lk2, dr[k2]);
+            }
+        }
+      }
+      if (lane < pw)
+#pragma unroll
+        for (int c = 0; c < kNwPW; ++c) dblk[lane * kNwPW + c] = dr[c];
+      if (lane == 0 && bad) s_fail = 1;
+    }
+    __syncthreads();
+    if (s_fail) return 0;
+    // the rows below the block (and the two right-hand sides) against it; then every row to Amat
+#pragma unroll
+    for (int q = 0; q < kNwRows; ++q) {
+      const int i = p0 + t + nt * q;
+      if (!rv[q]) continue;
+      if (i < p0 + pw) {
+#pragma unroll
+        for (int c = 0; c < kNwPW; ++c) sv[q][c] = dblk[(i - p0) * kNwPW + c];
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < kNwPW; ++kk)
+          if (kk < pw) {
+            sv[q][kk] = sv[q][kk] / dblk[kk * kNwPW + kk];
+#pragma unroll
+            for (int k2 = kk + 1; k2 < kNwPW; ++k2)
+              if (k2 < pw) sv[q][k2] = __builtin_fma(-sv[q][kk], dblk[k2 * kNwPW + kk], sv[q][k2]);
+          }
+      }
+#pragma unroll
+      for (int c = 0; c < kNwPW; ++c)
+        if (c < pw && (i >= nf || p0 + c <= i)) Amat[int64_t(i) * ldA + p0 + c] = sv[q][c];
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (prof && threadIdx.x == 0) prof[2] = wall_clock64();
+  // 4. back substitution: s1 / s2 = z (the right-hand-side rows), x = L^-T z, by blocks of 64 columns
+  double* s1 = lp;
+  double* s2 = lp + kNwMax;
+  double* dB = lp + 2 * kNwMax;  // the block's triangle, 64 x 64
+  double* x1 = pb;
+  double* x2 = pb + kNwMax;
+  for (int k = t; k < nf; k += nt) {
+    s1[k] = Amat[int64_t(nf) * ldA + k];
+    s2[k] = Amat[int64_t(nf + 1) * ldA + k];
+  }
+  for (int jb = (nf - 1) / 64 * 64; jb >= 0; jb -= 64) {
+    const int je = min(jb + 64, nf), bw = je - jb;
+    for (int e = t; e < 64 * 64; e += nt) {
+      const int r = e >> 6, c = e & 63;
+      dB[e] = r < bw && c <= r ? Amat[int64_t(jb + r) * ldA + jb + c] : 0.0;
+    }
+    __syncthreads();
+    if (w == 0) {  // the block's triangle in registers: lane i holds column i (L_ji, j >= i) and s_i
+      double col[64];
+#pragma unroll
+      for (int r = 0; r < 64; ++r) col[r] = dB[r * 64 + lane];
+      const int i = jb + lane;
+      double a1 = i < je ? s1[i] : 0.0, a2 = i < je ? s2[i] : 0.0;
+#pragma unroll
+      for (int r = 63; r >= 0; --r) {
+        if (r < bw) {  // j = jb + r, descending
+          const double ljj = read_lane64(col[r], r);
+          const double xa = read_lane64(a1, r) / ljj, xb = read_lane64(a2, r) / ljj;
+          if (lane == r) {
+            x1[jb + r] = xa;
+            x2[jb + r] = xb;
+          }
+          if (lane < r) {
+            a1 = __builtin_fma(-col[r], xa, a1);
+            a2 = __builtin_fma(-col[r], xb, a2);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < jb; i += nt) {  // the block's columns on the entries below it, descending j
+      double a1 = s1[i], a2 = s2[i];
+      for (int j0 = je - 1; j0 >= jb; j0 -= 32) {
+        double l[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) l[u] = j0 - u >= jb ? Amat[int64_t(j0 - u) * ldA + i] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if (j0 - u >= jb) {
+            a1 = __builtin_fma(-l[u], x1[j0 - u], a1);
+            a2 = __builtin_fma(-l[u], x2[j0 - u], a2);
+          }
+      }
+      s1[i] = a1;
+      s2[i] = a2;
+    }
+    __syncthreads();
+  }
+  if (prof && threadIdx.x == 0) prof[3] = wall_clock64();
+  // 5. b = sum x1 / sum x2 (ascending)
+  if (t == 0) {
+    double S1 = 0.0, S2 = 0.0;
+    for (int k = 0; k < nf; ++k) {
+      S1 += x1[k];
+      S2 += x2[k];
+    }
+    const bool ok = S2 > 0.0 && __builtin_isfinite(S1);
+    s_fail = ok ? 0 : 1;
+    s_b = ok ? S1 / S2 : 0.0;
+  }
+  __syncthreads();
+  if (s_fail) return 0;
+  // 6. the step's cut: min over k of the bound ratios (value, then lowest k)
+  const double b = s_b;
+  double* dal = lp;  // dalpha by F position (s1 / s2 are consumed)
+  VI best{__builtin_inf(), kSentinel};
+  for (int k = t; k < nf; k += nt) {
+    const double u = __builtin_fma(b, x2[k], -x1[k]);
+    const double dk = sy[fidx[k]] == 1 ? u : -u;
+    dal[k] = dk;
+    const double ak = gA[fidx[k]];
+    const double tk = dk > 0.0 ? (C - ak) / dk : dk < 0.0 ? (0.0 - ak) / dk : __builtin_inf();
+    if (tk < best.v) best = VI{tk, uint32_t(k)};  // ascending k within a thread: strict keeps the lowest
+  }
+  const VIL wb = wave_arg<true>(best);
+  if (lane == 0) {
+    s_wv[w] = wb.v;
+    s_wi[w] = wb.i;
+  }
+  __syncthreads();
+  if (t == 0) {
+    VI bb{s_wv[0], s_wi[0]};
+    for (int q = 1; q < nw; ++q) {
+      const VI c{s_wv[q], s_wi[q]};
+      if (beats<true>(c, bb)) bb = c;
+    }
+    s_t = bb.v < 1.0 ? bb.v : 1.0;
+    s_blk = bb.v < 1.0 ? int(bb.i) : -1;
+  }
+  __syncthreads();
+  // 7. alpha, and the realised changes (an - a) y
+  const double tt = s_t;
+  const int blk = s_blk;
+  double* ur = x1;  // x1 / x2 are consumed after the reads above
+  __syncthreads();
+  for (int k = t; k < nf; k += nt) {
+    const double ak = gA[fidx[k]], dk = dal[k];
+    double an = k == blk ? (dk > 0.0 ? C : 0.0) : __builtin_fma(tt, dk, ak);
+    an = fmin(C, fmax(0.0, an));
+    ur[k] = sy[fidx[k]] == 1 ? an - ak : ak - an;
+    gA[fidx[k]] = an;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (prof && threadIdx.x == 0) prof[4] = wall_clock64();
+  // 8. f of every position of W: f_q += sum_k K(F_k, q) ur_k (ascending k), 16 loads per batch
+  for (int q0 = 0; q0 < m; q0 += nt) {
+    const int q = q0 + t;
+    if (q < m) {
+      double sacc = 0.0;
+      for (int k0 = 0; k0 < nf; k0 += 16) {
+        double kv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) kv[u] = k0 + u < nf ? Kw[int64_t(fidx[k0 + u]) * ldw + q] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (k0 + u < nf) sacc = __builtin_fma(kv[u], ur[k0 + u], sacc);
+      }
+      gF[q] += sacc;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (prof && t == 0) {
+    prof[5] = wall_clock64();
+    prof[6] = nf;
+  }
+  return blk >= 0 ? 2 : 1;
+}
+
+// One Newton step on a given working set (tests / timing, svmd_decomp_newton_probe): K(W, W) in Kw (m x
+// m, row stride ldw), alpha and f by position in gA / gF (updated), labels y; *code_out = the step's code.
+__global__ __launch_bounds__(256) void ws_newton_probe_kernel(int m, const double* __restrict__ Kw, int64_t ldw,
+                                                              const int32_t* __restrict__ y, double* __restrict__ gA,
+                                                              double* __restrict__ gF, double* __restrict__ Amat,
+                                                              double C, double eps, int max_free,
+                                                              int32_t* __restrict__ code_out, int64_t* __restrict__ prof) {
+  __shared__ int8_t sy[kMaxWS];
+  for (int k = threadIdx.x; k < kMaxWS; k += blockDim.x) sy[k] = k < m ? int8_t(y[k]) : int8_t(0);
+  __syncthreads();
+  const int code = newton_wg(m, Kw, ldw, sy, gA, gF, Amat, C, eps, max_free, prof);
+  if (threadIdx.x == 0) *code_out = code;
+}
+
 // First-order SMO on the working set in ONE workgroup of NT threads: thread t holds the PER contiguous
 // points W[t PER + e] (f, alpha, y in registers; its entries of a K(W, W) row are PER / 2 16-byte loads).
 // Per iteration:
@@ -367,6 +751,8 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // Stops at W's own gap <= 2 tau_in, at max_inner, or on a reference stop reason.  Then the points
 // whose alpha changed are compacted in position order: cols[j] = their global ids, coef[j] =
 // (alpha_new - alpha_old) y, *mcount = how many -- the f update of all n points reads only those.
+// With packed rows (a shrunk solve, pos_of: local row -> packed position or -1), cdiag[j] = column j's
+// packed position on this GPU (-1: none), the f update's unit diagonal.
 //   DP (second order only): a second pair per iteration from the same selection -- i2 = the best
 //            I_high candidate of the waves other than i_high's, j2 = the first-order j (max f over
 //            I_low) -- whose rows load beside row i_high; after the first pair's update it is applied
@@ -374,14 +760,17 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 //            iterations of the chain at 60k for ~10 % more work per iteration.
 //   J2S (with DP): j2 by the second-order gain of row i2 instead of the first-order j (row i2 loads
 //            beside row i before the gains; both gains reduce in the same wave / barrier / fold).
-template <int NT, int PER, bool PROF = false, bool W2 = false, bool DP = false, bool J2S = false>
+template <int NT, int PER, bool PROF = false, bool W2 = false, bool DP = false, bool J2S = false, bool NWT = false>
 __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__ Kw, int64_t ldw,
                                                       const int32_t* __restrict__ W, DecompCtl* __restrict__ ctl,
                                                       const int32_t* __restrict__ y, double* __restrict__ alpha,
                                                       const double* __restrict__ Wf, double C, double eps,
                                                       int32_t* __restrict__ cols, double* __restrict__ coef,
                                                       int32_t* __restrict__ mcount, DecompHost* __restrict__ hs,
-                                                      DecompCtl* __restrict__ pub) {
+                                                      DecompCtl* __restrict__ pub, const int32_t* __restrict__ pos_of,
+                                                      int64_t lo, int64_t nloc, int32_t* __restrict__ cdiag,
+                                                      double* __restrict__ gAw, double* __restrict__ gFw,
+                                                      double* __restrict__ nAmat, NwDev nw) {
   if (ctl->stop != SVM_STOP_RUNNING) return;
   const int m = ctl->m;
   const double tau_in = ctl->tau_in;
@@ -420,6 +809,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
   const double c_hi = C - eps, c_lo = 0.0 + eps, inf = __builtin_inf();
   int64_t it = 0;
   int32_t reason = SVM_STOP_CONVERGED;
+  // the Newton polish (decomp_newton.h): chain iterations with no bound-status change, starting at `every`
+  // after a long last inner solve (newton_since0)
+  int32_t since = NWT && ctl->last_m > 0 && double(ctl->last_inner_it) >= nw.frac * double(ctl->last_m) ? nw.every : 0;
+  int32_t ntrig = 0;
+  int64_t nsteps = 0;
   // PROF: wave 0's clock at the phase boundaries (select | publish+barrier | merge | row loads | update)
   int64_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t pt = PROF ? int64_t(clock64()) : 0;
@@ -519,6 +913,36 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     if (it >= max_inner) {
       reason = SVM_STOP_MAX_ITER;
       break;
+    }
+    if (NWT && since >= nw.every && ntrig < nw.per_solve) {  // uniform: the polish, then select again
+      ++ntrig;
+      since = 0;
+#pragma unroll
+      for (int e = 0; e < PER; ++e)
+        if (pos(e) < m) {
+          gAw[pos(e)] = a[e];
+          gFw[pos(e)] = ft[e];
+        }
+      __threadfence_block();
+      __syncthreads();
+      int steps = 0;
+      while (NWT && steps < nw.repeat) {
+        const int code = newton_wg(m, Kw, ldw, sy, gAw, gFw, nAmat, C, eps, nw.max_free);
+        if (code == 0) break;
+        ++steps;
+        if (code == 1) break;
+      }
+      if (steps > 0) {
+#pragma unroll
+        for (int e = 0; e < PER; ++e)
+          if (pos(e) < m) {
+            a[e] = gAw[pos(e)];
+            ft[e] = gFw[pos(e)];
+          }
+        it += steps;
+        nsteps += steps;
+        continue;
+      }
     }
     int ih = int(uih), il = int(uil);
     double K12, bl_upd = bl, al;  // the second index's f in the update (first order: b_low)
@@ -759,6 +1183,9 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     const double ah_new = ah + double(s) * (al - al_new);
     const double ch = (ah_new - ah) * double(yh);
     const double cl = (al_new - al) * double(yl);
+    // a bound-status change of an updated point (bound_status): the Newton polish waits for a settled set
+    auto bst = [&](double v) { return v <= c_lo ? 0 : v >= c_hi ? 2 : 1; };
+    bool moved_status = NWT && (bst(ah_new) != bst(ah) || bst(al_new) != bst(al));
     if constexpr (W2) {
 #pragma unroll
       for (int h = 0; h < PER / 2; ++h) {
@@ -816,9 +1243,11 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
             a[e] = k == i2 ? ah2 : k == j2 ? al2 : a[e];
           }
           ++it;
+          if constexpr (NWT) moved_status = moved_status || bst(ah2) != bst(a2h) || bst(al2) != bst(a2l);
         }
       }
     }
+    if constexpr (NWT) since = moved_status ? 0 : since + 1;
     stamp(4);
   }
   // compaction in position order: pair h, then wave, then lane, then e & 1
@@ -850,6 +1279,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
       if (chg[e]) {
         cols[j] = int32_t(gid[e]);
         coef[j] = (a[e] - a0[e]) * (yp[e] ? 1.0 : -1.0);
+        // packed rows (shrinking): the column's row in the packed list, for the unit diagonal of the update
+        if (cdiag) cdiag[j] = gid[e] >= lo && gid[e] < lo + nloc ? pos_of[gid[e] - lo] : -1;
         ++j;
       }
   }
@@ -865,6 +1296,8 @@ __global__ __launch_bounds__(NT) void ws_inner_kernel(const double* __restrict__
     ctl->inner_total += it;
     ctl->changed_total += base;
     ctl->last_inner_it = it;
+    ctl->last_m = m;
+    ctl->newton_steps += nsteps;
     ctl->last_inner_reason = reason;
     publish_ctl(*ctl, pub);
   }
@@ -936,7 +1369,9 @@ __global__ __launch_bounds__(1024) void ws_cache_plan_kernel(const int32_t* __re
                                                              int32_t* __restrict__ state, int32_t* __restrict__ rd_slot,
                                                              int32_t* __restrict__ miss_ids,
                                                              int32_t* __restrict__ miss_slots,
-                                                             int32_t* __restrict__ meta) {
+                                                             int32_t* __restrict__ meta,
+                                                             const int32_t* __restrict__ cdiag,
+                                                             int32_t* __restrict__ miss_diag) {
   __shared__ int32_t wsum[16];
   __shared__ int32_t vict[kMaxWS];
   __shared__ int32_t s_nv, s_hand, s_stop;
@@ -1014,6 +1449,7 @@ __global__ __launch_bounds__(1024) void ws_cache_plan_kernel(const int32_t* __re
     }
     miss_ids[r] = id;
     miss_slots[r] = sl;
+    if (cdiag) miss_diag[r] = cdiag[k];  // packed rows: the column's packed position (the unit diagonal)
   }
   if (valid) rd_slot[k] = sl;
   __syncthreads();  // every thread has read state[0] / state[3] / state[4]
@@ -1034,14 +1470,17 @@ __global__ __launch_bounds__(1024) void ws_cache_plan_kernel(const int32_t* __re
 // A thread per RPT rows (16-byte loads: ldc is a multiple of 4); the 32 leaves of a half run as 4
 // rolled groups of 8 (8 column pairs of loads in flight per group; unrolled, the compiler hoisted all
 // 64 and ran at 3 waves / SIMD: 4.3 against 5.9 TB/s), the level of a group's last leaf depending on g.
+// Packed rows (a shrunk solve): row i of the cache is f[act[i]], i < *nrows.
 template <int RPT>
 __global__ __launch_bounds__(256) void ws_cache_fsum_kernel(const double* __restrict__ cache, int64_t ldc,
                                                              const int32_t* __restrict__ rd_slot,
                                                              const double* __restrict__ coef,
                                                              const int32_t* __restrict__ count, double* __restrict__ f,
-                                                             int64_t nloc) {
+                                                             int64_t nloc, const int32_t* __restrict__ act = nullptr,
+                                                             const int32_t* __restrict__ nrows = nullptr) {
   const int64_t i = RPT * (int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
   const int cnt = *count;
+  if (nrows) nloc = std::min<int64_t>(nloc, *nrows);
   if (i >= nloc || cnt <= 0) return;
   const int halves = (cnt + 63) / 64;
   const double* base = cache + i;
@@ -1107,27 +1546,188 @@ __global__ __launch_bounds__(256) void ws_cache_fsum_kernel(const double* __rest
   }
 #pragma unroll
   for (int r = 0; r < RPT; ++r)
-    if (i + r < nloc) f[i + r] += s[r];
+    if (i + r < nloc) f[act ? int64_t(act[i + r]) : i + r] += s[r];
 }
 
-// f[i] += the first ceil(*mcount / 64) column halves of part (the ones the GEMV wrote).
+// f[i] += the first ceil(*mcount / 64) column halves of part (the ones the GEMV wrote).  Packed rows
+// (a shrunk solve): part row i is f[act[i]], i < *nrows.
 __global__ __launch_bounds__(256) void ws_fsum_count_kernel(const double* __restrict__ part, int64_t ldp,
                                                             const int32_t* __restrict__ mcount,
-                                                            double* __restrict__ f, int64_t n) {
+                                                            double* __restrict__ f, int64_t n,
+                                                            const int32_t* __restrict__ act = nullptr,
+                                                            const int32_t* __restrict__ nrows = nullptr) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const int npart = (*mcount + 63) / 64;
+  if (nrows) n = std::min<int64_t>(n, *nrows);
   if (i >= n || npart == 0) return;
   const double* p = part + i * ldp;
   double s = 0.0;
   for (int c = 0; c < npart; ++c) s += p[c];
-  f[i] += s;
+  f[act ? int64_t(act[i]) : i] += s;
+}
+
+// ---- shrinking (decomp_shrink.h) ----------------------------------------------------------------------
+// The shrink pass after an outer iteration: every active row of this GPU (the packed list act[0 ..
+// *nrows), or all nloc rows) that the rule drops gets shr = 1; ctl->n_active counts what is left and
+// ctl->shrunk records that a pass ran (the build then unshrinks instead of stopping).  The bounds are the
+// outer iteration's build's.
+__global__ __launch_bounds__(256) void ws_shrink_pass_kernel(const double* __restrict__ f,
+                                                             const double* __restrict__ alpha,
+                                                             const int32_t* __restrict__ y, int64_t lo, int64_t nloc,
+                                                             const int32_t* __restrict__ act,
+                                                             const int32_t* __restrict__ nrows,
+                                                             uint8_t* __restrict__ shr, double C, double eps,
+                                                             double margin, DecompCtl* __restrict__ ctl) {
+  if (ctl->stop != SVM_STOP_RUNNING) return;
+  __shared__ int32_t wdrop[4];
+  const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t nr = act ? std::min<int64_t>(nloc, *nrows) : nloc;
+  const double g = margin * (ctl->b_low - ctl->b_high);  // shrink_cuts
+  const double hi_cut = ctl->b_low + g, lo_cut = ctl->b_high - g;
+  const double c_hi = C - eps, c_lo = 0.0 + eps;
+  bool drop = false;
+  if (k < nr) {
+    const int64_t i = act ? int64_t(act[k]) : k;
+    if (!shr[i]) {
+      const int32_t yi = y[lo + i];
+      const double a = alpha[lo + i], fi = f[i];
+      const bool up = (yi == 1 && a < c_hi) || (yi == -1 && a > c_lo);
+      const bool dn = (yi == 1 && a > c_lo) || (yi == -1 && a < c_hi);
+      drop = (up && !dn && fi > hi_cut) || (dn && !up && fi < lo_cut);  // shrinkable()
+      if (drop) shr[i] = 1;
+    }
+  }
+  const unsigned long long b = __ballot(drop);
+  if ((threadIdx.x & 63) == 0) wdrop[threadIdx.x >> 6] = __popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int d = wdrop[0] + wdrop[1] + wdrop[2] + wdrop[3];
+    if (d) atomicAdd(reinterpret_cast<unsigned long long*>(&ctl->n_active), static_cast<unsigned long long>(-int64_t(d)));
+    if (blockIdx.x == 0) {
+      ctl->shrunk = 1;
+      ctl->passes += 1;
+    }
+  }
+}
+
+// Repacking the active rows, 1 of 2 (one workgroup per selection block of this GPU): the block's rows
+// still active -- its packed rows [boff[b], boff[b + 1]) of the current list act, or its full range
+// [b per, (b + 1) per) before the first repack (act null) -- counted into bcnt[b].
+__global__ __launch_bounds__(256) void ws_pack_count_kernel(const int32_t* __restrict__ act,
+                                                            const int32_t* __restrict__ boff, int64_t per,
+                                                            int64_t nloc, const uint8_t* __restrict__ shr,
+                                                            int32_t* __restrict__ bcnt) {
+  __shared__ int32_t wsum[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t b0 = act ? int64_t(boff[blockIdx.x]) : int64_t(blockIdx.x) * per;
+  const int64_t b1 = act ? int64_t(boff[blockIdx.x + 1]) : std::min<int64_t>(nloc, b0 + per);
+  int c = 0;
+  for (int64_t k = b0 + t; k < b1; k += 256) c += shr[act ? int64_t(act[k]) : k] ? 0 : 1;
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if (lane == 0) wsum[w] = c;
+  __syncthreads();
+  if (t == 0) bcnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// Repacking, 2 of 2 (one workgroup per selection block): the block's new offset (the sum of the counts
+// before it; the last block also writes the total to nboff[nb] and *nrows), then its active rows in
+// order to the new list nact, pos_of[row] = the new position (-1 for the rows dropped), and the packed
+// copies of their quantised rows (Qa, N0a, WNa: the GEMV / column store's row operand).  It reads the old
+// list (act, boff) and writes the other buffer of the pair, so no block overwrites a list another reads.
+__global__ __launch_bounds__(256) void ws_pack_write_kernel(const int32_t* __restrict__ act,
+                                                            const int32_t* __restrict__ boff, int64_t per,
+                                                            int64_t nloc, const uint8_t* __restrict__ shr,
+                                                            const int32_t* __restrict__ bcnt,
+                                                            int32_t* __restrict__ nboff, int32_t* __restrict__ nrows,
+                                                            int32_t* __restrict__ nact, int32_t* __restrict__ pos_of,
+                                                            const int8_t* __restrict__ Q, const int32_t* __restrict__ N0,
+                                                            const double* __restrict__ WN, int64_t lo, int kq,
+                                                            int8_t* __restrict__ Qa, int32_t* __restrict__ N0a,
+                                                            double* __restrict__ WNa) {
+  __shared__ int32_t wsum[4];
+  __shared__ int32_t rows[256], dst[256];
+  __shared__ int32_t s_n;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nb = int(gridDim.x), b = int(blockIdx.x);
+  {  // this block's offset: the counts of the blocks before it (nb <= 512)
+    int v = 0;
+    for (int q = t; q < b; q += 256) v += bcnt[q];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) wsum[w] = v;
+    __syncthreads();
+    if (t == 0) {
+      const int base = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      nboff[b] = base;
+      s_n = base;
+      if (b == nb - 1) {
+        nboff[nb] = base + bcnt[b];
+        *nrows = base + bcnt[b];
+      }
+    }
+    __syncthreads();
+  }
+  int base = s_n;
+  const int64_t b0 = act ? int64_t(boff[b]) : int64_t(b) * per;
+  const int64_t b1 = act ? int64_t(boff[b + 1]) : std::min<int64_t>(nloc, b0 + per);
+  const int cpr = kq / 16;  // 16-byte chunks per quantised row
+  for (int64_t c0 = b0; c0 < b1; c0 += 256) {
+    const int64_t k = c0 + t;
+    const int64_t i = k < b1 ? (act ? int64_t(act[k]) : k) : -1;
+    const bool keep = i >= 0 && !shr[i];
+    const unsigned long long bal = __ballot(keep);
+    __syncthreads();  // the previous chunk is done with wsum / s_n / rows / dst
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int r = __popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+    for (int q = 0; q < 4; ++q) {
+      if (q < w) r += wsum[q];
+      tot += wsum[q];
+    }
+    if (keep) {
+      nact[base + r] = int32_t(i);
+      pos_of[i] = base + r;
+      rows[r] = int32_t(i);
+      dst[r] = base + r;
+      N0a[base + r] = N0[lo + i];
+      WNa[base + r] = WN[lo + i];
+    } else if (i >= 0) {
+      pos_of[i] = -1;
+    }
+    __syncthreads();  // rows / dst complete
+    for (int64_t c = t; c < int64_t(tot) * cpr; c += 256) {  // the kept rows' bytes, 16 at a time
+      const int rr = int(c / cpr), ch = int(c - int64_t(rr) * cpr);
+      reinterpret_cast<int4*>(Qa + int64_t(dst[rr]) * kq)[ch] =
+          reinterpret_cast<const int4*>(Q + (lo + int64_t(rows[rr])) * kq)[ch];
+    }
+    base += tot;
+  }
+}
+
+// Unshrink, on the device side: every row active again (shr = 0; the host resets the packed list to the
+// identity), the control block running with no shrink pass since (origin = now), and the no-progress test
+// disarmed for the next working set (last_inner_it = -1: the last inner solve ran on the active problem).
+__global__ void ws_unshrink_ctl_kernel(DecompCtl* __restrict__ ctl, int64_t nloc) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    ctl->stop = SVM_STOP_RUNNING;
+    ctl->shrunk = 0;
+    ctl->n_active = nloc;
+    ctl->last_inner_it = -1;
+    ctl->last_m = 0;
+  }
+}
+
+// pos_of = the identity (the packed list before any repack, or after an unshrink).
+__global__ void ws_iota_kernel(int32_t* __restrict__ v, int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = int32_t(i);
 }
 
 __global__ void ws_init_kernel(const int32_t* __restrict__ y, double* __restrict__ alpha, double* __restrict__ f,
-                               int64_t lo, int64_t nloc, int64_t n, int warm) {
+                               int64_t lo, int64_t nloc, int64_t n, int warm, DecompCtl* __restrict__ ctl) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n && !warm) alpha[i] = 0.0;
   if (i < nloc) f[i] = -static_cast<double>(y[lo + i]);  // main3.cpp:165-172
+  if (i == 0 && ctl) ctl->n_active = nloc;
 }
 
 // Warm start: the ascending ids j with alpha_j != 0 into cols, alpha_j y_j into coef, their number to
@@ -1379,10 +1979,31 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                o_cmeta = use_cache && cache_evict ? take(size_t(cache_cap) * 12) : 0;
   // K(W, W) through the narrow column store: the identity ids 0 .. kMaxWS - 1 and the column count
   const size_t o_wid = f64 ? 0 : take(kMaxWS * 4 + 64);
-  // warm start: the nonzero alphas' ids and alpha y (all n at most), the per-chunk column counts
+  // warm start (and the recomputation of f when a shrunk solve unshrinks): the nonzero alphas' ids and
+  // alpha y (all n at most), the per-chunk column counts
+  const ShrinkCfg shc = shrink_cfg(p);
+  const bool nzbuf = o.warm || shc.on;
   const int64_t nchunks = (n + kMaxWS - 1) / kMaxWS;
-  const size_t o_wcols = o.warm ? take(size_t(n) * 4) : 0, o_wcoef = o.warm ? take(size_t(n) * 8) : 0,
-               o_wcnt = o.warm ? take(size_t(nchunks + 1) * 4) : 0;
+  const size_t o_wcols = nzbuf ? take(size_t(n) * 4) : 0, o_wcoef = nzbuf ? take(size_t(n) * 8) : 0,
+               o_wcnt = nzbuf ? take(size_t(nchunks + 1) * 4) : 0;
+  // shrinking (decomp_shrink.h): the per-row flags; with packing (exact-integer rows) the packed lists of
+  // active rows (two buffers), the selection blocks' offsets into them (two), the blocks' counts, the
+  // rows' packed positions, the device-side packed row count, the moved columns' (and misses') packed
+  // positions for the unit diagonal, and the packed copies of the quantised rows
+  const char* pk_env = getenv("SVM355_DECOMP_PACK");
+  const bool pack_on = shc.on && !f64 && nloc > 0 && !(pk_env && atoi(pk_env) == 0);
+  double repack_frac = 0.75;  // repack when the active rows are at most this share of the packed ones
+  if (const char* v = getenv("SVM355_DECOMP_REPACK")) repack_frac = std::min(1.0, std::max(0.0, atof(v)));
+  const size_t o_shr = shc.on ? take(nl1) : 0;
+  // the Newton polish (decomp_newton.h): W's alpha by position and the factorisation's scratch
+  const NewtonCfg nwc = newton_cfg(p);
+  const NwDev nwd{nwc.on ? 1 : 0, nwc.every, nwc.per_solve, nwc.repeat, nwc.max_free, 0, nwc.frac};
+  const size_t o_gaw = take(kMaxWS * 8), o_namat = nwc.on ? take(size_t(kMaxWS + 2) * kMaxWS * 8) : 0;
+  const size_t o_act = pack_on ? take(nl1 * 4 * 2) : 0, o_boff = pack_on ? take(size_t(NBr + 1) * 4 * 2) : 0,
+               o_bcnt = pack_on ? take(size_t(NBr + 1) * 4) : 0, o_pos = pack_on ? take(nl1 * 4) : 0,
+               o_nrows = pack_on ? take(64) : 0, o_cdiag = pack_on ? take(kMaxWS * 4) : 0,
+               o_mdiag = pack_on ? take(kMaxWS * 4) : 0, o_Qa = pack_on ? take(nl1 * size_t(P.kq)) : 0,
+               o_N0a = pack_on ? take(nl1 * 4) : 0, o_WNa = pack_on ? take(nl1 * 8) : 0;
   int rc = ctx->ensure_ws(off);
   if (rc) return rc;
   rc = ctx->ensure_pinned(sizeof(DecompHost) * 2 + 2 * sizeof(DecompCtl) + 64);
@@ -1415,31 +2036,61 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   auto* cmeta = use_cache && cache_evict ? reinterpret_cast<int32_t*>(ws + o_cmeta) : nullptr;
   auto* wid = reinterpret_cast<int32_t*>(ws + o_wid);  // [kMaxWS] identity, then the count kMaxWS
   auto* ctl = reinterpret_cast<DecompCtl*>(ws + o_ctl);
+  auto* shr = shc.on ? reinterpret_cast<uint8_t*>(ws + o_shr) : nullptr;
+  auto* gAw = reinterpret_cast<double*>(ws + o_gaw);
+  auto* nAmat = nwc.on ? reinterpret_cast<double*>(ws + o_namat) : nullptr;
+  double* Wfw = Wf;  // the inner solve's W-local f, also the Newton polish's
+  int32_t* pact[2] = {reinterpret_cast<int32_t*>(ws + o_act), reinterpret_cast<int32_t*>(ws + o_act) + nl1};
+  int32_t* pboff[2] = {reinterpret_cast<int32_t*>(ws + o_boff), reinterpret_cast<int32_t*>(ws + o_boff) + (NBr + 1)};
+  auto* pbcnt = reinterpret_cast<int32_t*>(ws + o_bcnt);
+  auto* pos_of = reinterpret_cast<int32_t*>(ws + o_pos);
+  auto* pk_rows = reinterpret_cast<int32_t*>(ws + o_nrows);
+  auto* cdiag = reinterpret_cast<int32_t*>(ws + o_cdiag);
+  auto* mdiag = reinterpret_cast<int32_t*>(ws + o_mdiag);
+  auto* Qa = reinterpret_cast<int8_t*>(ws + o_Qa);
+  auto* N0a = reinterpret_cast<int32_t*>(ws + o_N0a);
+  auto* WNa = reinterpret_cast<double*>(ws + o_WNa);
+  // the packed state (host side): pk = the current list's buffer (-1: none, the rows in place -- before
+  // the first repack and after an unshrink), pk_bound = an upper bound of the device's packed row count
+  // (the active count the host last read: passes only drop rows)
+  int pk = -1;
+  int64_t pk_bound = nloc;
   // f += K(this GPU's rows, cols[0:*cnt]) coef: the exact-integer GEMV (column-half partials summed in
   // order) or, for FP64 rows, the moved columns' rows gathered, their block on FP64 MFMA and a row sum
   // tiled: also launch the tiled column store for updates of more than 64 misses (it exits at once
   // otherwise, but a launch over every row tile costs ~5-8 us); off after the first outer iterations,
   // where the narrow store takes any count itself (only the cold start misses hundreds of columns)
+  // Packed rows (a shrunk solve, pk >= 0): the row operand is the packed copy (Qa, N0a, WNa) of the active
+  // rows, pk_bound of them by the host's bound (the device count pk_rows gates the sums), the unit
+  // diagonal from the columns' packed positions (the inner solve's cdiag), and the sums go to f[act[k]].
   auto f_update = [&](const int32_t* cl, const double* cf, const int32_t* cnt, bool tiled = true) -> int {
     if (nloc <= 0) return SVM_OK;
+    const bool packed = pk >= 0;
+    const int8_t* Qr = packed ? Qa : Q + lo * int64_t(P.kq);
+    const int32_t* N0r = packed ? N0a : N0 + lo;
+    const double* WNr = packed ? WNa : WN + lo;
+    const int64_t nr = packed ? pk_bound : nloc, roff = packed ? 0 : lo;
+    const int32_t* pa = packed ? pact[pk] : nullptr;
+    const int32_t* pn = packed ? pk_rows : nullptr;
+    if (nr <= 0) return SVM_OK;
     if (use_cache) {  // plan the slots, compute and store the missing columns, sum every column from the cache
       hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cl, cnt, cslot, cache_cap, cst, crd, cmid,
-                         cmsl, cmeta);
+                         cmsl, cmeta, packed ? cdiag : nullptr, mdiag);
       SVMD_LAUNCH_CHECK();
-      const int rc2 = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid,
-                                            cmsl, cst + 1, kMaxWS, P, p.gamma, cache, ldc_cache, cst + 2, tiled);
+      const int rc2 = launch_igram_colstore(s, Qr, N0r, WNr, stw, nr, roff, Q, N0, WN, cmid, cmsl, cst + 1, kMaxWS, P,
+                                            p.gamma, cache, ldc_cache, cst + 2, tiled, packed ? mdiag : nullptr);
       if (rc2) return rc2;
-      hipLaunchKernelGGL((ws_cache_fsum_kernel<2>), dim3(unsigned((nloc + 511) / 512)), dim3(256), 0, s, cache,
-                         ldc_cache, crd, cf, cnt, f, nloc);
+      hipLaunchKernelGGL((ws_cache_fsum_kernel<2>), dim3(unsigned((nr + 511) / 512)), dim3(256), 0, s, cache,
+                         ldc_cache, crd, cf, cnt, f, nr, pa, pn);
       SVMD_LAUNCH_CHECK();
       return SVM_OK;
     }
     if (!f64) {
-      const int rc2 = launch_igram_gemv(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cl, cf,
-                                        cnt, kMaxWS, P, p.gamma, part, ldp);
+      const int rc2 = launch_igram_gemv(s, Qr, N0r, WNr, stw, nr, roff, Q, N0, WN, cl, cf, cnt, kMaxWS, P, p.gamma, part,
+                                        ldp, packed ? cdiag : nullptr);
       if (rc2) return rc2;
-      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nloc + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f,
-                         nloc);
+      hipLaunchKernelGGL(ws_fsum_count_kernel, dim3(unsigned((nr + 255) / 256)), dim3(256), 0, s, part, ldp, cnt, f, nr,
+                         pa, pn);
       SVMD_LAUNCH_CHECK();
       return SVM_OK;
     }
@@ -1470,21 +2121,25 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     }();
     SVMD_CHECK(hipMemcpyAsync(wid, ident.data(), ident.size() * 4, hipMemcpyHostToDevice, s));
   }
-  if (use_cache) {  // a fresh cache per fit: no point has a slot, the first free slot is 0
+  auto cache_reset = [&]() -> int {  // no point has a slot, the first free slot is 0
+    if (!use_cache) return SVM_OK;
     SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
     SVMD_CHECK(hipMemsetAsync(cst, 0, 64, s));
     if (cmeta) {  // owners and stamps -1, CLOCK bits clear
       SVMD_CHECK(hipMemsetAsync(cmeta, 0xFF, size_t(cache_cap) * 8, s));
       SVMD_CHECK(hipMemsetAsync(cmeta + 2 * int64_t(cache_cap), 0, size_t(cache_cap) * 4, s));
     }
-  }
+    return SVM_OK;
+  };
+  if ((rc = cache_reset())) return rc;  // a fresh cache per fit
+  if (shr) SVMD_CHECK(hipMemsetAsync(shr, 0, nl1, s));
   hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n,
-                     int(o.warm));
+                     int(o.warm), ctl);
   SVMD_LAUNCH_CHECK();
-  int64_t warm_cols = 0;
-  if (o.warm) {
-    // f = -y + K(:, nz) (alpha y)_nz: the nonzero alphas compacted (ascending ids), then the GEMV in
-    // chunks of kMaxWS columns, each summed into f in order (svm_decomp_train_gram does the same)
+  // f += K(:, nz) (alpha y)_nz: the nonzero alphas compacted (ascending ids), then the GEMV in chunks of
+  // kMaxWS columns, each summed into f in order (svm_decomp_train_gram does the same): a warm start, and
+  // the recomputation of f when a shrunk solve unshrinks.  The one host read: how many chunks.
+  auto nz_update = [&](int64_t* nz_out) -> int {
     auto* wcols = reinterpret_cast<int32_t*>(ws + o_wcols);
     auto* wcoef = reinterpret_cast<double*>(ws + o_wcoef);
     auto* wcnt = reinterpret_cast<int32_t*>(ws + o_wcnt);
@@ -1494,10 +2149,10 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     hipLaunchKernelGGL(ws_nz_compact_kernel, dim3(1), dim3(1024), 0, s, alpha, y, n, wcols, wcoef, wcnt + nchunks,
                        nz_h);
     SVMD_LAUNCH_CHECK();
-    SVMD_CHECK(hipStreamSynchronize(s));  // the one host read of a warm start: how many chunks
+    SVMD_CHECK(hipStreamSynchronize(s));
     const int64_t nz = *nz_h;
     if (nz < 0 || nz > n) {
-      set_error("decomposition SMO: warm-start compaction returned no count");
+      set_error("decomposition SMO: the nonzero-alpha compaction returned no count");
       return SVM_ERR_INTERNAL;
     }
     const int nch = int((nz + kMaxWS - 1) / kMaxWS);
@@ -1507,11 +2162,35 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       SVMD_LAUNCH_CHECK();
     }
     for (int c = 0; c < nch; ++c) {
-      rc = f_update(wcols + int64_t(c) * kMaxWS, wcoef + int64_t(c) * kMaxWS, wcnt + c);
-      if (rc) return rc;
+      const int rc2 = f_update(wcols + int64_t(c) * kMaxWS, wcoef + int64_t(c) * kMaxWS, wcnt + c);
+      if (rc2) return rc2;
     }
-    warm_cols = nz;
-  }
+    if (nz_out) *nz_out = nz;
+    return SVM_OK;
+  };
+  int64_t warm_cols = 0;
+  if (o.warm && (rc = nz_update(&warm_cols))) return rc;
+  // shrinking, host side: o_dev = the device's outer-iteration count when the next enqueued one runs
+  // (exact: only a stop or an unshrink turns launches into no-ops, and the host re-reads the count at
+  // an unshrink), origin = the outer count at the start or the last unshrink, seen_active = the active
+  // rows the host last read back
+  int64_t o_dev = 0, origin = 0, seen_active = nloc, min_active = nloc, unshrinks = 0, repacks = 0;
+  // repack: the active rows (not shrunk) into the other list buffer, their quantised rows copied, the
+  // column cache (whose rows are the packed ones) cleared
+  auto repack = [&]() -> int {
+    const int nb = pk < 0 ? 0 : pk ^ 1;
+    const int32_t* ca = pk < 0 ? nullptr : pact[pk];
+    const int32_t* cb = pk < 0 ? nullptr : pboff[pk];
+    hipLaunchKernelGGL(ws_pack_count_kernel, dim3(unsigned(NBr)), dim3(256), 0, s, ca, cb, sh.per, nloc, shr, pbcnt);
+    SVMD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ws_pack_write_kernel, dim3(unsigned(NBr)), dim3(256), 0, s, ca, cb, sh.per, nloc, shr, pbcnt,
+                       pboff[nb], pk_rows, pact[nb], pos_of, Q, N0, WN, lo, P.kq, Qa, N0a, WNa);
+    SVMD_LAUNCH_CHECK();
+    pk = nb;
+    pk_bound = seen_active;
+    ++repacks;
+    return cache_reset();
+  };
   if (tr) tr->count = 0;
   // Outer iterations are enqueued `batch` at a time (SVM355_DECOMP_BATCH, default 1): every kernel reads
   // the device control block, so after the stop the rest are no-op launches.  Each batch ends with a
@@ -1534,13 +2213,19 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   do {                                                                                                             \
     if (inner_j2s && S2)                                                                                           \
       hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,  \
-                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub, ipos, lo, nloc, icdiag, gAw, Wfw, nAmat, \
+                         nwd);                                                                                     \
+    else if (inner_dp && S2 && nwc.on)                                                                             \
+      hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2, false, true>), dim3(1), dim3(NT), 0, s, Kw, ldw, W,  \
+                         ctl, y, alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub, ipos, lo, nloc, icdiag, gAw, Wfw, \
+                         nAmat, nwd);                                                                              \
     else if (inner_dp && S2)                                                                                       \
       hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y,      \
-                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                      \
+                         alpha, Wf, p.C, p.eps, cols, coef, mcount, hs, pub, ipos, lo, nloc, icdiag, gAw, Wfw, nAmat, \
+                         nwd);                                                                                     \
     else                                                                                                           \
       hipLaunchKernelGGL((ws_inner_kernel<NT, PER, PR, S2>), dim3(1), dim3(NT), 0, s, Kw, ldw, W, ctl, y, alpha,   \
-                         Wf, p.C, p.eps, cols, coef, mcount, hs, pub);                                             \
+                         Wf, p.C, p.eps, cols, coef, mcount, hs, pub, ipos, lo, nloc, icdiag, gAw, Wfw, nAmat, nwd); \
   } while (0)
 #define SVM_WS_INNER(NT, PER)                \
   if (prof && inner_wss2)                    \
@@ -1584,6 +2269,34 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
   const DecompCtl* fin = nullptr;  // the readback that saw the stop
   DecompCtl* ctl_pub = nullptr;  // ctl_h as the device addresses it
   SVMD_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctl_pub), ctl_h, 0));
+  // The unshrink (decomp_shrink.h), when a readback shows kStopUnshrink: the queued batch ran as no-ops and
+  // `ev` (recorded after it) is waited for under the exchange's policy; then every row is active again, the
+  // rows are in place again (no packed list), the column cache is cleared, f is recomputed from alpha (the
+  // warm start's chunked update), and the outer loop resumes at the device's outer count.
+  const bool shrink_log = getenv("SVM355_DECOMP_SHRINK_LOG") && atoi(getenv("SVM355_DECOMP_SHRINK_LOG")) == 1;
+  auto unshrink = [&](const DecompCtl& seen, hipEvent_t ev) -> int {
+    if (ev && !(world > 1 && allgather.wait && allgather.wait(ev))) SVMD_CHECK(hipEventSynchronize(ev));
+    hipLaunchKernelGGL(ws_unshrink_ctl_kernel, dim3(1), dim3(64), 0, s, ctl, nloc);
+    SVMD_LAUNCH_CHECK();
+    SVMD_CHECK(hipMemsetAsync(shr, 0, nl1, s));
+    pk = -1;
+    pk_bound = nloc;
+    seen_active = nloc;
+    int rc2 = cache_reset();
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(ws_init_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, y, alpha, f, lo, nloc, n, 1,
+                       ctl);
+    SVMD_LAUNCH_CHECK();
+    if ((rc2 = nz_update(nullptr))) return rc2;
+    o_dev = origin = seen.outer;
+    ++unshrinks;
+    if (shrink_log) {
+      SVMD_CHECK(hipStreamSynchronize(s));
+      fprintf(stderr, "decomp: rank %d unshrink at outer %lld (%.3f ms)\n", rank, (long long)seen.outer, ms_since(t0));
+    }
+    return SVM_OK;
+  };
+  bool queued = false;  // a batch is in flight whose readback the host has not checked
   for (int64_t bt = 0;; ++bt) {
     DecompCtl* pub = tr ? nullptr : ctl_pub + (bt & 1);  // the trace path copies the block itself
     for (int bi = 0; bi < batch; ++bi) {
@@ -1592,9 +2305,15 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
         return SVM_ERR_INTERNAL;
       }
       if ((rc = solo_begin(0))) return rc;
+      // repack once the active rows the host last read are at most repack_frac of the packed ones
+      if (pack_on && NBr > 0 && bi == 0 && seen_active < pk_bound && double(seen_active) <= repack_frac * double(pk_bound))
+        if ((rc = repack())) return rc;
+      const int32_t* sact = pk >= 0 ? pact[pk] : nullptr;
+      const int32_t* sboff = pk >= 0 ? pboff[pk] : nullptr;
       if (NBr > 0)
         hipLaunchKernelGGL(wide_select ? ws_select_wide_kernel : ws_select_kernel, dim3(unsigned(NBr)), dim3(kSelNT),
-                           0, s, f, alpha, y, lo, nloc, sh.per, T, p.C, p.eps, cown, cown + NBr * T, ctl);
+                           0, s, f, alpha, y, lo, nloc, sh.per, T, p.C, p.eps, cown, cown + NBr * T, ctl, sact, sboff,
+                           shr);
       SVMD_LAUNCH_CHECK();
       if ((rc = solo_end(0))) return rc;
       if (world > 1) allgather.gather(cown, int64_t(Lr * sizeof(CandRec)), call);  // stream-ordered
@@ -1624,6 +2343,8 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
                                   &ctl->m, nullptr, 0);
         if (rc) return rc;
       }
+      const int32_t* ipos = pk >= 0 ? pos_of : nullptr;
+      int32_t* icdiag = pk >= 0 ? cdiag : nullptr;
       if (inner_nt == 65)
         SVM_WS_INNER(64, 6);
       else if (inner_nt == 64)
@@ -1637,6 +2358,13 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       SVMD_LAUNCH_CHECK();
       rc = f_update(cols, coef, mcount, bt * batch + bi < 4);
       if (rc) return rc;
+      ++o_dev;  // this outer iteration's count once it has run
+      if (shc.pass_after(o_dev, origin) && nloc > 0) {  // the shrink pass, with this outer iteration's bounds
+        const int64_t np = pk >= 0 ? pk_bound : nloc;
+        hipLaunchKernelGGL(ws_shrink_pass_kernel, dim3(unsigned((np + 255) / 256)), dim3(256), 0, s, f, alpha, y, lo,
+                           nloc, pk >= 0 ? pact[pk] : nullptr, pk_rows, shr, p.C, p.eps, shc.margin, ctl);
+        SVMD_LAUNCH_CHECK();
+      }
       if ((rc = solo_end(1))) return rc;
 #undef SVM_WS_INNER
 #undef SVM_WS_INNER_
@@ -1644,10 +2372,17 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     if (tr) {  // trace: every outer iteration is read back before the next is enqueued
       SVMD_CHECK(hipMemcpyAsync(ctl_h, ctl, sizeof(DecompCtl), hipMemcpyDeviceToHost, s));
       SVMD_CHECK(hipStreamSynchronize(s));
+      if (ctl_h->stop == kStopUnshrink) {
+        const DecompCtl seen = *ctl_h;
+        if ((rc = unshrink(seen, nullptr))) return rc;
+        continue;
+      }
       if (ctl_h->stop != SVM_STOP_RUNNING) {
         fin = ctl_h;
         break;
       }
+      seen_active = ctl_h->n_active;
+      min_active = std::min(min_active, seen_active);
       if (tr->count < tr->cap) {
         const int64_t oi = tr->count++;
         const int m = ctl_h->m;
@@ -1674,7 +2409,15 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
         }
         if (tr->n == n && tr->alpha)
           SVMD_CHECK(hipMemcpy(tr->alpha + oi * n, alpha, size_t(n) * 8, hipMemcpyDeviceToHost));
-        if (tr->n == n && tr->f) SVMD_CHECK(hipMemcpy(tr->f + oi * n, f, size_t(n) * 8, hipMemcpyDeviceToHost));
+        if (tr->n == n && tr->f) {
+          SVMD_CHECK(hipMemcpy(tr->f + oi * n, f, size_t(n) * 8, hipMemcpyDeviceToHost));
+          if (shr) {  // shrunk rows: NaN (their f is not part of the trajectory; the oracle's trace agrees)
+            std::vector<uint8_t> sh_h(static_cast<size_t>(n));
+            SVMD_CHECK(hipMemcpy(sh_h.data(), shr, size_t(n), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < n; ++i)
+              if (sh_h[size_t(i)]) tr->f[oi * n + i] = __builtin_nan("");
+          }
+        }
       }
       if (bt >= max_batches) {
         set_error("decomposition SMO: no stop after %lld outer iterations", (long long)ctl_h->outer);
@@ -1683,16 +2426,31 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
       continue;
     }
     SVMD_CHECK(hipEventRecord(ctx->ev_ctl[bt & 1], s));  // the batch's kernels published into ctl_h[bt & 1]
-    if (bt == 0) continue;  // keep one batch queued ahead of the wait
+    if (!queued) {  // keep one batch queued ahead of the wait
+      queued = true;
+      continue;
+    }
     const int64_t pb = bt - 1;
     hipEvent_t ev = ctx->ev_ctl[pb & 1];
     const auto tw = std::chrono::steady_clock::now();
     if (!(world > 1 && allgather.wait && allgather.wait(ev))) SVMD_CHECK(hipEventSynchronize(ev));
     if (o.host_wait_ms) *o.host_wait_ms += ms_since(tw);
+    if (ctl_h[pb & 1].stop == kStopUnshrink) {  // batch bt ran as no-ops: drain it, unshrink, restart the pipeline
+      const DecompCtl seen = ctl_h[pb & 1];
+      if ((rc = unshrink(seen, ctx->ev_ctl[bt & 1]))) return rc;
+      queued = false;
+      continue;
+    }
     if (ctl_h[pb & 1].stop != SVM_STOP_RUNNING) {
       fin = ctl_h + (pb & 1);  // batch bt (queued) runs as no-ops; the state is final
       break;
     }
+    seen_active = ctl_h[pb & 1].n_active;
+    min_active = std::min(min_active, seen_active);
+    if (shrink_log)
+      fprintf(stderr, "decomp: rank %d outer %lld gap %.6g active %lld packed %lld (%.3f ms)\n", rank,
+              (long long)ctl_h[pb & 1].outer, ctl_h[pb & 1].b_low - ctl_h[pb & 1].b_high, (long long)seen_active,
+              (long long)(pk >= 0 ? pk_bound : nloc), ms_since(t0));
     if (bt >= max_batches) {
       set_error("decomposition SMO: no stop after %lld outer iterations", (long long)ctl_h[pb & 1].outer);
       return SVM_ERR_INTERNAL;
@@ -1726,6 +2484,11 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     stats[5] = inner_nt;
     stats[6] = f64 ? 1 : 0;
     stats[7] = warm_cols;
+    stats[8] = unshrinks;
+    stats[9] = fin->passes;
+    stats[10] = min_active;
+    stats[11] = repacks;
+    stats[12] = fin->newton_steps;
   }
   if (r) {
     r->iterations = inner_total + 1;
@@ -2098,7 +2861,7 @@ SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t
     SVMD_CHECK(hipMemsetAsync(cslot, 0xFF, size_t(n) * 4, s));
     SVMD_CHECK(hipMemsetAsync(cst, 0, 256, s));
     hipLaunchKernelGGL(ws_cache_plan_kernel, dim3(1), dim3(kMaxWS), 0, s, cols, cnt, cslot, m, cst, crd, cmid, cmsl,
-                       nullptr);
+                       nullptr, nullptr, nullptr);
     SVMD_LAUNCH_CHECK();
     rc = launch_igram_colstore(s, Q + lo * int64_t(P.kq), N0 + lo, WN + lo, stw, nloc, lo, Q, N0, WN, cmid, cmsl,
                                cst + 1, kMaxWS, P, gamma, cache, ldc, cst + 2);
@@ -2117,6 +2880,68 @@ SVM_API int svmd_decomp_gemv_u8(void* h, const uint8_t* Xu_d, int64_t n, int64_t
   SVMD_CHECK(hipMemcpyAsync(f_out, f, size_t(nloc) * 8, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipStreamSynchronize(s));
   if (used_out) *used_out = 1;
+  return ctx->end();
+}
+
+// One Newton polish step (decomp_newton.h) on the device for a host working set (tests / timing): Kw_h
+// (m x m), y_h, a_h / f_h by position (overwritten with the result); *code = 0 / 1 / 2; prof (optional, 8
+// int64): wall-clock stamps of the phases (free set, K_FF, factorisation, back substitution, step, f) of
+// the last of `reps` runs (each from the same inputs), ticks at 100 MHz; ms_out: the mean time per step.
+SVM_API int svmd_decomp_newton_probe(void* h, const double* Kw_h, const int32_t* y_h, int32_t m, double* a_h,
+                                     double* f_h, double C, double eps, int32_t max_free, int32_t reps, int32_t* code,
+                                     int64_t* prof_h, double* ms_out) {
+  SVMD_CTX(h);
+  if (!Kw_h || !y_h || !a_h || !f_h || !code || m < 1 || m > kMaxWS || reps < 1) {
+    set_error("svmd_decomp_newton_probe: bad arguments (1 <= m <= %d)", kMaxWS);
+    return SVM_ERR_ARG;
+  }
+  int rc = ctx->begin();
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t o_k = 0, o_y = al(size_t(kMaxWS) * kMaxWS * 8), o_a = o_y + al(kMaxWS * 4), o_f = o_a + al(kMaxWS * 8),
+               o_a0 = o_f + al(kMaxWS * 8), o_f0 = o_a0 + al(kMaxWS * 8), o_c = o_f0 + al(kMaxWS * 8), o_p = o_c + 256,
+               o_A = o_p + 256, need = o_A + size_t(kMaxWS + 2) * kMaxWS * 8;
+  if ((rc = ctx->ensure_ws(need))) return rc;
+  char* ws = static_cast<char*>(ctx->ws);
+  auto* Kw = reinterpret_cast<double*>(ws + o_k);
+  auto* yd = reinterpret_cast<int32_t*>(ws + o_y);
+  auto* ad = reinterpret_cast<double*>(ws + o_a);
+  auto* fd = reinterpret_cast<double*>(ws + o_f);
+  auto* a0 = reinterpret_cast<double*>(ws + o_a0);
+  auto* f0 = reinterpret_cast<double*>(ws + o_f0);
+  auto* cd = reinterpret_cast<int32_t*>(ws + o_c);
+  auto* pd = reinterpret_cast<int64_t*>(ws + o_p);
+  auto* Ad = reinterpret_cast<double*>(ws + o_A);
+  SVMD_CHECK(hipMemcpy2DAsync(Kw, kMaxWS * 8, Kw_h, size_t(m) * 8, size_t(m) * 8, size_t(m), hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(yd, y_h, size_t(m) * 4, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(a0, a_h, size_t(m) * 8, hipMemcpyHostToDevice, s));
+  SVMD_CHECK(hipMemcpyAsync(f0, f_h, size_t(m) * 8, hipMemcpyHostToDevice, s));
+  hipEvent_t e0, e1;
+  SVMD_CHECK(hipEventCreate(&e0));
+  SVMD_CHECK(hipEventCreate(&e1));
+  float tot = 0.0f;
+  for (int r = 0; r < reps; ++r) {
+    SVMD_CHECK(hipMemcpyAsync(ad, a0, size_t(m) * 8, hipMemcpyDeviceToDevice, s));
+    SVMD_CHECK(hipMemcpyAsync(fd, f0, size_t(m) * 8, hipMemcpyDeviceToDevice, s));
+    SVMD_CHECK(hipEventRecord(e0, s));
+    hipLaunchKernelGGL(ws_newton_probe_kernel, dim3(1), dim3(256), 0, s, m, Kw, int64_t(kMaxWS), yd, ad, fd, Ad, C, eps,
+                       max_free, cd, pd);
+    SVMD_LAUNCH_CHECK();
+    SVMD_CHECK(hipEventRecord(e1, s));
+    SVMD_CHECK(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    SVMD_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    tot += ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  SVMD_CHECK(hipMemcpyAsync(a_h, ad, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipMemcpyAsync(f_h, fd, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipMemcpyAsync(code, cd, 4, hipMemcpyDeviceToHost, s));
+  if (prof_h) SVMD_CHECK(hipMemcpyAsync(prof_h, pd, 8 * 8, hipMemcpyDeviceToHost, s));
+  SVMD_CHECK(hipStreamSynchronize(s));
+  if (ms_out) *ms_out = double(tot) / reps;
   return ctx->end();
 }
 

@@ -298,6 +298,9 @@ __global__ __launch_bounds__(256) void exp_check_kernel(const double* __restrict
 // deterministic).
 // CST (with GEMV, decomposition column cache): the same columns and kernel values, stored instead of
 // reduced: K(row, colid[j]) to K[slot[j] * ldk + row] (column j's cache slot, rows contiguous).
+// diag (GEMV / CST, optional): the row operand is a packed subset of the rows (a shrunk solve's active
+// rows, decomp.hip) and column j's point is row diag[j] of it (-1: none) -- the unit diagonal is then
+// local row == diag[j] (row_off 0) instead of row_off + row == colid[j].
 template <bool EXTRA, int BK, bool RECT = false, bool GEMV = false, bool CST = false>
 __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int8_t* __restrict__ Q, int64_t n, int kq, int main0, const int32_t* __restrict__ N0,
@@ -306,7 +309,8 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
     const int32_t* __restrict__ colid = nullptr, const double* __restrict__ coef = nullptr,
     const int32_t* __restrict__ ncount = nullptr, const int8_t* __restrict__ Qc = nullptr,
     const int32_t* __restrict__ N0c = nullptr, const double* __restrict__ WNc = nullptr, int64_t row_off = 0,
-    const int32_t* __restrict__ gate = nullptr, int64_t cstride = 0, const int32_t* __restrict__ slot = nullptr) {
+    const int32_t* __restrict__ gate = nullptr, int64_t cstride = 0, const int32_t* __restrict__ slot = nullptr,
+    const int32_t* __restrict__ diag = nullptr) {
   static_assert(!GEMV || RECT, "the GEMV epilogue is a rectangular block's");
   static_assert(!CST || GEMV, "the column store is the GEMV's operands with a store epilogue");
   if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch (decomp.hip)
@@ -463,7 +467,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       const int cl = bj * 32 + l32;
       const int64_t gj = bn + cl;
       const bool colok = gj < ncol;
-      const int64_t gid = colok ? int64_t(colid[gj]) : -1;
+      const int64_t gid = colok ? int64_t(diag ? diag[gj] : colid[gj]) : -1;
       double* dst = K + (colok ? int64_t(slot[gj]) * ldk : 0);
       const int32_t nbj = n0_c[cl];
       const double wbj = EXTRA ? wn_c[cl] : 0.0;
@@ -508,7 +512,7 @@ __global__ __launch_bounds__(256, 2) void igram_tri_kernel(
       const int64_t gj = bn + cl;
       const bool colok = gj < ncol;
       const double cf = colok ? coef[gj] : 0.0;
-      const int64_t gid = colok ? int64_t(colid[gj]) : -1;
+      const int64_t gid = colok ? int64_t(diag ? diag[gj] : colid[gj]) : -1;
       const int32_t nbj = n0_c[cl];
       const double wbj = EXTRA ? wn_c[cl] : 0.0;
 #pragma unroll
@@ -644,11 +648,11 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
     const int8_t* __restrict__ Qc, const int32_t* __restrict__ N0c, const double* __restrict__ WNc,
     const int32_t* __restrict__ ids, const int32_t* __restrict__ slots, const int32_t* __restrict__ count,
     int64_t row_off, double* __restrict__ cache, int64_t ldc, int kused, const int32_t* __restrict__ gate = nullptr,
-    bool gsplit = false, bool all = false) {
+    bool gsplit = false, bool all = false, const int32_t* __restrict__ diag = nullptr) {
   __shared__ double sw[kMaxSteps];
   __shared__ double wn_c[32];
   __shared__ int64_t off_c[32];
-  __shared__ int32_t n0_c[32], id_c[32];
+  __shared__ int32_t n0_c[32], id_c[32], dg_c[32];
   extern __shared__ __attribute__((aligned(16))) char nsm[];
   if (gate && *gate != 0) return;  // a stopped decomposition solve's remaining batch
   const int cnt = *count;
@@ -674,6 +678,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
       const bool ok = t < gc;
       const int32_t id = ok ? ids[g0 + t] : -1;
       id_c[t] = id;
+      dg_c[t] = ok && diag ? diag[g0 + t] : id;
       off_c[t] = ok ? int64_t(slots[g0 + t]) * ldc : 0;
       n0_c[t] = ok ? N0c[id] : 0;
       if (EXTRA) wn_c[t] = ok ? WNc[id] : 0.0;
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(256, 3) void igram_colstore_narrow_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int cc = q + 8 * qtr + 4 * h;
-          const double kv = gi + row_off == int64_t(id_c[cc]) ? 1.0 : ex[q];
+          const double kv = gi + row_off == int64_t(dg_c[cc]) ? 1.0 : ex[q];
           if (cc < gc && rowok) cache[off_c[cc] + gi] = kv;
         }
       }
@@ -1127,7 +1132,7 @@ int run_igram_block(hipStream_t s, const double* X, int64_t n, int64_t ld, int64
 int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const double* WN, const double* stw,
                       int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                       const int32_t* cols, const double* coef, const int32_t* mcount, int64_t m, const QuantPlan& P,
-                      double gamma, double* part, int64_t ldp) {
+                      double gamma, double* part, int64_t ldp, const int32_t* diag) {
   if (n <= 0 || m <= 0) return SVM_OK;
   const int64_t tiles = (n + QBM - 1) / QBM, ctiles = (m + QBM - 1) / QBM;
   // the grid covers gc 128-column tiles per row tile; its workgroups walk further halves when *mcount
@@ -1153,7 +1158,7 @@ int launch_igram_gemv(hipStream_t s, const int8_t* Q, const int32_t* N0, const d
 #define SVM_IGRAM_GEMV(EX, B)                                                                                       \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,        \
                      P.main0, N0, WN, stw, P.w0, -gamma, part, ldp, tiles, gc * QBM, int64_t(0), cols, coef, mcount, Qc,  \
-                     N0c, WNc, row_off, nullptr, cstride)
+                     N0c, WNc, row_off, nullptr, cstride, nullptr, diag)
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM_GEMV(true, 128); else SVM_IGRAM_GEMV(true, 64);
   } else {
@@ -1171,7 +1176,7 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
                           int64_t n, int64_t row_off, const int8_t* Qc, const int32_t* N0c, const double* WNc,
                           const int32_t* ids, const int32_t* slots, const int32_t* count, int64_t m,
                           const QuantPlan& P, double gamma, double* cache, int64_t ldc, const int32_t* gate,
-                          bool tiled) {
+                          bool tiled, const int32_t* diag) {
   if (n <= 0 || m <= 0) return SVM_OK;
   const bool narrow_all = !tiled && gate && P.kq <= kNarrowMaxKq;  // the narrow store alone, any count
   if (gate && P.kq <= kNarrowMaxKq) {  // <= kNarrowCols columns: the streaming kernel (the tiled one exits)
@@ -1197,11 +1202,11 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
     if (P.main0 > 0)
       hipLaunchKernelGGL(igram_colstore_narrow_kernel<true>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
                          WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused, nullptr,
-                         false, narrow_all);
+                         false, narrow_all, diag);
     else
       hipLaunchKernelGGL(igram_colstore_narrow_kernel<false>, dim3(nwg), dim3(256), lds, s, Q, n, P.kq, P.main0, N0,
                          WN, stw, P.w0, -gamma, Qc, N0c, WNc, ids, slots, count, row_off, cache, ldc, kused, nullptr,
-                         false, narrow_all);
+                         false, narrow_all, diag);
     SVMD_LAUNCH_CHECK();
     if (narrow_all) return SVM_OK;
   }
@@ -1221,7 +1226,7 @@ int launch_igram_colstore(hipStream_t s, const int8_t* Q, const int32_t* N0, con
 #define SVM_IGRAM_CST(EX, B)                                                                                        \
   hipLaunchKernelGGL((igram_tri_kernel<EX, B, true, true, true>), dim3(unsigned(nwg)), dim3(256), 0, s, Q, n, P.kq,  \
                      P.main0, N0, WN, stw, P.w0, -gamma, cache, ldc, tiles, gc * QBM, int64_t(0), ids, nullptr, count,  \
-                     Qc, N0c, WNc, row_off, P.kq <= kNarrowMaxKq ? gate : nullptr, cstride, slots)
+                     Qc, N0c, WNc, row_off, P.kq <= kNarrowMaxKq ? gate : nullptr, cstride, slots, diag)
   if (P.main0 > 0) {
     if (bk == 128) SVM_IGRAM_CST(true, 128); else SVM_IGRAM_CST(true, 64);
   } else {

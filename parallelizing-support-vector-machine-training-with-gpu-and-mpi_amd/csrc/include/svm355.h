@@ -51,7 +51,8 @@ typedef struct svm_params {
   int32_t n_threads; // CPU worker threads (1 = the serial reference baseline)
   int32_t verbose;
   int32_t wss;       // working-set selection: 0 / 1 = first order (reference), 2 = second-order j
-  int32_t reserved;
+  int32_t shrink;    // decomposition solver shrinking: 0 = default (on), -1 = off, k > 0 = every k outer
+                     // iterations (decomp_shrink.h)
 } svm_params;
 
 typedef struct svm_result {
@@ -111,6 +112,10 @@ SVM_API int svm_smo_train_gram(const double* K, int64_t ldk, const int32_t* y, i
 // (svmd_train_decomp with a trace) and its CPU oracle's (svm_decomp_train_gram).  Caller-allocated
 // arrays for `cap` outer iterations; the stopping build is not recorded.
 #define SVM_DECOMP_MAX_WS 1024
+// int64 entries of a decomposition solve's stats array: outer / inner iterations, working-set capacity,
+// solve us, moved columns, inner threads, kernel-value path, warm columns, unshrinks, shrink passes,
+// the least active rows seen, repacks, Newton steps (decomp_shrink.h / decomp_newton.h), 3 reserved
+#define SVM_DECOMP_STATS 16
 typedef struct svm_decomp_trace {
   int64_t cap;     // capacity in outer iterations
   int64_t count;   // out: outer iterations recorded

@@ -44,7 +44,7 @@ class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto",
-                 wss: str = "first", solver: str = "auto", working_set: int = 1024):
+                 wss: str = "first", solver: str = "auto", working_set: int = 1024, shrinking=True):
         if wss not in ("first", "second"):
             raise ValueError("wss must be 'first' (the reference's selection) or 'second'")
         if solver not in ("auto", "smo", "decomp"):
@@ -52,7 +52,7 @@ class SVC:
                              "decomposition) or 'smo' (the reference's pairwise SMO over all n points)")
         self.params = SVMParams(C=C, gamma=gamma, tau=tol, eps=eps, sv_tol=sv_tol, max_iter=max_iter,
                                 n_threads=n_threads if n_threads > 0 else default_threads(),
-                                wss=2 if wss == "second" else 1)
+                                wss=2 if wss == "second" else 1, shrinking=shrinking)
         self.device = device
         self.scale = scale
         self.zero_is_positive = zero_is_positive
@@ -65,7 +65,9 @@ class SVC:
         # pixel rows, FP64 MFMA for real-valued rows; cold or warm start) -- the same support vectors,
         # b within the stop tolerance, a different pair sequence.  "smo": the reference's solver (one
         # pair per iteration over all n points, resident Gram or row cache; the CPU oracle's, the CPU
-        # default).  "auto" resolves per fit by device.
+        # default).  "auto" resolves per fit by device.  shrinking (the decomposition solver, as LIBSVM's /
+        # scikit-learn's option): selection and the f update on the active points only, the stop test
+        # still on all n (decomp_shrink.h); True, False, or a pass every k outer iterations.
         self.solver = solver
         self.working_set = int(working_set)
 

@@ -90,21 +90,19 @@ def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Op
     _gram_shape(K, n)
     a = _start(alpha, n)
     r = N.SvmResult()
-    st = (ctypes.c_int64 * 8)()
+    st = (ctypes.c_int64 * 16)()
     tr = N.DecompTrace(trace_cap, n if snapshots else 0) if trace_cap > 0 else None
     p = params.to_struct()
     N.check(N.core().svm_decomp_train_gram(N.ptr(K), K.shape[1], N.ptr(y), n, N.ptr(a), int(alpha is not None),
                                            ctypes.byref(p), int(q), float(tau_frac), int(inner_wss), ctypes.byref(r),
                                            st, ctypes.byref(tr.struct) if tr is not None else None),
             "svm_decomp_train_gram")
-    stats = {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
-             "solve_us": int(st[3]), "update_columns": int(st[4])}
-    return a, SMOResult.from_struct(r), stats, tr
+    return a, SMOResult.from_struct(r), _decomp_stats(st), tr
 
 
 def _decomp_stats(st) -> dict:
     return {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
-            "solve_us": int(st[3]), "update_columns": int(st[4])}
+            "solve_us": int(st[3]), "update_columns": int(st[4]), **N.shrink_stats(st)}
 
 
 def decomp_train_gram_dist(K: np.ndarray, y: np.ndarray, params: SVMParams, world: int = 1, comm=None,
@@ -121,7 +119,7 @@ def decomp_train_gram_dist(K: np.ndarray, y: np.ndarray, params: SVMParams, worl
     _gram_shape(K, n)
     a = _start(alpha, n)
     r = N.SvmResult()
-    st = (ctypes.c_int64 * 8)()
+    st = (ctypes.c_int64 * 16)()
     p = params.to_struct()
     if comm is not None:
         comm.error = None

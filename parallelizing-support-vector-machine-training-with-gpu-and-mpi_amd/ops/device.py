@@ -435,7 +435,7 @@ def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: 
     a, b, dd = _host_stats(mn, mx)
     d = ld if u8 else dd
     r, tm, used = N.SvmResult(), N.SvmdTiming(), ctypes.c_int32(0)
-    st = (ctypes.c_int64 * 8)()
+    st = (ctypes.c_int64 * 16)()
     p = params.to_struct()
     N.check(ctx.lib.svmd_train_decomp(ctx.bind(), N.ptr(X), int(u8), n, ld, d, N.ptr(a), N.ptr(b), N.ptr(y),
                                       N.ptr(alpha), ctypes.byref(p), int(working_set), int(warm), ctypes.byref(r),
@@ -448,7 +448,8 @@ def train_decomp(X: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: 
                                       "rows": "uint8" if u8 else "fp64", "solver": "decomp", "warm_start": bool(warm),
                                       "warm_columns": int(st[7]), "outer_iterations": int(st[0]),
                                       "inner_iterations": int(st[1]), "working_set": int(st[2]),
-                                      "update_columns": int(st[4]), "inner_threads": int(st[5])}
+                                      "update_columns": int(st[4]), "inner_threads": int(st[5]),
+                                      **N.shrink_stats(st)}
 
 
 def train_decomp_u8(Xu: torch.Tensor, y: torch.Tensor, alpha: torch.Tensor, params: SVMParams, mn, mx,
@@ -480,6 +481,24 @@ def decomp_gemv_u8(Xu: torch.Tensor, mn, mx, gamma: float, cols: np.ndarray, coe
                                         N.ptr(cols), N.ptr(coef), int(cols.size), N.ptr(out), ctypes.byref(used)),
             "svmd_decomp_gemv_u8")
     return out if used.value else None
+
+
+def decomp_newton_probe(Kw: np.ndarray, y: np.ndarray, a: np.ndarray, f: np.ndarray, C: float = 10.0,
+                        eps: float = 1e-12, max_free: int = 1024, reps: int = 1, device="cuda:0"):
+    """One Newton polish step (decomp_newton.h) on the device for a host working set: returns (alpha, f,
+    code, phase stamps (100 MHz ticks: free set, K_FF, factorisation, back substitution, step, f; then
+    |F|), mean ms per step)."""
+    Kw = np.ascontiguousarray(Kw, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.int32)
+    a = np.array(a, dtype=np.float64)
+    f = np.array(f, dtype=np.float64)
+    prof = np.zeros(8, dtype=np.int64)
+    code, ms = ctypes.c_int32(0), ctypes.c_double(0.0)
+    ctx = _ctx_for(torch.empty(1, device=device))
+    N.check(ctx.lib.svmd_decomp_newton_probe(ctx.bind(), N.ptr(Kw), N.ptr(y), len(y), N.ptr(a), N.ptr(f), float(C),
+                                             float(eps), int(max_free), int(reps), ctypes.byref(code), N.ptr(prof),
+                                             ctypes.byref(ms)), "svmd_decomp_newton_probe")
+    return a, f, int(code.value), prof, float(ms.value)
 
 
 def rbf_gram_u8(Xu: torch.Tensor, gamma: float, mn, mx, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:

@@ -48,7 +48,7 @@ def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: 
     alpha = np.empty(n, dtype=np.float64)
     mm = np.empty(2 * d, dtype=np.float64)
     r = N.SvmResult()
-    st = (ctypes.c_int64 * 8)()
+    st = (ctypes.c_int64 * 16)()
     ms = np.zeros(max(world, 1), dtype=np.float64)
     p = params.to_struct()
     t0 = time.perf_counter()
@@ -60,7 +60,8 @@ def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: 
             "iterations": int(r.iterations), "stop_reason": N.STOP_NAMES.get(int(r.stop_reason), str(r.stop_reason)),
             "n_sv": int(r.n_sv), "mn": mm[:d].copy(), "mx": mm[d:].copy(),
             "stats": {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
-                      "solve_us": int(st[3]), "update_columns": int(st[4]), "inner_threads": int(st[5])},
+                      "solve_us": int(st[3]), "update_columns": int(st[4]), "inner_threads": int(st[5]),
+                      **N.shrink_stats(st)},
             "rank_ms": [float(x) for x in ms[:world]], "wall_ms": wall}
 
 

@@ -45,6 +45,10 @@ class SVMParams:
     # working-set selection: 1 = first order (the reference, Keerthi et al.), 2 = second-order choice
     # of the second index (Fan, Chen & Lin 2005; opt-in, not the reference's trajectory)
     wss: int = 1
+    # shrinking (an active set) in the working-set decomposition solver (decomp_shrink.h): True = on
+    # (every 2 outer iterations), False = off, an int k > 0 = a pass every k outer iterations.  The
+    # stop test is still the reference's, on all n points (f recomputed when the solve unshrinks).
+    shrinking: object = True
 
     def __post_init__(self):
         # the reference hard-codes these; as parameters they must keep the problem well posed:
@@ -54,15 +58,26 @@ class SVMParams:
                                               ("sv_tol", self.sv_tol, self.sv_tol >= 0),
                                               ("max_iter", self.max_iter, self.max_iter >= 1),
                                               ("n_threads", self.n_threads, self.n_threads >= 0),
-                                              ("wss", self.wss, self.wss in (1, 2)))
+                                              ("wss", self.wss, self.wss in (1, 2)),
+                                              ("shrinking", self._shrink_code(), self._shrink_code() >= -1))
                if not (ok and np.isfinite(v))]
         if bad:
             raise ValueError("SVM parameters out of range: " + ", ".join(bad) +
                              " (C, gamma, tau > 0; eps, sv_tol >= 0; max_iter >= 1; wss 1 or 2)")
 
+    def _shrink_code(self) -> int:
+        s = self.shrinking
+        if isinstance(s, (bool, np.bool_)):
+            return 0 if s else -1
+        try:
+            k = int(s)
+        except (TypeError, ValueError):
+            return -2
+        return k if k > 0 and k == s else -2
+
     def to_struct(self, verbose: int = 0):
         return params_struct(self.C, self.gamma, self.tau, self.eps, self.sv_tol, self.max_iter,
-                             self.n_threads, verbose, self.wss)
+                             self.n_threads, verbose, self.wss, self._shrink_code())
 
     def replace(self, **kw) -> "SVMParams":
         return dataclasses.replace(self, **kw)

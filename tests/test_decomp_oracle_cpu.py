@@ -65,7 +65,8 @@ def test_oracle_trace_is_consistent(prob2k):
         moved = np.flatnonzero(d != 0)
         np.testing.assert_array_equal(moved, x["cols"])
         np.testing.assert_array_equal(d[moved] * y[moved], x["coef"])  # (a - a0) y, exactly
-        np.testing.assert_allclose(x["f"], K @ (x["alpha"] * y) - y, rtol=0, atol=1e-10)
+        act = ~np.isnan(x["f"])  # shrunk points carry NaN (their f is not part of the trajectory)
+        np.testing.assert_allclose(x["f"][act], (K @ (x["alpha"] * y) - y)[act], rtol=0, atol=1e-10)
         bh, bl = x["bounds"]
         assert bl > bh + 2 * p.tau  # only running builds are recorded
         prev = x["alpha"]
@@ -93,6 +94,49 @@ def test_oracle_warm_start(prob2k):
     np.testing.assert_array_equal(np.flatnonzero(a3 > p.sv_tol), np.flatnonzero(a > p.sv_tol))
 
 
+AGGRESSIVE = {"SVM355_DECOMP_SHRINK": "1", "SVM355_DECOMP_SHRINK_START": "1", "SVM355_DECOMP_SHRINK_MARGIN": "0"}
+
+
+@pytest.mark.parametrize("mode", ["default", "aggressive", "period3"])
+def test_shrinking_keeps_the_stop_test_on_all_points(prob2k, monkeypatch, mode):
+    """Shrinking (decomp_shrink.h): the solve on the active points, f recomputed from alpha when the active
+    problem stops, the reference's stop test on all n points.  LIBSVM's rule every outer iteration
+    (margin 0, "aggressive") shrinks points the solve needs again -- it must unshrink and still reach the
+    unshrunk solve's support vectors; the trace shows NaN exactly for the points out of the active set,
+    and only for points at a bound."""
+    K, y = prob2k
+    p = SVMParams(n_threads=4)
+    ref, rr, _, _ = C.decomp_train_gram(K, y, p.replace(shrinking=False))
+    if mode == "aggressive":
+        for k, v in AGGRESSIVE.items():
+            monkeypatch.setenv(k, v)
+    q = p.replace(shrinking=3) if mode == "period3" else p
+    a, r, st, tr = C.decomp_train_gram(K, y, q, trace_cap=400, snapshots=True)
+    assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
+    np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), np.flatnonzero(ref > p.sv_tol))
+    assert abs(r.b - rr.b) <= 10 * p.tau
+    assert st["shrink_passes"] >= 1
+    if mode == "aggressive":
+        assert st["unshrinks"] >= 1 and st["min_active"] < len(y) // 2
+    for x in tr.records():
+        out = np.isnan(x["f"])
+        ax = x["alpha"]
+        free = (ax > p.eps) & (ax < p.C - p.eps)
+        assert not np.any(out & free)  # only points at a bound are shrunk
+
+
+def test_shrinking_off_is_the_unshrunk_trajectory(prob2k, monkeypatch):
+    """shrinking=False and SVM355_DECOMP_SHRINK=0 are the same solve: no pass, nothing NaN."""
+    K, y = prob2k
+    p = SVMParams(n_threads=4, shrinking=False)
+    a, r, st, tr = C.decomp_train_gram(K, y, p, trace_cap=400, snapshots=True)
+    monkeypatch.setenv("SVM355_DECOMP_SHRINK", "0")
+    a2, r2, st2, _ = C.decomp_train_gram(K, y, p.replace(shrinking=True))
+    np.testing.assert_array_equal(a, a2)
+    assert st["shrink_passes"] == st2["shrink_passes"] == 0 and st["min_active"] == len(y)
+    assert not any(np.isnan(x["f"]).any() for x in tr.records())
+
+
 def test_oracle_reports_the_real_working_set_capacity():
     """q below 2 x blocks: every block still gives its extreme pair, so the capacity is 2 NB, and
     stats say so (decomp_shape)."""
@@ -104,12 +148,17 @@ def test_oracle_reports_the_real_working_set_capacity():
     assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
 
 
-@pytest.mark.parametrize("world", [1, 2, 4, 8])
-def test_distributed_oracle_thread_ranks_are_bit_identical(prob2k, world):
+@pytest.mark.parametrize("world,shrink", [(1, "default"), (2, "default"), (4, "default"), (8, "default"),
+                                          (2, "aggressive"), (8, "aggressive")])
+def test_distributed_oracle_thread_ranks_are_bit_identical(prob2k, world, shrink, monkeypatch):
     """decomp.hip's world > 1 form on the CPU oracle: every rank owns 1/world of the blocks and of f,
     the candidate records are all-gathered (strict loopback), each rank keeps an alpha replica (the
     native side requires them all equal).  For world | 8 the block partition is the one-rank one, so
-    alpha, b and the iteration counts equal the one-rank solve bit for bit."""
+    alpha, b and the iteration counts equal the one-rank solve bit for bit -- also when the ranks shrink
+    their own points and unshrink together (the build's bounds are global)."""
+    if shrink == "aggressive":
+        for k, v in AGGRESSIVE.items():
+            monkeypatch.setenv(k, v)
     K, y = prob2k
     p = SVMParams(n_threads=2)
     a, r, st, _ = C.decomp_train_gram(K, y, p)
@@ -156,3 +205,55 @@ def test_distributed_oracle_failing_rank_ends_every_rank(prob2k, monkeypatch):
     monkeypatch.setenv("SVM355_DECOMP_FAIL_OUTER", "3")
     with pytest.raises(NativeError, match="rank 2: .*injected failure of rank 2 at outer iteration 3"):
         C.decomp_train_gram_dist(K, y, SVMParams(n_threads=1), world=4, comm_timeout_s=30)
+
+
+@pytest.mark.parametrize("env", [{}, {"SVM355_DECOMP_NEWTON_EVERY": "3", "SVM355_DECOMP_NEWTON_FRAC": "0"},
+                                 {"SVM355_DECOMP_NEWTON_EVERY": "10", "SVM355_DECOMP_NEWTON_REPEAT": "5",
+                                  "SVM355_DECOMP_NEWTON_MAX": "30"}])
+def test_newton_polish_keeps_the_stop_test_and_the_svs(prob2k, monkeypatch, env):
+    """The Newton polish of the working set's free variables (decomp_newton.h): the solve still meets the
+    reference's stop test on all points with the pairwise solve's support vectors, and it takes fewer
+    pair updates than the polish-free solve when it fires."""
+    K, y = prob2k
+    p = SVMParams(n_threads=4)
+    monkeypatch.setenv("SVM355_DECOMP_NEWTON", "0")
+    a0, r0, st0, _ = C.decomp_train_gram(K, y, p)
+    monkeypatch.delenv("SVM355_DECOMP_NEWTON")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    a, r, st, _ = C.decomp_train_gram(K, y, p)
+    assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
+    np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), np.flatnonzero(a0 > p.sv_tol))
+    assert abs(r.b - r0.b) <= 10 * p.tau and abs(float(a @ y)) < 1e-9 * max(1.0, a.sum())
+    assert np.all((a >= -1e-9) & (a <= p.C + 1e-9))  # the pairwise clip arithmetic rounds
+    if env.get("SVM355_DECOMP_NEWTON_FRAC") == "0":  # a step at the start of every inner solve
+        assert st["newton_steps"] >= 1
+    if st["newton_steps"]:
+        assert st["inner_iterations"] < st0["inner_iterations"]
+
+
+def test_newton_step_solves_the_free_subproblem():
+    """One step on a working set whose free points stay free (a well-separated RBF set: K close to I, so
+    the free optimum alpha = 1 - mean(y) y is inside the box): afterwards every free point has the same f
+    (the QP on F solved, to rounding), f is the kernel's f of the new alpha, and sum y alpha is unchanged."""
+    from svm355._native import newton_step_probe
+
+    rng = np.random.default_rng(3)
+    m = 40
+    X = rng.normal(size=(m, 5)) * 3.0
+    sq = (X * X).sum(1)
+    Kw = np.exp(-0.5 * np.maximum(sq[:, None] + sq[None, :] - 2 * X @ X.T, 0.0))
+    np.fill_diagonal(Kw, 1.0)
+    y = np.where(np.arange(m) % 3 == 0, 1, -1).astype(np.int32)
+    a = rng.uniform(0.8, 1.2, size=m)
+    a[y == 1] *= a[y == -1].sum() / a[y == 1].sum()  # sum y a = 0
+    f = Kw @ (a * y) - y
+    a2, f2, code = newton_step_probe(Kw, y, a, f, C=10.0)
+    assert code == 1 and np.all((a2 > 0) & (a2 < 10.0))
+    np.testing.assert_allclose(f2, Kw @ (a2 * y) - y, rtol=0, atol=1e-12)
+    assert np.ptp(f2) < 1e-12
+    assert abs(float(a2 @ y)) < 1e-12 * a2.sum()
+    # cut at a bound: a box so small the step must stop at the first bound it meets
+    a3, f3, code3 = newton_step_probe(Kw, y, a * 0.1, Kw @ (0.1 * a * y) - y, C=0.15)
+    assert code3 == 2 and np.sum((a3 == 0.0) | (a3 == 0.15)) >= 1
+    np.testing.assert_allclose(f3, Kw @ (a3 * y) - y, rtol=0, atol=1e-12)

@@ -238,3 +238,113 @@ def test_streamed_selection_equals_the_cpu_oracle(n, q, monkeypatch):
     assert res.stop_reason == r_o.stop_reason == "converged"
     assert res.iterations == r_o.iterations and res.b == r_o.b
     np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
+
+
+AGGRESSIVE = {"SVM355_DECOMP_SHRINK": "1", "SVM355_DECOMP_SHRINK_START": "1", "SVM355_DECOMP_SHRINK_MARGIN": "0"}
+
+
+@pytest.mark.parametrize("mode,cache,repack", [("aggressive", "0", None), ("aggressive", "0", "1.0"),
+                                               ("aggressive", "1", "1.0"), ("default", "1", None),
+                                               ("aggressive", "1", "0")])
+def test_shrinking_trajectory_equals_the_oracle(monkeypatch, mode, cache, repack):
+    """Shrinking (decomp_shrink.h) on the device -- the shrink passes, the packed active rows (the GEMV /
+    column store over them, their unit diagonal from packed positions, the column cache cleared at every
+    repack; SVM355_DECOMP_REPACK=1.0 repacks after every drop, 0 never), the unshrink with f recomputed
+    from alpha -- against the CPU oracle's trajectory bit for bit, cold and warm; f is compared on the
+    active points (NaN elsewhere on both sides)."""
+    if mode == "aggressive":
+        for k, v in AGGRESSIVE.items():
+            monkeypatch.setenv(k, v)
+    monkeypatch.setenv("SVM355_DECOMP_CCACHE", cache)
+    if repack is not None:
+        monkeypatch.setenv("SVM355_DECOMP_REPACK", repack)
+    n = 6000
+    tr = synthetic_mnist(n, seed=61).compact()
+    Xu, mn, mx = _dev_rows(tr)
+    K = _exact_gram_host(Xu, mn, mx, n)
+    yd = torch.from_numpy(tr.y).to(DEV)
+    half = tr.subset(0, n // 2)
+    a_half = SVC(device="cuda:0", solver="decomp").fit(half.X, half.y).alpha_
+    for warm in (False, True):
+        a0 = np.concatenate([a_half, np.zeros(n - n // 2)]) if warm else np.zeros(n)
+        alpha = torch.from_numpy(a0.copy()).to(DEV)
+        dt = N.DecompTrace(400, n)
+        res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx, warm=warm, trace=dt)
+        a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), alpha=a0 if warm else None,
+                                                 trace_cap=400, snapshots=True)
+        _compare(dt, ot)
+        a = alpha.cpu().numpy()
+        np.testing.assert_array_equal(a, a_o)
+        assert res.stop_reason == r_o.stop_reason == "converged" and res.b == r_o.b
+        assert tm["unshrinks"] == st_o["unshrinks"] and tm["shrink_passes"] == st_o["shrink_passes"]
+        if mode == "aggressive":
+            assert tm["unshrinks"] >= 1 and tm["min_active"] < n // 2
+            if repack != "0":
+                assert tm["repacks"] >= 1
+
+
+def _kkt_gap_fp64(X, y, a, p):
+    """b_low - b_high over ALL points from an independent FP64 RBF (torch, min-max scaled rows)."""
+    Xs = torch.from_numpy(X.astype(np.float64)).to(DEV)
+    mn, mx = Xs.min(0).values, Xs.max(0).values
+    rng = torch.where(mx - mn < 1e-12, torch.ones_like(mx), mx - mn)
+    Xs = (Xs - mn) / rng
+    sq = (Xs * Xs).sum(1)
+    ay = torch.from_numpy(a * y).to(DEV)
+    f = torch.empty(len(y), dtype=torch.float64, device=DEV)
+    for i0 in range(0, len(y), 4096):
+        B = Xs[i0:i0 + 4096] @ Xs.T
+        Kb = torch.exp(-p.gamma * torch.clamp(sq[i0:i0 + 4096, None] + sq[None, :] - 2.0 * B, min=0.0))
+        f[i0:i0 + 4096] = Kb @ ay
+    f = f.cpu().numpy() - y
+    hi = ((y == 1) & (a < p.C - p.eps)) | ((y == -1) & (a > p.eps))
+    lo = ((y == 1) & (a > p.eps)) | ((y == -1) & (a < p.C - p.eps))
+    return f[lo].max() - f[hi].min()
+
+
+@pytest.mark.parametrize("n", [60000])
+def test_shrunk_solve_meets_the_stop_test_on_all_points(n):
+    """The headline shape with shrinking (the default) against shrinking=False: the same support
+    vectors, b within the stop tolerance, and the reference's stop test recomputed on all n points from
+    an independent FP64 kernel (not the solver's int8-exact values, and not its f)."""
+    tr = synthetic_mnist(n, seed=2024).compact()
+    p = SVMParams()
+    on = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
+    off = SVC(device="cuda:0", solver="decomp", shrinking=False).fit(tr.X, tr.y)
+    np.testing.assert_array_equal(on.support_, off.support_)
+    assert abs(on.b_ - off.b_) <= 10 * p.tau
+    assert on.timings_["shrink_passes"] >= 1 and on.timings_["min_active"] < n
+    assert off.timings_["shrink_passes"] == 0
+    y = tr.y.astype(np.float64)
+    assert _kkt_gap_fp64(tr.X, y, on.alpha_, p) <= 2 * p.tau + 1e-9
+
+
+@pytest.mark.parametrize("env", [{"SVM355_DECOMP_NEWTON_EVERY": "5", "SVM355_DECOMP_NEWTON_FRAC": "0"},
+                                 {"SVM355_DECOMP_NEWTON_EVERY": "20", "SVM355_DECOMP_NEWTON_REPEAT": "4",
+                                  "SVM355_DECOMP_SHRINK": "1", "SVM355_DECOMP_SHRINK_START": "1"},
+                                 {"SVM355_DECOMP_NEWTON_EVERY": "10", "SVM355_DECOMP_CCACHE": "1",
+                                  "SVM355_DECOMP_NEWTON_FRAC": "0", "SVM355_DECOMP_NEWTON_MAX": "150"}])
+def test_newton_polish_trajectory_equals_the_oracle(monkeypatch, env):
+    """The Newton polish of the working set's free variables (decomp_newton.h, newton_wg in the inner
+    solve: a left-looking panel Cholesky of K_FF with two right-hand-side rows, the back substitution in
+    one wave, the cut at the first bound) against the oracle's sequential reference, bit for bit: every
+    working set, moved column, coefficient, alpha and f; forced often here (every 5-20 quiet chain
+    iterations, from the first working set), with shrinking, with the column cache and a small |F| cap."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    fired = 0
+    for n, seed in ((2000, 5), (6000, 61)):
+        tr = synthetic_mnist(n, seed=seed).compact()
+        Xu, mn, mx = _dev_rows(tr)
+        K = _exact_gram_host(Xu, mn, mx, n)
+        yd = torch.from_numpy(tr.y).to(DEV)
+        alpha = torch.empty(n, dtype=torch.float64, device=DEV)
+        dt = N.DecompTrace(400, n)
+        res, tm = D.train_decomp(Xu, yd, alpha, SVMParams(), mn, mx, trace=dt)
+        a_o, r_o, st_o, ot = C.decomp_train_gram(K, tr.y, SVMParams(n_threads=8), trace_cap=400, snapshots=True)
+        _compare(dt, ot)
+        np.testing.assert_array_equal(alpha.cpu().numpy(), a_o)
+        assert res.stop_reason == r_o.stop_reason == "converged" and res.b == r_o.b
+        assert tm["newton_steps"] == st_o["newton_steps"], (tm["newton_steps"], st_o["newton_steps"])
+        fired += tm["newton_steps"]
+    assert fired >= 1
