@@ -97,8 +97,10 @@ def main(argv=None):
                     help="under torchrun: when the RCCL rank cannot be set up or fails its preflight on any rank, time "
                          "the same ranks over host-staged gloo exchanges (config.parallelism then ends in -gloo) "
                          "instead of exiting non-zero with the failing rank and step")
-    ap.add_argument("--input", choices=["u8", "f64"], default="u8",
-                    help="host row format: uint8 pixels (default) or FP64 as in the reference")
+    ap.add_argument("--input", choices=["u8", "f64", "f64-real"], default="u8",
+                    help="host row format: uint8 pixels (default), FP64 as in the reference, or f64-real: the same "
+                         "rows plus a deterministic uniform [0, 0.5) offset per value (real-valued data: no "
+                         "exact-integer plan, every kernel value on FP64 MFMA; --parallel decomp / cascade)")
     ap.add_argument("--cascade", action="store_true", help="run the cascade even with one GPU")
     ap.add_argument("--cascade-steps", type=int, default=2,
                     help="N > 1 with the distributed decomposition headline: the star and tree cascades (BASELINE "
@@ -202,10 +204,15 @@ def main(argv=None):
     if a.input == "u8":
         full, part = full.compact(), part.compact()
         te = te.compact() if te is not None else None
+    elif a.input == "f64-real":  # real-valued rows: the same pixels plus a fixed per-value offset in [0, 0.5)
+        full.X = full.X + np.random.default_rng(a.seed + 7).uniform(0.0, 0.5, size=full.X.shape)
+        part = full.subset(lo, hi)
+        if te is not None:
+            te.X = te.X + np.random.default_rng(a.seed + 8).uniform(0.0, 0.5, size=te.X.shape)
     pixel = full.X.dtype == np.uint8 and full.X.dtype == part.X.dtype
 
     mode = "single" if not distributed else ("cascade" if a.cascade else a.parallel)
-    if mode == "auto" and a.solver == "decomp" and pixel:
+    if mode == "auto" and a.solver == "decomp" and (pixel or a.input == "f64-real"):
         mode = "decomp"  # the headline solver, distributed (bit-identical to its one-GPU trajectory)
     auto = mode == "auto"
     fallback_reason = None
@@ -214,8 +221,9 @@ def main(argv=None):
         if mode == "cascade":
             fallback_reason = ("not pixel rows" if not pixel else "cpu device" if cpu else "second-order selection"
                                if a.wss != "first" else "cascade requested" if a.cascade else "more than 8 GPUs")
-    elif mode == "smo" and (cpu or not pixel) or mode == "decomp" and not cpu and not pixel:
-        print(f"bench.py: --parallel {mode} needs uint8 pixel rows on GPUs", file=sys.stderr)
+    elif mode == "smo" and (cpu or not pixel) or mode == "decomp" and not cpu and not pixel and a.input != "f64-real":
+        print(f"bench.py: --parallel {mode} needs uint8 pixel rows on GPUs (or --input f64-real for the "
+              "decomposition's FP64 rows)", file=sys.stderr)
         return 2
     if hostcomm and mode not in ("decomp", "cascade"):
         print("bench.py: --transport hostcomm runs the per-process decomposition and cascade ranks", file=sys.stderr)
@@ -706,7 +714,9 @@ def main(argv=None):
             "scaling": "strong",
             "vs_baseline": round(value / REF_GPU_S, 6) if a.n == 60000 else None,  # the reference's 60k time
             "dtype": "fp64",
-            "data": "synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)",
+            "data": ("synthetic (deterministic MNIST-shaped 784-dim uint8 pixels, digit-1 one-vs-rest)"
+                     if a.input != "f64-real" else "synthetic (MNIST-shaped 784-dim pixels plus a uniform [0, 0.5) "
+                     "offset per value: real-valued FP64 rows, digit-1 one-vs-rest)"),
             "config": {
                 "model": (f"RBF SVM, {a.wss}-order SMO" if a.solver == "smo" and mode != "decomp"
                           else "RBF SVM, SMO-type working-set decomposition (reference stop test on all n points)")
@@ -720,6 +730,7 @@ def main(argv=None):
                       ("in-process thread ranks" if distributed else "single process"),
             **({"device": "cpu (C++ oracle; launch-path check, not a benchmark)"} if cpu else {}),
             "host_rows": "uint8 (the device reads the bytes; only the SVs are widened to fp64)" if a.input == "u8"
+                         else "fp64 (real-valued)" if a.input == "f64-real"
                          else "fp64",
             "speedup_vs_serial": round(REF_SERIAL_S / value, 2) if a.n == 60000 else None,
             "speedup_vs_ref_gpu": round(REF_GPU_S / value, 2) if a.n == 60000 else None,

@@ -284,8 +284,12 @@ _HIP_SIGS = {
     "svmd_minmax_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P]),
     "svmd_cascade_group_decomp": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32, _P,
                                             POINTER(SvmResult), POINTER(c_int64), _P, _P]),
+    "svmd_cascade_group_decomp_rows": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32,
+                                                 _P, POINTER(SvmResult), POINTER(c_int64), _P, _P]),
     "svmd_cascade_rank_decomp": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32, _P,
                                            POINTER(SvmResult), POINTER(c_int64), _P, _P]),
+    "svmd_cascade_rank_decomp_rows": (c_int32, [c_void_p, _P, _P, c_int64, c_int64, POINTER(SvmParams), c_int32,
+                                                _P, POINTER(SvmResult), POINTER(c_int64), _P, _P]),
     "svmd_rbf_gram_u8": (c_int32, [c_void_p, _P, c_int64, c_int64, _P, _P, c_double, _P, c_int64, POINTER(c_int32)]),
     "svmd_sv_rows_u8": (c_int32, [c_void_p, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P]),
     "svmd_count_correct": (c_int32, [c_void_p, _P, _P, c_int64, c_int32, POINTER(c_int64)]),

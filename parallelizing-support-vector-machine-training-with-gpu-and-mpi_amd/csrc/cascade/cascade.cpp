@@ -265,9 +265,11 @@ class Rank {
     B_.d2h(mn_h.data(), mn.get(), d_ * 8);
     B_.d2h(mx_h.data(), mx.get(), d_ * 8);
   }
-  // The training set a checkpoint belongs to: FNV-1a over n and the global column bounds (a resume on
-  // other data would otherwise warm-start from another problem's support vectors without a word).
-  uint64_t data_fingerprint(int64_t n_total) const {
+  // The training set a checkpoint belongs to: FNV-1a over n, the global column bounds and every rank's
+  // rows, labels and ids (rows_hash, combined in rank order; a resume on other data -- other rows with
+  // the same bounds, or the same rows with another positive class -- would otherwise warm-start from
+  // another problem's support vectors without a word).
+  uint64_t data_fingerprint(int64_t n_total, uint64_t rows_hash) const {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&h](const void* p, size_t bytes) {
       const auto* c = static_cast<const unsigned char*>(p);
@@ -276,6 +278,7 @@ class Rank {
     mix(&n_total, 8);
     mix(mn_h.data(), mn_h.size() * 8);
     mix(mx_h.data(), mx_h.size() * 8);
+    mix(&rows_hash, 8);
     return h;
   }
   uint64_t fingerprint = 0;  // set by run_cascade after the global scaling
@@ -539,7 +542,28 @@ CascadeOutput run_cascade(Transport& t, Backend& B, const void* X, bool u8, cons
   const auto t0 = Clock::now();
   R.phase[kPhSetup] = ms_between(t_entry, t0) - R.phase[kPhUpload];
   R.scale_global(part);
-  R.fingerprint = R.data_fingerprint(n_total);
+  // with checkpoints, this rank's rows as passed, labels and ids hashed (64-bit words, FNV-1a style; ~10
+  // GB/s on the host) and the hashes gathered in rank order
+  uint64_t rows_hash = 0;
+  if (t.bcast_i64(cfg.checkpoint_dir.empty() ? 0 : 1, 0)) {
+    auto hash_words = [](uint64_t h, const void* p, size_t bytes) {
+      const auto* c = static_cast<const unsigned char*>(p);
+      size_t i = 0;
+      for (; i + 8 <= bytes; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, c + i, 8);
+        h = (h ^ w) * 1099511628211ull;
+      }
+      for (; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
+      return h;
+    };
+    uint64_t local = 1469598103934665603ull;
+    local = hash_words(local, X, size_t(n_part) * size_t(d) * (u8 ? 1 : 8));
+    local = hash_words(local, y, size_t(n_part) * 4);
+    if (ids) local = hash_words(local, ids, size_t(n_part) * 8);
+    for (int64_t v : t.allgather_i64(int64_t(local))) rows_hash = hash_words(rows_hash ^ 0x9E3779B97F4A7C15ull, &v, 8);
+  }
+  R.fingerprint = R.data_fingerprint(n_total, rows_hash);
   DSet G = R.make(0);  // global SV set (meaningful on rank 0; broadcast each round)
   std::unordered_set<int64_t> global_ids;
   double b = 0.0;

@@ -840,10 +840,13 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
   return "";
 }
 
-// One rank of the distributed decomposition SMO (decomp.hip): the rank's GPU gets all n uint8 rows
-// and labels, quantises them, and runs the solve over its block range with the candidate records
-// all-gathered through `tr` (null: one GPU).  alpha_out (host, n doubles) may be null.
-void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+// One rank of the distributed decomposition SMO (decomp.hip): the rank's GPU gets all n rows and
+// labels and runs the solve over its block range with the candidate records all-gathered through `tr`
+// (null: one GPU).  u8: uint8 pixel rows (quantised on the device: exact-integer kernel values); else
+// FP64 rows (n x d, the reference's format, mpi_svm_main2.cpp:316-402 / mpi_svm_main3.cpp:433-518):
+// min-max scaled on the device, then the exact-integer plan when their values admit one, FP64-MFMA kernel
+// values otherwise (real-valued data; decomp_fit_rows).  alpha_out (host, n doubles) may be null.
+void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, const int32_t* y, int64_t n, int64_t d,
                     const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
                     double* mm_out, DecompSolo* solo = nullptr, double* host_wait_ms = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -855,8 +858,9 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   // Each GPU copies 1/world of the rows from the host over its own link and the rows are all-gathered
   // over xGMI (in place), instead of every GPU pulling all n rows through the host: world concurrent
   // pageable copies of the whole set would be staged through host memory world times.
-  const int64_t rows_per = (n + world - 1) / world, chunk = rows_per * d;
-  auto* Xd = static_cast<uint8_t*>(be.alloc(chunk * world));
+  const int64_t ld = u8 ? d : svmd_padded_dim(d), esz = u8 ? 1 : 8;
+  const int64_t rows_per = (n + world - 1) / world, chunk = rows_per * ld * esz;
+  auto* Xd = static_cast<char*>(be.alloc(chunk * world));
   auto* yd = static_cast<int32_t*>(be.alloc(n * 4));
   auto* ad = static_cast<double*>(be.alloc(n * 8));
   auto* mm = static_cast<double*>(be.alloc(2 * d * 8));
@@ -868,14 +872,25 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
     }
   } fr{be, {Xd, yd, ad, mm}};
   const int64_t r0 = std::min<int64_t>(n, rank * rows_per), r1 = std::min<int64_t>(n, r0 + rows_per);
+  const char* Xh = static_cast<const char*>(Xv);
+  auto upload = [&](int64_t a0, int64_t a1, char* dst) {  // host rows [a0, a1) to the device (FP64: padded to ld)
+    if (a1 <= a0) return;
+    if (u8)
+      be.h2d(dst, Xh + a0 * d, (a1 - a0) * d);
+    else
+      be.upload_rows(Xh + a0 * d * 8, false, a1 - a0, d, reinterpret_cast<double*>(dst));
+  };
   if (world > 1) {
-    be.h2d(Xd + rank * chunk, X + r0 * d, (r1 - r0) * d);
+    upload(r0, r1, Xd + rank * chunk);
     tr->allgather(Xd + rank * chunk, chunk, Xd);  // rank r's slice at r * chunk = row r * rows_per
   } else {
-    be.h2d(Xd, X, n * d);
+    upload(0, n, Xd);
   }
   be.h2d(yd, y, n * 4);
-  check(svmd_minmax_u8(ctx, Xd, n, d, mm, mm + d), "svmd_minmax_u8");
+  if (u8)
+    check(svmd_minmax_u8(ctx, reinterpret_cast<uint8_t*>(Xd), n, d, mm, mm + d), "svmd_minmax_u8");
+  else  // the single-GPU SVC's scaling (svmd_preprocess: column min / max, then the rows scaled in place)
+    check(svmd_preprocess(ctx, reinterpret_cast<double*>(Xd), n, d, ld, mm, mm + d, nullptr, 0), "svmd_preprocess");
   std::vector<double> mmh(size_t(2 * d));
   be.d2h(mmh.data(), mm, 2 * d * 8);
   if (mm_out) std::memcpy(mm_out, mmh.data(), size_t(2 * d) * 8);
@@ -895,11 +910,19 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const uint8_t* X, const int32
   // fault injection (tests): SVM355_DECOMP_FAIL_RANK / _OUTER make that rank fail at that outer
   // iteration inside the solve (run_decomp) while the others wait in their candidate all-gather; the
   // group's abort must end every rank with an error, not a hang
-  check(decomp_fit_u8(ctx, Xd, n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res, stats, &used, &prep, o),
-        "decomposition SMO");
+  if (u8)
+    check(decomp_fit_u8(ctx, reinterpret_cast<uint8_t*>(Xd), n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res,
+                        stats, &used, &prep, o),
+          "decomposition SMO");
+  else
+    check(decomp_fit_rows(ctx, reinterpret_cast<double*>(Xd), n, ld, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res,
+                          stats, &used, &prep, o),
+          "decomposition SMO");
   if (!used)
-    throw CascadeError("decomposition SMO: the rows are not integer pixels (no exact-integer plan), or n = " +
-                       std::to_string(n) + " is beyond the solver's 2,097,152 rows");
+    throw CascadeError(u8 ? "decomposition SMO: the uint8 rows admit no exact-integer plan (more than 4,096 int8 "
+                            "columns after grouping), or n = " + std::to_string(n) + " is outside 2 .. 2^31 - 2"
+                          : "decomposition SMO: n = " + std::to_string(n) + " is outside 2 .. 2^31 - 2, or the "
+                            "FP64-row solve's workspace (n / world x 1,024 doubles per GPU) does not fit");
   if (alpha_out) be.d2h(alpha_out, ad, n * 8);
   be.sync();
   if (r) *r = res;
@@ -1091,12 +1114,11 @@ SVM_API svm_cascade_out* svmd_cascade_group_fit(void* h, const void* X, int32_t 
 
 // Distributed decomposition SMO over the group's ranks: every rank's GPU holds all n uint8 rows (host
 // X, n x d) and owns a block range of f; one candidate all-gather per outer iteration.  alpha_out
-// (host, n doubles) and r come from rank 0 (every rank's alpha is the same replica); stats: 8 int64
+// (host, n doubles) and r come from rank 0 (every rank's alpha is the same replica); stats: SVM_DECOMP_STATS int64
 // (decomp.h) from rank 0; rank_ms (world doubles, may be null): each rank's wall time; mm_out (2 d
 // doubles, may be null): the column min / max the model's scaling uses.
-SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
-                                      const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
-                                      int64_t* stats, double* rank_ms, double* mm_out) {
+static int group_decomp(void* h, const void* X, bool u8, const int32_t* y, int64_t n, int64_t d, const svm_params* pp,
+                        int32_t q, double* alpha_out, svm_result* r, int64_t* stats, double* rank_ms, double* mm_out) {
   auto* g = static_cast<Group*>(h);
   if (!g || !X || !y || n < 2 || d <= 0) {
     set_error("svmd_cascade_group_decomp: bad arguments");
@@ -1138,7 +1160,7 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
         token,
         [&](int rr) {
           if (hipSetDevice(g->devices[size_t(rr)]) != hipSuccess) throw CascadeError("hipSetDevice failed");
-          decomp_on_rank(*g->be[size_t(rr)], P > 1 ? tr[size_t(rr)] : nullptr, X, y, n, d, p, q,
+          decomp_on_rank(*g->be[size_t(rr)], P > 1 ? tr[size_t(rr)] : nullptr, X, u8, y, n, d, p, q,
                          rr == 0 ? alpha_out : nullptr, rr == 0 ? r : nullptr, rr == 0 ? stats : nullptr,
                          &ms[size_t(rr)], rr == 0 ? mm_out : nullptr, solo.empty() ? nullptr : &solo[size_t(rr)],
                          &g->host_wait_ms[size_t(rr)]);
@@ -1181,6 +1203,20 @@ SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* 
   return SVM_OK;
 }
 
+SVM_API int svmd_cascade_group_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                      const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                      int64_t* stats, double* rank_ms, double* mm_out) {
+  return group_decomp(h, X, true, y, n, d, pp, q, alpha_out, r, stats, rank_ms, mm_out);
+}
+
+// The same over FP64 rows (host X, n x d, unscaled): real-valued data train with FP64-MFMA kernel values
+// (decomp_fit_rows), pixel values held as doubles with the exact-integer plan.
+SVM_API int svmd_cascade_group_decomp_rows(void* h, const double* X, const int32_t* y, int64_t n, int64_t d,
+                                           const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                           int64_t* stats, double* rank_ms, double* mm_out) {
+  return group_decomp(h, X, false, y, n, d, pp, q, alpha_out, r, stats, rank_ms, mm_out);
+}
+
 // The last distributed decomposition fit's host time per rank blocked in the per-batch waits (the one
 // wait per outer iteration: RCCL's event poll under the deadline, or hipEventSynchronize); returns P.
 SVM_API int64_t svmd_cascade_group_decomp_waits(void* h, double* out, int64_t cap) {
@@ -1205,9 +1241,8 @@ SVM_API int64_t svmd_cascade_group_decomp_solo(void* h, double* out, int64_t cap
 }
 
 // One process rank of the distributed decomposition SMO (every rank passes all n rows and labels).
-SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
-                                     const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
-                                     int64_t* stats, double* ms_out, double* mm_out) {
+static int rank_decomp(void* h, const void* X, bool u8, const int32_t* y, int64_t n, int64_t d, const svm_params* pp,
+                       int32_t q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out, double* mm_out) {
   auto* pr = static_cast<ProcRank*>(h);
   if (!pr || !X || !y || n < 2 || d <= 0) {
     set_error("svmd_cascade_rank_decomp: bad arguments");
@@ -1227,8 +1262,8 @@ SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y
     pr->set_policy(WaitPolicy{nullptr, pr->timeout_s});
     try {
       pr->host_wait_ms = 0.0;
-      decomp_on_rank(*pr->be, pr->tr->world() > 1 ? pr->tr.get() : nullptr, X, y, n, d, p, q, alpha_out, r, stats,
-                     ms_out, mm_out, nullptr, &pr->host_wait_ms);
+      decomp_on_rank(*pr->be, pr->tr->world() > 1 ? pr->tr.get() : nullptr, X, u8, y, n, d, p, q, alpha_out, r,
+                     stats, ms_out, mm_out, nullptr, &pr->host_wait_ms);
     } catch (...) {
       pr->tr->abort();  // the peers' waits fail too
       pr->broken = true;
@@ -1239,6 +1274,19 @@ SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y
     set_error("decomposition SMO: %s", e.what());
     return SVM_ERR_DEVICE;
   }
+}
+
+SVM_API int svmd_cascade_rank_decomp(void* h, const uint8_t* X, const int32_t* y, int64_t n, int64_t d,
+                                     const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                     int64_t* stats, double* ms_out, double* mm_out) {
+  return rank_decomp(h, X, true, y, n, d, pp, q, alpha_out, r, stats, ms_out, mm_out);
+}
+
+// The same over FP64 rows (svmd_cascade_group_decomp_rows).
+SVM_API int svmd_cascade_rank_decomp_rows(void* h, const double* X, const int32_t* y, int64_t n, int64_t d,
+                                          const svm_params* pp, int32_t q, double* alpha_out, svm_result* r,
+                                          int64_t* stats, double* ms_out, double* mm_out) {
+  return rank_decomp(h, X, false, y, n, d, pp, q, alpha_out, r, stats, ms_out, mm_out);
 }
 
 // The last svmd_cascade_rank_decomp fit's host time blocked in the per-batch waits (ms).

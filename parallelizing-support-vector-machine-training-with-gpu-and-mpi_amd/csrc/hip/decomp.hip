@@ -400,6 +400,80 @@ __global__ __launch_bounds__(64) void ws_gather_kernel(const int8_t* __restrict_
 // Returns 0 (nothing changed), 1 (full step) or 2 (cut at a bound), the same in every thread.
 constexpr int kNwPW = 16;      // panel width
 constexpr int kNwMax = 512;    // |F| bound of the LDS buffers (NewtonCfg::max_free is clamped to it)
+// The factorisation's row updates for one panel (newton_wg): pb[r][c] = A[p0 + r][p0 + c] - sum_{j < p0}
+// L[p0 + r][j] L[p0 + c][j] (ascending j) for the panel's rows r < ract and columns c < pw (lower entries;
+// the right-hand-side rows nf, nf + 1 take every column), lp[j][c] = L[p0 + c][j].  CPT columns per
+// thread (kNwPW / CPT threads per row), up to NQ rows per thread.
+template <int CPT, int NQ>
+__device__ __forceinline__ void newton_rows(const double* __restrict__ Amat, int64_t ldA, const double* __restrict__ lp,
+                                            double* __restrict__ pb, int p0, int pw, int nf, int ract, int t, int nt) {
+  constexpr int G = kNwPW / CPT;  // threads per row
+  double sv[NQ][CPT];
+  const double* ar[NQ];
+  bool rv[NQ];
+  int rr[NQ], cg[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int item = t + nt * q;
+    rr[q] = item / G;
+    cg[q] = (item - rr[q] * G) * CPT;  // the thread's first column
+    rv[q] = rr[q] < ract;
+    const int i = p0 + rr[q];
+    ar[q] = Amat + int64_t(rv[q] ? i : 0) * ldA;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int cc = cg[q] + c;
+      sv[q][c] = rv[q] && cc < pw && (i >= nf || p0 + cc <= i) ? ar[q][p0 + cc] : 0.0;
+    }
+  }
+  int nq = 0;  // rows this thread has (uniform upper bound per wave is not needed: masked by rv)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) nq += rv[q] ? 1 : 0;
+  if (nq > 0) {
+    // the row entries 8 at a time, the next 8 loaded while these are used (one wave per SIMD: nothing
+    // else hides the loads' latency)
+    double nxt[NQ][8];
+    auto load8 = [&](int j, double (&dst)[NQ][8]) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          const f64x2 v = q < nq && j < p0 ? *reinterpret_cast<const f64x2*>(ar[q] + j + u) : f64x2{0.0, 0.0};
+          dst[q][u] = v[0];
+          dst[q][u + 1] = v[1];
+        }
+    };
+    load8(0, nxt);
+    for (int j = 0; j < p0; j += 8) {  // p0 is a multiple of 16
+      double lij[NQ][8];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) lij[q][u] = nxt[q][u];
+      load8(j + 8, nxt);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const f64x2* lr = reinterpret_cast<const f64x2*>(lp + (j + u) * kNwPW + cg[0]);
+#pragma unroll
+        for (int c2 = 0; c2 < CPT / 2; ++c2) {
+          const f64x2 l2 = lr[c2];
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+            if (q < nq) {
+              sv[q][2 * c2] = __builtin_fma(-lij[q][u], l2[0], sv[q][2 * c2]);
+              sv[q][2 * c2 + 1] = __builtin_fma(-lij[q][u], l2[1], sv[q][2 * c2 + 1]);
+            }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    if (rv[q])
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) pb[rr[q] * kNwPW + cg[q] + c] = sv[q][c];
+}
+
 __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, int64_t ldw, const int8_t* __restrict__ sy,
                                       double* __restrict__ gA, double* __restrict__ gF, double* __restrict__ Amat,
                                       double C, double eps, int max_free, int64_t* __restrict__ prof = nullptr) {
@@ -437,9 +511,9 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
   if (nf < 2 || nf > min(max_free, kNwMax)) return 0;
   if (prof && threadIdx.x == 0) prof[0] = wall_clock64();
   // 2. A = K_FF (lower) and the right-hand sides f_F, 1 (rows nf, nf + 1); the lower triangle as one flat
-  // range of nf (nf + 1) / 2 entries (row i starts at i (i + 1) / 2), 16 independent gathers per thread
+  // range of nf (nf + 1) / 2 entries (row i starts at i (i + 1) / 2), 32 independent gathers per thread
   {
-    constexpr int U = 16;
+    constexpr int U = 32;
     const int64_t ne = int64_t(nf) * (nf + 1) / 2;
     for (int64_t e0 = t; e0 < ne; e0 += U * int64_t(nt)) {
       double v[U];
@@ -470,62 +544,39 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
   __threadfence_block();
   __syncthreads();
   if (prof && threadIdx.x == 0) prof[1] = wall_clock64();
-  // 3. the factorisation, a panel of kNwPW columns at a time.  Every thread holds up to kNwRows rows of
-  // the panel in registers (rows p0 + t + nt q): it applies the earlier columns (ascending j; the panel's
-  // own rows of L staged in LDS as lp[j][c], shared by the thread's rows), wave 0 factors the panel's
-  // diagonal block in registers (a lane per row, readlane broadcasts), and every thread then solves its
-  // rows below the block against it (ascending kk, no barrier).
-  constexpr int kNwRows = (kNwMax + 2 + 255) / 256;  // rows per thread (nt = 256)
+  // 3. the factorisation, a panel of kNwPW columns at a time: every panel row takes the terms of the earlier
+  // columns (newton_rows, ascending j; the panel's own rows of L staged in LDS as lp[j][c]) into pb, wave 0
+  // factors the panel's diagonal block in registers (a lane per row, readlane broadcasts), and a thread per
+  // row then solves the rows below the block against it (ascending kk) and stores the panel to Amat.
   double* dblk = pb;  // the panel's diagonal block, kNwPW x kNwPW
+  int64_t pt0 = 0;
+  auto pstamp = [&](int k) {
+    if (prof && t == 0) {
+      const int64_t now = wall_clock64();
+      if (pt0) prof[k] += now - pt0;
+      pt0 = now;
+    }
+  };
+  if (prof && t == 0) prof[8] = prof[9] = prof[10] = prof[11] = 0;
   for (int p0 = 0; p0 < nf; p0 += kNwPW) {
     const int pw = min(kNwPW, nf - p0);
+    pstamp(11);
     for (int e = t; e < kNwPW * p0; e += nt) {  // lp[j][c] = L[p0 + c][j], j < p0
       const int j = e / kNwPW, c = e - j * kNwPW;
       lp[e] = c < pw ? Amat[int64_t(p0 + c) * ldA + j] : 0.0;
     }
     __syncthreads();
-    double sv[kNwRows][kNwPW];
-    const double* ar[kNwRows];
-    bool rv[kNwRows];
-#pragma unroll
-    for (int q = 0; q < kNwRows; ++q) {
-      const int i = p0 + t + nt * q;
-      rv[q] = i < nf + 2;
-      ar[q] = Amat + int64_t(rv[q] ? i : 0) * ldA;
-#pragma unroll
-      for (int c = 0; c < kNwPW; ++c) sv[q][c] = rv[q] && c < pw && (i >= nf || p0 + c <= i) ? ar[q][p0 + c] : 0.0;
-    }
-    const bool any = rv[0];
-    if (any) {
-      for (int j = 0; j < p0; j += 4) {  // p0 is a multiple of 16
-        double lij[kNwRows][4];
-#pragma unroll
-        for (int q = 0; q < kNwRows; ++q)
-#pragma unroll
-          for (int u = 0; u < 4; u += 2) {
-            const f64x2 v = rv[q] ? *reinterpret_cast<const f64x2*>(ar[q] + j + u) : f64x2{0.0, 0.0};
-            lij[q][u] = v[0];
-            lij[q][u + 1] = v[1];
-          }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f64x2* lr = reinterpret_cast<const f64x2*>(lp + (j + u) * kNwPW);
-#pragma unroll
-          for (int c2 = 0; c2 < kNwPW / 2; ++c2) {
-            const f64x2 l2 = lr[c2];
-#pragma unroll
-            for (int q = 0; q < kNwRows; ++q) {
-              sv[q][2 * c2] = __builtin_fma(-lij[q][u], l2[0], sv[q][2 * c2]);
-              sv[q][2 * c2 + 1] = __builtin_fma(-lij[q][u], l2[1], sv[q][2 * c2 + 1]);
-            }
-          }
-        }
-      }
-    }
-    // the diagonal block's rows (p0 .. p0 + pw - 1, held by threads 0 .. pw - 1 as q = 0) to LDS
-    if (t < pw)
-#pragma unroll
-      for (int c = 0; c < kNwPW; ++c) dblk[t * kNwPW + c] = sv[0][c];
+    // the earlier columns' terms on the panel's rows [p0, nf + 2), into pb[r][c] (r = row - p0): a thread per
+    // row below 129 rows... above 128 rows (up to 3 rows per thread), 2 threads per row (8 columns each)
+    // up to 128, 4 (4 columns each) up to 64 -- every lane busy however few rows are left
+    const int ract = nf + 2 - p0;
+    if (ract > 128)
+      newton_rows<kNwPW, (kNwMax + 2 + 255) / 256>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
+    else if (ract > 64)
+      newton_rows<kNwPW / 2, 1>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
+    else
+      newton_rows<kNwPW / 4, 1>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
+    pstamp(8);
     __syncthreads();
     if (w == 0) {  // the diagonal block in wave 0's registers: lane r = row p0 + r
       double dr[kNwPW];
@@ -554,31 +605,36 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
       if (lane == 0 && bad) s_fail = 1;
     }
     __syncthreads();
+    pstamp(9);
     if (s_fail) return 0;
-    // the rows below the block (and the two right-hand sides) against it; then every row to Amat
+    // the rows below the block (and the two right-hand sides) against it, a thread per row; then every
+    // row to Amat
+    for (int r = t; r < ract; r += nt) {
+      const int i = p0 + r;
+      double sv[kNwPW];
 #pragma unroll
-    for (int q = 0; q < kNwRows; ++q) {
-      const int i = p0 + t + nt * q;
-      if (!rv[q]) continue;
-      if (i < p0 + pw) {
-#pragma unroll
-        for (int c = 0; c < kNwPW; ++c) sv[q][c] = dblk[(i - p0) * kNwPW + c];
-      } else {
+      for (int c2 = 0; c2 < kNwPW / 2; ++c2) {
+        const f64x2 v = reinterpret_cast<const f64x2*>(pb + r * kNwPW)[c2];
+        sv[2 * c2] = v[0];
+        sv[2 * c2 + 1] = v[1];
+      }
+      if (r >= pw) {
 #pragma unroll
         for (int kk = 0; kk < kNwPW; ++kk)
           if (kk < pw) {
-            sv[q][kk] = sv[q][kk] / dblk[kk * kNwPW + kk];
+            sv[kk] = sv[kk] / dblk[kk * kNwPW + kk];
 #pragma unroll
             for (int k2 = kk + 1; k2 < kNwPW; ++k2)
-              if (k2 < pw) sv[q][k2] = __builtin_fma(-sv[q][kk], dblk[k2 * kNwPW + kk], sv[q][k2]);
+              if (k2 < pw) sv[k2] = __builtin_fma(-sv[kk], dblk[k2 * kNwPW + kk], sv[k2]);
           }
       }
 #pragma unroll
       for (int c = 0; c < kNwPW; ++c)
-        if (c < pw && (i >= nf || p0 + c <= i)) Amat[int64_t(i) * ldA + p0 + c] = sv[q][c];
+        if (c < pw && (i >= nf || p0 + c <= i)) Amat[int64_t(i) * ldA + p0 + c] = sv[c];
     }
     __threadfence_block();
     __syncthreads();
+    pstamp(10);
   }
   if (prof && threadIdx.x == 0) prof[2] = wall_clock64();
   // 4. back substitution: s1 / s2 = z (the right-hand-side rows), x = L^-T z, by blocks of 64 columns
@@ -697,19 +753,26 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
   __syncthreads();
   if (prof && threadIdx.x == 0) prof[4] = wall_clock64();
   // 8. f of every position of W: f_q += sum_k K(F_k, q) ur_k (ascending k), 16 loads per batch
-  for (int q0 = 0; q0 < m; q0 += nt) {
-    const int q = q0 + t;
-    if (q < m) {
-      double sacc = 0.0;
-      for (int k0 = 0; k0 < nf; k0 += 16) {
-        double kv[16];
+  for (int q0 = 0; q0 < m; q0 += 4 * nt) {  // four positions per thread at once: 4 x 16 loads in flight
+    double sacc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < nf; k0 += 16) {
+      double kv[4][16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) kv[u] = k0 + u < nf ? Kw[int64_t(fidx[k0 + u]) * ldw + q] : 0.0;
+      for (int v = 0; v < 4; ++v) {
+        const int q = q0 + v * nt + t;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) kv[v][u] = q < m && k0 + u < nf ? Kw[int64_t(fidx[k0 + u]) * ldw + q] : 0.0;
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-          if (k0 + u < nf) sacc = __builtin_fma(kv[u], ur[k0 + u], sacc);
-      }
-      gF[q] += sacc;
+          if (k0 + u < nf) sacc[v] = __builtin_fma(kv[v][u], ur[k0 + u], sacc[v]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = q0 + v * nt + t;
+      if (q < m) gF[q] += sacc[v];
     }
   }
   __threadfence_block();
@@ -2600,7 +2663,7 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
       return SVM_OK;
     }
   }
-  if (ld % 16 != 0 || ld < d || o.world != 1) return SVM_OK;  // the FP64 block kernel's k-steps
+  if (ld % 16 != 0 || ld < d) return SVM_OK;  // the FP64 block kernel's k-steps
   // The FP64-row solve keeps the moved columns' block K(rows, <= 1024 columns) per f update: n x 1024
   // doubles of workspace (8 GB at 1M rows).  When that does not fit 80 % of what the device has free
   // (plus the context's current workspace, which it would replace), nothing runs (*used = false) and
@@ -2608,7 +2671,8 @@ int decomp_fit_rows(DeviceCtx* ctx, const double* X_d, int64_t n, int64_t ld, in
   {
     size_t free_b = 0, total_b = 0;
     SVMD_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const double need = double(n) * double(kMaxWS) * 8.0 + double(size_t(kMaxWS) * ld * 16);
+    const double need = double(n) / double(std::max(1, o.world)) * double(kMaxWS) * 8.0 +
+                        double(size_t(kMaxWS) * ld * 16);  // this GPU's rows (distributed: ~n / world)
     if (need > 0.8 * double(free_b + ctx->ws_bytes)) return SVM_OK;
   }
   // FP64 rows: their squared norms in the context's grow-only buffer, then the solve
@@ -2642,8 +2706,8 @@ int decomp_fit_u8(DeviceCtx* ctx, const uint8_t* Xu_d, int64_t n, int64_t d, con
                   bool* used, double* prep_ms, const DecompOpts& o) {
   const auto t0 = std::chrono::steady_clock::now();
   *used = false;
-  // beyond the solver's shapes (n > 512 blocks x 4,096 points = 2,097,152 rows): nothing runs, the caller
-  // takes the pairwise solver (SVC(solver="auto"))
+  // outside the solver's shapes (n < 2 or n >= 2^31 - 1, decomp_shape): nothing runs, the caller takes
+  // the pairwise solver (SVC(solver="auto"))
   if (!decomp_shape(n, q, o.world).ok) return SVM_OK;
   QuantPlan P;
   if (!plan_quant(mn_h, mx_h, d, &P) || P.kq > 32 * 128) return SVM_OK;  // igram's LDS table bound
@@ -2939,7 +3003,7 @@ SVM_API int svmd_decomp_newton_probe(void* h, const double* Kw_h, const int32_t*
   SVMD_CHECK(hipMemcpyAsync(a_h, ad, size_t(m) * 8, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipMemcpyAsync(f_h, fd, size_t(m) * 8, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipMemcpyAsync(code, cd, 4, hipMemcpyDeviceToHost, s));
-  if (prof_h) SVMD_CHECK(hipMemcpyAsync(prof_h, pd, 8 * 8, hipMemcpyDeviceToHost, s));
+  if (prof_h) SVMD_CHECK(hipMemcpyAsync(prof_h, pd, 16 * 8, hipMemcpyDeviceToHost, s));
   SVMD_CHECK(hipStreamSynchronize(s));
   if (ms_out) *ms_out = double(tot) / reps;
   return ctx->end();

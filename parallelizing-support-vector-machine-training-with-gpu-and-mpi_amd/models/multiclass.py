@@ -41,45 +41,58 @@ from ..utils.trace import trace_range
 
 
 _POOL_LOCK = threading.Lock()
-_POOLS: dict = {}
+_POOL: list = [None, 0]  # the one persistent pool of the decomposition class solves, and its width
 _TLS = threading.local()
 
 
+def _release_pool(pool: ThreadPoolExecutor, workers: int, timeout_s: float) -> bool:
+    """Every thread of `pool` hands back its device slabs (one task per thread, all held at a barrier so
+    that no thread takes two); False when the barrier timed out (a fit was using the pool)."""
+    from ..ops import device as D
+
+    barrier = threading.Barrier(workers)
+
+    def release(_):
+        try:
+            barrier.wait(timeout_s)
+        except threading.BrokenBarrierError:
+            return False
+        D.release_gram_buffers()
+        return True
+
+    return all(list(pool.map(release, range(workers))))
+
+
 def _pool(workers: int) -> ThreadPoolExecutor:
-    """A persistent pool per width for the decomposition class solves: its threads keep their device
-    contexts (DeviceContext is per thread) and streams from one fit to the next; never shut down under
-    a caller (thread ranks of one process may map onto the same pool at once)."""
+    """The persistent pool for the decomposition class solves: its threads keep their device contexts
+    (DeviceContext is per thread), streams and column-cache slabs from one fit to the next.  ONE pool at a
+    time: a fit with another width first has the old pool's threads hand back their slabs and
+    shuts it down, so the slabs never pile up across widths and the threads stay bounded.  (If the old pool
+    is busy -- a concurrent fit of thread ranks -- it is left to finish and dropped; its threads exit with it.)"""
     workers = max(1, int(workers))
     with _POOL_LOCK:
-        if workers not in _POOLS:
-            _POOLS[workers] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix=f"svm355-ovr{workers}")
-        return _POOLS[workers]
+        pool, width = _POOL
+        if pool is not None and width == workers:
+            return pool
+        if pool is not None:
+            if _release_pool(pool, width, 2.0):
+                pool.shutdown(wait=False)
+        _POOL[0] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix=f"svm355-ovr{workers}")
+        _POOL[1] = workers
+        return _POOL[0]
 
 
 def release_solver_caches(timeout_s: float = 5.0) -> bool:
     """Hand back the device memory the one-vs-rest decomposition solves keep between fits -- each pool
-    thread's column-cache slab (large n; at most half the HBM over a pool), invisible to PyTorch's
-    allocator -- on every thread of every pool (``ops.device.release_gram_buffers`` acts on the calling
-    thread only): one task per thread, all held at a barrier so that no thread takes two.  Call it with no
-    fit running; False when a pool's barrier timed out (a fit was using it) and its slabs were kept."""
-    from ..ops import device as D
-
+    thread's column-cache slab (large n; at most half the HBM over the pool), invisible to PyTorch's
+    allocator -- on every thread of the pool (``ops.device.release_gram_buffers`` acts on the calling
+    thread only).  Call it with no fit running; False when the pool's barrier timed out (a fit was using
+    it) and its slabs were kept.  ``ops.device.device_empty`` calls it before retrying an allocation."""
     with _POOL_LOCK:
-        pools = dict(_POOLS)
-    ok = True
-    for workers, pool in pools.items():
-        barrier = threading.Barrier(workers)
-
-        def release(_, barrier=barrier):
-            try:
-                barrier.wait(timeout_s)
-            except threading.BrokenBarrierError:
-                return False
-            D.release_gram_buffers()
+        pool, width = _POOL
+        if pool is None:
             return True
-
-        ok = all(list(pool.map(release, range(workers)))) and ok
-    return ok
+        return _release_pool(pool, width, timeout_s)
 
 
 def _thread_stream(device):

@@ -110,13 +110,18 @@ def available() -> bool:
 def device_empty(shape, dtype, device) -> torch.Tensor:
     """``torch.empty`` for the library's large device buffers.  On an out-of-memory error the memory the
     library itself holds outside PyTorch's allocator -- the Gram and the row-cache / column-cache slab
-    its contexts keep between fits, and the grow-only Gram buffers (``release_gram_buffers``) -- is
-    handed back and the allocation retried once: a cache kept for speed never makes a later allocation
-    fail."""
+    its contexts keep between fits, the grow-only Gram buffers (``release_gram_buffers``), and the
+    one-vs-rest pool threads' column-cache slabs (``models.multiclass.release_solver_caches``) -- is handed
+    back and the allocation retried once: a cache kept for speed never makes a later allocation fail
+    (ADVICE r4, r5).""" 
     try:
         return torch.empty(shape, dtype=dtype, device=device)
     except torch.OutOfMemoryError:
         release_gram_buffers()
+        # and the one-vs-rest pool threads' column-cache slabs (their contexts are not this thread's)
+        from ..models.multiclass import release_solver_caches
+
+        release_solver_caches(timeout_s=1.0)
         torch.cuda.empty_cache()
         return torch.empty(shape, dtype=dtype, device=device)
 
@@ -492,7 +497,7 @@ def decomp_newton_probe(Kw: np.ndarray, y: np.ndarray, a: np.ndarray, f: np.ndar
     y = np.ascontiguousarray(y, dtype=np.int32)
     a = np.array(a, dtype=np.float64)
     f = np.array(f, dtype=np.float64)
-    prof = np.zeros(8, dtype=np.int64)
+    prof = np.zeros(16, dtype=np.int64)
     code, ms = ctypes.c_int32(0), ctypes.c_double(0.0)
     ctx = _ctx_for(torch.empty(1, device=device))
     N.check(ctx.lib.svmd_decomp_newton_probe(ctx.bind(), N.ptr(Kw), N.ptr(y), len(y), N.ptr(a), N.ptr(f), float(C),

@@ -6,7 +6,9 @@ kinds of work: choosing the working set (top violators per block of points), sol
 workgroup, latency-bound), and updating f for all n points (an int8-MFMA GEMV over the points whose
 alpha moved).  The first and last scale with n; the middle does not.  Here every GPU:
 
-- holds all n rows (uint8, quantised on its own device), the labels and a replica of alpha;
+- holds all n rows (uint8 pixels quantised on its own device: exact-integer kernel values; or FP64
+  rows min-max scaled on it: FP64-MFMA kernel values for real-valued data), the labels and a replica of
+  alpha;
 - owns a contiguous range of the selection's blocks and keeps f for those points only;
 - selects its blocks' candidates, and ONE all-gather per outer iteration (RCCL ``ncclAllGather``
   over xGMI, 16-byte records: id and f) gives every GPU the same candidate list;
@@ -39,10 +41,25 @@ from ..utils.config import SVMParams
 from ..utils.trace import trace_range
 
 
-def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: int, world: int) -> dict:
-    from ..utils.data import check_labels, pixel_rows
+def _rows(X) -> tuple:
+    """(rows, is_u8): integer pixel rows as uint8 (the exact-integer path, 8x less host-to-device traffic),
+    anything else as C-contiguous FP64 (min-max scaled on the GPUs; real-valued data train with FP64-MFMA
+    kernel values, mpi_svm_main2.cpp:316-402 / mpi_svm_main3.cpp:433-518 partition double rows)."""
+    from ..utils.data import check_finite_bounds, compact_pixels
 
-    X = pixel_rows(X, "the distributed decomposition solver")
+    Xc = compact_pixels(X)
+    if Xc is not None and Xc.ndim == 2:
+        return np.ascontiguousarray(Xc), True
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    if X.ndim != 2:
+        raise ValueError("X must be (n, d)")
+    check_finite_bounds(X.min(0), X.max(0))
+    return X, False
+
+
+def _fit_native(fn, handle, X: np.ndarray, y: np.ndarray, params: SVMParams, q: int, world: int) -> dict:
+    from ..utils.data import check_labels
+
     n, d = X.shape
     y = check_labels(y, n)
     alpha = np.empty(n, dtype=np.float64)
@@ -98,7 +115,9 @@ def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] =
     """One distributed decomposition solve over a ``DeviceGroup`` (its ranks are this process's
     threads; RCCL or the loopback rehearsal)."""
     lib = N.hip()
-    out = _fit_native(lib.svmd_cascade_group_decomp, group.handle, X, y, params or SVMParams(), q, group.world)
+    X, u8 = _rows(X)
+    fn = lib.svmd_cascade_group_decomp if u8 else lib.svmd_cascade_group_decomp_rows
+    out = _fit_native(fn, group.handle, X, y, params or SVMParams(), q, group.world)
     waits = np.zeros(group.world)
     if int(lib.svmd_cascade_group_decomp_waits(group.handle, N.ptr(waits), waits.size)) == group.world:
         out["host_wait_ms"] = [round(float(v), 3) for v in waits]
@@ -114,7 +133,9 @@ def group_fit(group, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] =
 def rank_fit(rank, X: np.ndarray, y: np.ndarray, params: Optional[SVMParams] = None, q: int = 1024) -> dict:
     """This process's rank of a distributed decomposition solve (every rank passes all rows)."""
     lib = N.hip()
-    out = _fit_native(lib.svmd_cascade_rank_decomp, rank.handle, X, y, params or SVMParams(), q, 1)
+    X, u8 = _rows(X)
+    fn = lib.svmd_cascade_rank_decomp if u8 else lib.svmd_cascade_rank_decomp_rows
+    out = _fit_native(fn, rank.handle, X, y, params or SVMParams(), q, 1)
     out["host_wait_ms"] = [round(float(lib.svmd_cascade_rank_decomp_wait(rank.handle)), 3)]
     return out
 
@@ -166,7 +187,7 @@ class DistributedDecompSVC:
                 m.support_vectors_ = out["rows"][sup]
             elif X.dtype == np.uint8:
                 m._device_model_from_u8(X[sup], dev)
-            else:  # pixel values held as FP64 (validated integers): widened on the host
+            else:  # FP64 rows (real-valued, or pixel values as doubles): scaled on the host
                 m.support_vectors_ = m.scaler_.transform(X[sup])
                 m._upload_model(dev)
         self.model_ = m

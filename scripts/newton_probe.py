@@ -30,4 +30,6 @@ for m, nf in [(700, 339), (1024, 500), (400, 100)]:
     ph = np.diff(np.r_[prof[7], prof[:6]]) / 100.0  # 100 MHz ticks -> us
     print(f"m={m} nf={int(prof[6])}: code {cd} (ref {cr})  alpha bit-identical {np.array_equal(ad, ar)}  "
           f"f bit-identical {np.array_equal(fd, fr)}  {ms * 1e3:.1f} us/step  phases us: free {ph[0]:.1f} "
-          f"K_FF {ph[1]:.1f} chol {ph[2]:.1f} backsub {ph[3]:.1f} step {ph[4]:.1f} f {ph[5]:.1f}", flush=True)
+          f"K_FF {ph[1]:.1f} chol {ph[2]:.1f} (row updates {prof[8] / 100:.1f} block {prof[9] / 100:.1f} "
+          f"solve+store {prof[10] / 100:.1f} staging {prof[11] / 100:.1f}) backsub {ph[3]:.1f} step {ph[4]:.1f} "
+          f"f {ph[5]:.1f}", flush=True)

@@ -165,6 +165,25 @@ def test_checkpoint_of_other_training_set_is_rejected(tmp_path, data):
         CascadeSVM(P2, topology="star", checkpoint_dir=str(tmp_path), resume=True).fit(X2, tr.y, world=2)
 
 
+def test_checkpoint_of_other_labels_or_rows_with_the_same_bounds_is_rejected(tmp_path, data):
+    """the fingerprint also covers every rank's rows, labels and ids -- a resume of another
+    one-vs-rest class on the same rows (other labels), or on other rows whose columns span the same
+    ranges, is refused; the same data still resumes."""
+    tr, _ = data
+    ck = str(tmp_path)
+    CascadeSVM(P2, topology="star", max_rounds=1, checkpoint_dir=ck).fit(tr.X, tr.y, world=2)
+    y2 = tr.y.copy()
+    y2[:5] = -y2[:5]  # another positive class on the same rows
+    with pytest.raises(NativeError, match="another training set"):
+        CascadeSVM(P2, topology="star", checkpoint_dir=ck, resume=True).fit(tr.X, y2, world=2)
+    X3 = tr.X.copy()
+    X3[[3, 4]] = X3[[4, 3]]  # two rows swapped: the same column bounds, other rows
+    with pytest.raises(NativeError, match="another training set"):
+        CascadeSVM(P2, topology="star", checkpoint_dir=ck, resume=True).fit(X3, tr.y, world=2)
+    res = CascadeSVM(P2, topology="star", checkpoint_dir=ck, resume=True).fit(tr.X, tr.y, world=2).result
+    assert res.converged
+
+
 @pytest.mark.parametrize("world,fail_rank,fail_round", [(2, 1, 1), (3, 0, 0), (4, 2, 1)])
 def test_failing_rank_ends_every_rank(data, world, fail_rank, fail_round):
     """One rank throws mid-run: the others leave their exchanges and the call reports that rank."""

@@ -119,6 +119,22 @@ def test_torchrun_processes_share_one_gpu_over_hostcomm(nproc, rows):
             assert abs(c["b_minus_headline_b"]) <= 10 * 1e-5
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_torchrun_hostcomm_on_real_valued_rows(nproc):
+    """bench.py --parallel decomp --input f64-real -- the per-process ranks on FP64
+    real-valued rows (FP64-MFMA kernel values), exchanging over gloo on the one GPU: the model equals the
+    one-GPU FP64 decomposition bit for bit."""
+    p, wall = _torchrun(nproc, "--parallel", "decomp", "--transport", "hostcomm", "--input", "f64-real", "--rows",
+                        "6000", "--test-rows", "500", "--steps", "1", "--warmup", "1", "--baseline-1gpu", "1",
+                        "--cascade-steps", "0")
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["config"]["parallelism"] == f"distributed-decomp-dp{nproc}-gloo"
+    assert out["host_rows"] == "fp64 (real-valued)" and out["stop_reason"] == "converged"
+    assert out["bit_identical_to_1gpu"] is True and out["n_sv"] > 0
+
+
 def test_torchrun_world_not_dividing_8_converges_to_the_same_model():
     """Three processes (a world that does not divide the 8-block grain): the selection's blocks are then
     a multiple of 8 x world, another trajectory to the same optimum -- the preflight checks convergence,

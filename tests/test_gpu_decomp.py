@@ -194,6 +194,49 @@ def test_distributed_rehearsal_equals_one_gpu(n, world, ccache, monkeypatch):
     np.testing.assert_array_equal(m.predict(te.X), one.predict(te.X))
 
 
+def _real_problem(n, d, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    w = rng.standard_normal(d)
+    y = np.where(X @ w + 0.3 * rng.standard_normal(n) > np.median(X @ w), 1, -1).astype(np.int32)
+    return X, y
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_distributed_rehearsal_on_real_valued_rows_equals_one_gpu(world):
+    """the distributed decomposition on FP64 real-valued rows (no exact-integer plan:
+    every kernel value on FP64 MFMA, each rank's f update over its own rows) -- P thread ranks rehearsed on
+    the one GPU give alpha, b and the iteration counts of the one-GPU FP64 decomposition bit for bit, and
+    the reference's stop test holds against a numpy RBF (the reference's MPI programs partition double
+    rows: mpi_svm_main2.cpp:316-402)."""
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.rccl import DeviceGroup
+
+    X, y = _real_problem(6000, 50, 7)
+    gamma, C = 0.05, 2.0
+    one = SVC(device="cuda:0", solver="decomp", gamma=gamma, C=C).fit(X, y)
+    assert one.timings_["gram_path"] == "fp64"
+    g = DeviceGroup(world, "loopback")
+    try:
+        m = DistributedDecompSVC(world, group=g, gamma=gamma, C=C).fit(X, y)
+    finally:
+        g.close()
+    assert m.stop_reason_ == "converged"
+    assert m.n_iter_ == one.n_iter_ and m.b_ == one.b_
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
+    Xs = (X - X.min(0)) / np.where(X.max(0) - X.min(0) < 1e-12, 1.0, X.max(0) - X.min(0))
+    sq = np.einsum("ij,ij->i", Xs, Xs)
+    K = np.exp(-gamma * np.maximum(sq[:, None] + sq[None, :] - 2.0 * Xs @ Xs.T, 0.0))
+    np.fill_diagonal(K, 1.0)
+    a, yf, p = m.alpha_, y.astype(np.float64), m.params
+    f = K @ (a * yf) - yf
+    hi = ((yf == 1) & (a < C - p.eps)) | ((yf == -1) & (a > p.eps))
+    lo = ((yf == 1) & (a > p.eps)) | ((yf == -1) & (a < C - p.eps))
+    assert f[lo].max() - f[hi].min() <= 2 * p.tau + 1e-8
+    te, _ = _real_problem(500, 50, 8)
+    np.testing.assert_array_equal(m.predict(te), one.predict(te))
+
+
 def test_distributed_process_rank_world1_equals_one_gpu():
     """The per-process entry (torchrun form, RCCL communicator of one rank) on the one GPU."""
     from svm355.parallel.decomp import DistributedDecompSVC

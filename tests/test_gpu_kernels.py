@@ -764,7 +764,8 @@ def test_ovr_keeps_column_caches_across_classes_and_releases_them(dev, monkeypat
     import ctypes
 
     from svm355 import OneVsRestSVC
-    from svm355.models.multiclass import _POOLS, release_solver_caches
+    from svm355.models import multiclass as MC
+    from svm355.models.multiclass import release_solver_caches
 
     tr = synthetic_mnist(6000, seed=38).compact()
     ref = OneVsRestSVC(device="cuda:0", concurrent_solves=2).fit(tr.X, tr.labels)
@@ -788,9 +789,17 @@ def test_ovr_keeps_column_caches_across_classes_and_releases_them(dev, monkeypat
         b = threading.Barrier(workers)
         return list(pool.map(lambda i: (b.wait(10), slab(i))[1], range(workers)))
 
-    assert sum(per_thread(_POOLS[2], 2)) > 0  # kept for the next fit
+    pool2 = MC._POOL[0]
+    assert MC._POOL[1] == 2 and sum(per_thread(pool2, 2)) > 0  # kept for the next fit
     assert release_solver_caches()
-    assert sum(per_thread(_POOLS[2], 2)) == 0
+    assert sum(per_thread(pool2, 2)) == 0
+    # another width: the 2-thread pool hands its slabs back and is replaced (no pile-up across widths)
+    OneVsRestSVC(device="cuda:0", concurrent_solves=2).fit(tr.X, tr.labels)
+    assert sum(per_thread(pool2, 2)) > 0
+    m3 = OneVsRestSVC(device="cuda:0", concurrent_solves=3).fit(tr.X, tr.labels)
+    np.testing.assert_array_equal(m3.dual_coef_, ref.dual_coef_)
+    assert MC._POOL[1] == 3 and MC._POOL[0] is not pool2 and pool2._shutdown
+    assert sum(per_thread(MC._POOL[0], 3)) > 0 and release_solver_caches()
 
 
 def test_ovr_device_model_save_load(dev, tmp_path):

@@ -111,3 +111,41 @@ def test_ovr_class_absent_from_the_labels_is_never_predicted():
     assert m.stop_reasons_[3] == "no_candidate" and m.intercepts_b_[3] == 1.0
     assert np.all(m.decision_function(tr.X)[:, 3] == -1.0)
     assert 7 not in set(m.predict(tr.X).tolist())
+
+
+def test_device_empty_releases_the_ovr_pool_slabs_on_oom(monkeypatch):
+    """an out-of-memory allocation hands back the library's own device memory -- including the
+    one-vs-rest pool threads' column-cache slabs, which the calling thread's release cannot reach --
+    before its one retry."""
+    import torch
+
+    from svm355.models import multiclass as MC
+    from svm355.ops import device as D
+
+    calls = []
+    real_empty = torch.empty
+
+    def empty(*a, **k):
+        if not calls:
+            calls.append("oom")
+            raise torch.OutOfMemoryError("injected")
+        return real_empty(*a, **{kk: v for kk, v in k.items() if kk != "device"})
+
+    monkeypatch.setattr(torch, "empty", empty)
+    monkeypatch.setattr(D, "release_gram_buffers", lambda: calls.append("gram"))
+    monkeypatch.setattr(MC, "release_solver_caches", lambda timeout_s=5.0: calls.append("ovr") or True)
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: calls.append("empty_cache"))
+    out = D.device_empty((4, 4), torch.float64, "cpu")
+    assert out.shape == (4, 4) and calls == ["oom", "gram", "ovr", "empty_cache"]
+
+
+def test_ovr_pool_is_replaced_not_piled_up():
+    """One persistent class-solve pool at a time: a fit of another width replaces it (its threads first
+    hand back their slabs), so threads and slabs stay bounded over a process's life."""
+    from svm355.models import multiclass as MC
+
+    p2 = MC._pool(2)
+    assert MC._pool(2) is p2 and MC._POOL[1] == 2
+    p3 = MC._pool(3)
+    assert p3 is not p2 and MC._POOL[1] == 3 and p2._shutdown
+    assert MC.release_solver_caches()
