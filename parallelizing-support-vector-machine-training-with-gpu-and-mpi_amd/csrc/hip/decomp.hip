@@ -43,6 +43,7 @@ namespace svm355 {
 namespace {
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 struct DecompHost {  // pinned: the PROF build's phase totals (the loop state is DecompCtl, on the device)
   int64_t prof[12];  // clock64 ticks per phase summed over iterations; [6] kernel clock64, [7] wall ticks;
@@ -402,76 +403,66 @@ constexpr int kNwPW = 16;      // panel width
 constexpr int kNwMax = 512;    // |F| bound of the LDS buffers (NewtonCfg::max_free is clamped to it)
 // The factorisation's row updates for one panel (newton_wg): pb[r][c] = A[p0 + r][p0 + c] - sum_{j < p0}
 // L[p0 + r][j] L[p0 + c][j] (ascending j) for the panel's rows r < ract and columns c < pw (lower entries;
-// the right-hand-side rows nf, nf + 1 take every column), lp[j][c] = L[p0 + c][j].  CPT columns per
-// thread (kNwPW / CPT threads per row), up to NQ rows per thread.
-template <int CPT, int NQ>
-__device__ __forceinline__ void newton_rows(const double* __restrict__ Amat, int64_t ldA, const double* __restrict__ lp,
-                                            double* __restrict__ pb, int p0, int pw, int nf, int ract, int t, int nt) {
-  constexpr int G = kNwPW / CPT;  // threads per row
-  double sv[NQ][CPT];
-  const double* ar[NQ];
-  bool rv[NQ];
-  int rr[NQ], cg[NQ];
+// the right-hand-side rows nf, nf + 1 take every column), lp[j][c] = L[p0 + c][j] -- on FP64 MFMA
+// (v_mfma_f64_16x16x4f64): a wave per 16-row tile of the panel rows,
+// 16 columns, k-steps of 4 columns j..j+3.  The instruction sums its four products into the accumulator
+// as four fused multiply-adds in k order -- measured bit for bit against the chain c = fma(a0, b0, c);
+// ... fma(a3, b3, c) on 512,000 random entries (bench_kernels/mfma_f64_order.hip) -- so with A = -L (exact)
+// every entry takes exactly newton_step_ref's ascending fma chain.  Lane l: A = -L[p0 + row0 + (l & 15)]
+// [j + (l >> 4)], B = L[p0 + (l & 15)][j + (l >> 4)] (lp[j][c]); D: col = l & 15, row = (l >> 4) + 4 r.
+__device__ __forceinline__ void newton_rows_mfma(const double* __restrict__ Amat, int64_t ldA,
+                                                 const double* __restrict__ lp, double* __restrict__ pb, int p0, int pw,
+                                                 int nf, int ract, int lane, int w, int nw) {
+  const int col = lane & 15, g = lane >> 4;
+  const int ntile = (ract + 15) / 16;
+  for (int tile = w; tile < ntile; tile += nw) {
+    const int r0 = tile * 16;
+    const int ar = r0 + col;                 // the A operand's row (panel-local)
+    const bool arv = ar < ract;
+    const double* arow = Amat + int64_t(p0 + (arv ? ar : 0)) * ldA;
+    f64x4 acc;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int item = t + nt * q;
-    rr[q] = item / G;
-    cg[q] = (item - rr[q] * G) * CPT;  // the thread's first column
-    rv[q] = rr[q] < ract;
-    const int i = p0 + rr[q];
-    ar[q] = Amat + int64_t(rv[q] ? i : 0) * ldA;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int cc = cg[q] + c;
-      sv[q][c] = rv[q] && cc < pw && (i >= nf || p0 + cc <= i) ? ar[q][p0 + cc] : 0.0;
+    for (int r = 0; r < 4; ++r) {
+      const int rr = r0 + g + 4 * r, i = p0 + rr;
+      acc[r] = rr < ract && col < pw && (i >= nf || p0 + col <= i) ? Amat[int64_t(i) * ldA + p0 + col] : 0.0;
     }
-  }
-  int nq = 0;  // rows this thread has (uniform upper bound per wave is not needed: masked by rv)
+    // A operands 16 k-steps (64 columns) at a time, the next 16 loaded while these run: one wave per SIMD,
+    // so only loads in flight hide their latency; k-steps at or beyond p0 are skipped (uniform), never
+    // run with zero operands (an added 0 could flip the sign of a zero)
+    // (the loads are unconditional -- columns up to p0 + 127 < kMaxWS stay inside Amat's row, and what
+    // lies beyond p0 is never used -- so all 16 are in flight together; a branch around each would make
+    // the compiler wait for every load before the next)
+    double nx[16];
+    auto load16 = [&](int j) {
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) nq += rv[q] ? 1 : 0;
-  if (nq > 0) {
-    // the row entries 8 at a time, the next 8 loaded while these are used (one wave per SIMD: nothing
-    // else hides the loads' latency)
-    double nxt[NQ][8];
-    auto load8 = [&](int j, double (&dst)[NQ][8]) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-          const f64x2 v = q < nq && j < p0 ? *reinterpret_cast<const f64x2*>(ar[q] + j + u) : f64x2{0.0, 0.0};
-          dst[q][u] = v[0];
-          dst[q][u + 1] = v[1];
-        }
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const double v = arow[j + 4 * s2 + g];
+        nx[s2] = arv ? -v : 0.0;
+      }
     };
-    load8(0, nxt);
-    for (int j = 0; j < p0; j += 8) {  // p0 is a multiple of 16
-      double lij[NQ][8];
+    load16(0);
+    for (int j = 0; j < p0; j += 64) {
+      double av[16];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
+      for (int s2 = 0; s2 < 16; ++s2) av[s2] = nx[s2];
+      load16(j + 64);
+      if (j + 64 <= p0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) lij[q][u] = nxt[q][u];
-      load8(j + 8, nxt);
+        for (int s2 = 0; s2 < 16; ++s2)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], lp[(j + 4 * s2 + g) * kNwPW + col], acc, 0, 0, 0);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const f64x2* lr = reinterpret_cast<const f64x2*>(lp + (j + u) * kNwPW + cg[0]);
-#pragma unroll
-        for (int c2 = 0; c2 < CPT / 2; ++c2) {
-          const f64x2 l2 = lr[c2];
-#pragma unroll
-          for (int q = 0; q < NQ; ++q)
-            if (q < nq) {
-              sv[q][2 * c2] = __builtin_fma(-lij[q][u], l2[0], sv[q][2 * c2]);
-              sv[q][2 * c2 + 1] = __builtin_fma(-lij[q][u], l2[1], sv[q][2 * c2 + 1]);
-            }
-        }
+        for (int s2 = 0; s2 < 16; ++s2)
+          if (j + 4 * s2 < p0)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], lp[(j + 4 * s2 + g) * kNwPW + col], acc, 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = r0 + g + 4 * r;
+      if (rr < ract) pb[rr * kNwPW + col] = acc[r];
+    }
   }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-    if (rv[q])
-#pragma unroll
-      for (int c = 0; c < CPT; ++c) pb[rr[q] * kNwPW + cg[q] + c] = sv[q][c];
 }
 
 __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, int64_t ldw, const int8_t* __restrict__ sy,
@@ -520,16 +511,12 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
       int64_t dst[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t e = e0 + int64_t(u) * nt;
-        dst[u] = -1;
-        v[u] = 0.0;
-        if (e < ne) {
-          int i = int((__builtin_sqrt(8.0 * double(e) + 1.0) - 1.0) * 0.5);
-          i = int64_t(i) * (i + 1) / 2 > e ? i - 1 : int64_t(i + 1) * (i + 2) / 2 <= e ? i + 1 : i;
-          const int k = int(e - int64_t(i) * (i + 1) / 2);
-          v[u] = Kw[int64_t(fidx[i]) * ldw + fidx[k]];
-          dst[u] = int64_t(i) * ldA + k;
-        }
+        const int64_t e1 = e0 + int64_t(u) * nt, e = min(e1, ne - 1);  // clamped: the gathers are unconditional
+        int i = int((__builtin_sqrt(8.0 * double(e) + 1.0) - 1.0) * 0.5);
+        i = int64_t(i) * (i + 1) / 2 > e ? i - 1 : int64_t(i + 1) * (i + 2) / 2 <= e ? i + 1 : i;
+        const int k = int(e - int64_t(i) * (i + 1) / 2);
+        v[u] = Kw[int64_t(fidx[i]) * ldw + fidx[k]];
+        dst[u] = e1 < ne ? int64_t(i) * ldA + k : -1;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -570,12 +557,7 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
     // row below 129 rows... above 128 rows (up to 3 rows per thread), 2 threads per row (8 columns each)
     // up to 128, 4 (4 columns each) up to 64 -- every lane busy however few rows are left
     const int ract = nf + 2 - p0;
-    if (ract > 128)
-      newton_rows<kNwPW, (kNwMax + 2 + 255) / 256>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
-    else if (ract > 64)
-      newton_rows<kNwPW / 2, 1>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
-    else
-      newton_rows<kNwPW / 4, 1>(Amat, ldA, lp, pb, p0, pw, nf, ract, t, nt);
+    newton_rows_mfma(Amat, ldA, lp, pb, p0, pw, nf, ract, lane, w, nw);
     pstamp(8);
     __syncthreads();
     if (w == 0) {  // the diagonal block in wave 0's registers: lane r = row p0 + r
@@ -682,7 +664,7 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
       for (int j0 = je - 1; j0 >= jb; j0 -= 32) {
         double l[32];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) l[u] = j0 - u >= jb ? Amat[int64_t(j0 - u) * ldA + i] : 0.0;
+        for (int u = 0; u < 32; ++u) l[u] = Amat[int64_t(max(j0 - u, jb)) * ldA + i];  // unconditional: all in flight
 #pragma unroll
         for (int u = 0; u < 32; ++u)
           if (j0 - u >= jb) {
@@ -759,9 +741,9 @@ __device__ __forceinline__ int newton_wg(int m, const double* __restrict__ Kw, i
       double kv[4][16];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int q = q0 + v * nt + t;
+        const int q = min(q0 + v * nt + t, m - 1);  // clamped: the loads are unconditional, all in flight
 #pragma unroll
-        for (int u = 0; u < 16; ++u) kv[v][u] = q < m && k0 + u < nf ? Kw[int64_t(fidx[k0 + u]) * ldw + q] : 0.0;
+        for (int u = 0; u < 16; ++u) kv[v][u] = Kw[int64_t(fidx[min(k0 + u, nf - 1)]) * ldw + q];
       }
 #pragma unroll
       for (int v = 0; v < 4; ++v)
@@ -2009,6 +1991,15 @@ int run_decomp(DeviceCtx* ctx, const DecompRows& R, const int32_t* y, double* al
     // ~8,000 slots of 8 MB for ~6,100 distinct columns a fit moves, so no fit of n <= 1M loses a hit.
     // (a context's own share when several solve side by side, svmd_set_ccache_frac; the env var overrides)
     double frac = ctx->ccache_frac >= 0.0 ? ctx->ccache_frac : 0.25;
+    // processes sharing this GPU (torchrun ranks over host-staged gloo on one device; alloc_mu orders the
+    // sizing within a process only): each takes its share of the quarter
+    if (ctx->ccache_frac < 0.0)
+      if (const char* lw = getenv("LOCAL_WORLD_SIZE")) {
+        int ndev = 1;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) ndev = 1;
+        const int sharing = (std::max(1, atoi(lw)) + ndev - 1) / ndev;
+        frac /= double(sharing);
+      }
     if (const char* v = getenv("SVM355_DECOMP_CCACHE_FRAC")) frac = std::min(0.9, std::max(0.0, atof(v)));
     cap = std::min<int64_t>(cap, int64_t(double(total_b) * frac / double(slot_b)) - kMaxWS);
     int64_t min_cap = 256;

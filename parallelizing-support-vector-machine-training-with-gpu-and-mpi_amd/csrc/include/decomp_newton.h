@@ -44,7 +44,7 @@
 namespace svm355 {
 
 struct NewtonCfg {
-  bool on = true;
+  bool on = false;         // opt-in (SVM355_DECOMP_NEWTON=1): a net loss on the headline, see below
   double frac = 0.5;       // a step at the start of the inner solve when the last one needed >= frac x m
   int32_t every = 50;      // a step after `every` chain iterations with no point changing its bound status
   int32_t per_solve = 8;   // at most this many triggers per inner solve
@@ -52,7 +52,10 @@ struct NewtonCfg {
   int32_t max_free = 640;  // |F| above this: no step (the factorisation costs |F|^3 / 6 FMAs)
 };
 
-// SVM355_DECOMP_NEWTON=0 turns the step off; SVM355_DECOMP_NEWTON_{FRAC,EVERY,PER_SOLVE,REPEAT,MAX} tune
+// Off by default.  The device step (newton_wg) costs ~0.67 ms at |F| = 302 (probe; ~0.77 ms in situ) against
+// ~0.74 us per pair update it saves: on the 60k headline 16 steps take the pair updates from 9,760 to 4,532
+// and the fit from 21.4 to 29.9 ms (profiles/newton.md) -- it pays only below ~0.2 ms per step.
+// SVM355_DECOMP_NEWTON=1 turns the step on; SVM355_DECOMP_NEWTON_{FRAC,EVERY,PER_SOLVE,REPEAT,MAX} tune
 // it (A/B runs; both sides read the same variables).
 inline NewtonCfg newton_cfg(const svm_params& p) {
   (void)p;

@@ -37,8 +37,11 @@ struct ShrinkCfg {
   }
 };
 
-// svm_params.shrink: 0 = the default (on, every 2 outer iterations from the 2nd), -1 = off, k > 0 =
-// every k outer iterations from the k-th.  SVM355_DECOMP_SHRINK (0 off, k > 0 the period),
+// svm_params.shrink: 0 = the default (off), -1 = off, k > 0 = a pass every k outer iterations from the
+// k-th.  Off by default: on the synthetic MNIST draws the gap stays wide for most of the solve, few points
+// leave the active set before the last few outer iterations, and the unshrink (f recomputed from alpha)
+// costs more than the smaller selections save -- 60k 21.2 vs 20.3 ms, 250k 98.3 vs 89.4 ms, 1M 319.8 vs
+// 307.2 ms on / off (profiles/shrinking.md).  SVM355_DECOMP_SHRINK (0 off, k > 0 the period),
 // SVM355_DECOMP_SHRINK_START and SVM355_DECOMP_SHRINK_MARGIN override it (A/B runs); both sides read the
 // same variables.  The margin: LIBSVM's rule (margin 0) drops points as soon as they leave the bounds;
 // on the synthetic MNIST draws that shrank points the solve needed again (60k: 12,566 pair updates and 2
@@ -46,7 +49,7 @@ struct ShrinkCfg {
 // with ~350 of the 60,000 points active (CPU oracle, scripts/shrink_sim.py).
 inline ShrinkCfg shrink_cfg(const svm_params& p) {
   ShrinkCfg c;
-  int32_t period = p.shrink == 0 ? 2 : p.shrink;
+  int32_t period = p.shrink > 0 ? p.shrink : -1;
   if (const char* v = std::getenv("SVM355_DECOMP_SHRINK")) period = std::atoi(v) > 0 ? std::atoi(v) : -1;
   c.on = period > 0;
   c.period = c.on ? period : 0;

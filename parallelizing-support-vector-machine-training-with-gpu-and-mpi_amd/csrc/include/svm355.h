@@ -51,7 +51,7 @@ typedef struct svm_params {
   int32_t n_threads; // CPU worker threads (1 = the serial reference baseline)
   int32_t verbose;
   int32_t wss;       // working-set selection: 0 / 1 = first order (reference), 2 = second-order j
-  int32_t shrink;    // decomposition solver shrinking: 0 = default (on), -1 = off, k > 0 = every k outer
+  int32_t shrink;    // decomposition solver shrinking: 0 = default (off), -1 = off, k > 0 = every k outer
                      // iterations (decomp_shrink.h)
 } svm_params;
 

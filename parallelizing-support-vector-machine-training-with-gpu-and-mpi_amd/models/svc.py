@@ -44,7 +44,7 @@ class SVC:
     def __init__(self, C: float = 10.0, gamma: float = 0.00125, tol: float = 1e-5, eps: float = 1e-12,
                  sv_tol: float = 1e-8, max_iter: int = 100000, device: str = "auto", n_threads: int = 0,
                  scale: bool = True, zero_is_positive: bool = False, gram: str = "auto", kcache: str = "auto",
-                 wss: str = "first", solver: str = "auto", working_set: int = 1024, shrinking=True):
+                 wss: str = "first", solver: str = "auto", working_set: int = 1024, shrinking=False):
         if wss not in ("first", "second"):
             raise ValueError("wss must be 'first' (the reference's selection) or 'second'")
         if solver not in ("auto", "smo", "decomp"):
@@ -67,7 +67,8 @@ class SVC:
         # pair per iteration over all n points, resident Gram or row cache; the CPU oracle's, the CPU
         # default).  "auto" resolves per fit by device.  shrinking (the decomposition solver, as LIBSVM's /
         # scikit-learn's option): selection and the f update on the active points only, the stop test
-        # still on all n (decomp_shrink.h); True, False, or a pass every k outer iterations.
+        # still on all n (decomp_shrink.h); True, False (the default: measured slower on the headline shapes,
+        # profiles/shrinking.md), or a pass every k outer iterations.
         self.solver = solver
         self.working_set = int(working_set)
 

@@ -46,9 +46,10 @@ class SVMParams:
     # of the second index (Fan, Chen & Lin 2005; opt-in, not the reference's trajectory)
     wss: int = 1
     # shrinking (an active set) in the working-set decomposition solver (decomp_shrink.h): True = on
-    # (every 2 outer iterations), False = off, an int k > 0 = a pass every k outer iterations.  The
-    # stop test is still the reference's, on all n points (f recomputed when the solve unshrinks).
-    shrinking: object = True
+    # (every 2 outer iterations), False = off (the default: measured slower on the headline shapes), an
+    # int k > 0 = a pass every k outer iterations.  The stop test is still the reference's, on all n
+    # points (f recomputed when the solve unshrinks).
+    shrinking: object = False
 
     def __post_init__(self):
         # the reference hard-codes these; as parameters they must keep the problem well posed:
@@ -68,7 +69,7 @@ class SVMParams:
     def _shrink_code(self) -> int:
         s = self.shrinking
         if isinstance(s, (bool, np.bool_)):
-            return 0 if s else -1
+            return 2 if s else 0
         try:
             k = int(s)
         except (TypeError, ValueError):

@@ -110,7 +110,7 @@ def test_shrinking_keeps_the_stop_test_on_all_points(prob2k, monkeypatch, mode):
     if mode == "aggressive":
         for k, v in AGGRESSIVE.items():
             monkeypatch.setenv(k, v)
-    q = p.replace(shrinking=3) if mode == "period3" else p
+    q = p.replace(shrinking=3 if mode == "period3" else True)
     a, r, st, tr = C.decomp_train_gram(K, y, q, trace_cap=400, snapshots=True)
     assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
     np.testing.assert_array_equal(np.flatnonzero(a > p.sv_tol), np.flatnonzero(ref > p.sv_tol))
@@ -148,7 +148,7 @@ def test_oracle_reports_the_real_working_set_capacity():
     assert r.stop_reason == "converged" and _gap(K, y, a, p) <= 2 * p.tau + 1e-9
 
 
-@pytest.mark.parametrize("world,shrink", [(1, "default"), (2, "default"), (4, "default"), (8, "default"),
+@pytest.mark.parametrize("world,shrink", [(1, "on"), (2, "on"), (4, "on"), (8, "on"), (2, "off"), (8, "off"),
                                           (2, "aggressive"), (8, "aggressive")])
 def test_distributed_oracle_thread_ranks_are_bit_identical(prob2k, world, shrink, monkeypatch):
     """decomp.hip's world > 1 form on the CPU oracle: every rank owns 1/world of the blocks and of f,
@@ -160,7 +160,7 @@ def test_distributed_oracle_thread_ranks_are_bit_identical(prob2k, world, shrink
         for k, v in AGGRESSIVE.items():
             monkeypatch.setenv(k, v)
     K, y = prob2k
-    p = SVMParams(n_threads=2)
+    p = SVMParams(n_threads=2, shrinking=shrink != "off")
     a, r, st, _ = C.decomp_train_gram(K, y, p)
     a2, r2, st2 = C.decomp_train_gram_dist(K, y, p, world=world)
     np.testing.assert_array_equal(a2, a)
@@ -207,18 +207,19 @@ def test_distributed_oracle_failing_rank_ends_every_rank(prob2k, monkeypatch):
         C.decomp_train_gram_dist(K, y, SVMParams(n_threads=1), world=4, comm_timeout_s=30)
 
 
-@pytest.mark.parametrize("env", [{}, {"SVM355_DECOMP_NEWTON_EVERY": "3", "SVM355_DECOMP_NEWTON_FRAC": "0"},
-                                 {"SVM355_DECOMP_NEWTON_EVERY": "10", "SVM355_DECOMP_NEWTON_REPEAT": "5",
-                                  "SVM355_DECOMP_NEWTON_MAX": "30"}])
+@pytest.mark.parametrize("env", [{"SVM355_DECOMP_NEWTON": "1"},
+                                 {"SVM355_DECOMP_NEWTON": "1", "SVM355_DECOMP_NEWTON_EVERY": "3",
+                                  "SVM355_DECOMP_NEWTON_FRAC": "0"},
+                                 {"SVM355_DECOMP_NEWTON": "1", "SVM355_DECOMP_NEWTON_EVERY": "10",
+                                  "SVM355_DECOMP_NEWTON_REPEAT": "5", "SVM355_DECOMP_NEWTON_MAX": "30"}])
 def test_newton_polish_keeps_the_stop_test_and_the_svs(prob2k, monkeypatch, env):
     """The Newton polish of the working set's free variables (decomp_newton.h): the solve still meets the
     reference's stop test on all points with the pairwise solve's support vectors, and it takes fewer
     pair updates than the polish-free solve when it fires."""
     K, y = prob2k
     p = SVMParams(n_threads=4)
-    monkeypatch.setenv("SVM355_DECOMP_NEWTON", "0")
-    a0, r0, st0, _ = C.decomp_train_gram(K, y, p)
-    monkeypatch.delenv("SVM355_DECOMP_NEWTON")
+    a0, r0, st0, _ = C.decomp_train_gram(K, y, p)  # the default: no polish
+    assert st0["newton_steps"] == 0
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     a, r, st, _ = C.decomp_train_gram(K, y, p)

@@ -244,7 +244,7 @@ AGGRESSIVE = {"SVM355_DECOMP_SHRINK": "1", "SVM355_DECOMP_SHRINK_START": "1", "S
 
 
 @pytest.mark.parametrize("mode,cache,repack", [("aggressive", "0", None), ("aggressive", "0", "1.0"),
-                                               ("aggressive", "1", "1.0"), ("default", "1", None),
+                                               ("aggressive", "1", "1.0"), ("period2", "1", None),
                                                ("aggressive", "1", "0")])
 def test_shrinking_trajectory_equals_the_oracle(monkeypatch, mode, cache, repack):
     """Shrinking (decomp_shrink.h) on the device -- the shrink passes, the packed active rows (the GEMV /
@@ -252,9 +252,8 @@ def test_shrinking_trajectory_equals_the_oracle(monkeypatch, mode, cache, repack
     repack; SVM355_DECOMP_REPACK=1.0 repacks after every drop, 0 never), the unshrink with f recomputed
     from alpha -- against the CPU oracle's trajectory bit for bit, cold and warm; f is compared on the
     active points (NaN elsewhere on both sides)."""
-    if mode == "aggressive":
-        for k, v in AGGRESSIVE.items():
-            monkeypatch.setenv(k, v)
+    for k, v in (AGGRESSIVE if mode == "aggressive" else {"SVM355_DECOMP_SHRINK": "2"}).items():
+        monkeypatch.setenv(k, v)
     monkeypatch.setenv("SVM355_DECOMP_CCACHE", cache)
     if repack is not None:
         monkeypatch.setenv("SVM355_DECOMP_REPACK", repack)
@@ -304,13 +303,13 @@ def _kkt_gap_fp64(X, y, a, p):
 
 @pytest.mark.parametrize("n", [60000])
 def test_shrunk_solve_meets_the_stop_test_on_all_points(n):
-    """The headline shape with shrinking (the default) against shrinking=False: the same support
+    """The headline shape with shrinking=True against the default (off): the same support
     vectors, b within the stop tolerance, and the reference's stop test recomputed on all n points from
     an independent FP64 kernel (not the solver's int8-exact values, and not its f)."""
     tr = synthetic_mnist(n, seed=2024).compact()
     p = SVMParams()
-    on = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
-    off = SVC(device="cuda:0", solver="decomp", shrinking=False).fit(tr.X, tr.y)
+    on = SVC(device="cuda:0", solver="decomp", shrinking=True).fit(tr.X, tr.y)
+    off = SVC(device="cuda:0", solver="decomp").fit(tr.X, tr.y)
     np.testing.assert_array_equal(on.support_, off.support_)
     assert abs(on.b_ - off.b_) <= 10 * p.tau
     assert on.timings_["shrink_passes"] >= 1 and on.timings_["min_active"] < n
@@ -319,10 +318,10 @@ def test_shrunk_solve_meets_the_stop_test_on_all_points(n):
     assert _kkt_gap_fp64(tr.X, y, on.alpha_, p) <= 2 * p.tau + 1e-9
 
 
-@pytest.mark.parametrize("env", [{"SVM355_DECOMP_NEWTON_EVERY": "5", "SVM355_DECOMP_NEWTON_FRAC": "0"},
-                                 {"SVM355_DECOMP_NEWTON_EVERY": "20", "SVM355_DECOMP_NEWTON_REPEAT": "4",
+@pytest.mark.parametrize("env", [{"SVM355_DECOMP_NEWTON": "1", "SVM355_DECOMP_NEWTON_EVERY": "5", "SVM355_DECOMP_NEWTON_FRAC": "0"},
+                                 {"SVM355_DECOMP_NEWTON": "1", "SVM355_DECOMP_NEWTON_EVERY": "20", "SVM355_DECOMP_NEWTON_REPEAT": "4",
                                   "SVM355_DECOMP_SHRINK": "1", "SVM355_DECOMP_SHRINK_START": "1"},
-                                 {"SVM355_DECOMP_NEWTON_EVERY": "10", "SVM355_DECOMP_CCACHE": "1",
+                                 {"SVM355_DECOMP_NEWTON": "1", "SVM355_DECOMP_NEWTON_EVERY": "10", "SVM355_DECOMP_CCACHE": "1",
                                   "SVM355_DECOMP_NEWTON_FRAC": "0", "SVM355_DECOMP_NEWTON_MAX": "150"}])
 def test_newton_polish_trajectory_equals_the_oracle(monkeypatch, env):
     """The Newton polish of the working set's free variables (decomp_newton.h, newton_wg in the inner

@@ -9,7 +9,7 @@ import datetime
 import numpy as np
 import pytest
 
-from svm355.parallel.decomp import _fit_native
+from svm355.parallel.decomp import _fit_native, _rows
 from svm355.parallel.dsmo import DsmoGroup, DsmoRank
 from svm355.utils.config import SVMParams
 from svm355.utils.data import check_labels, pixel_rows
@@ -48,9 +48,13 @@ def test_distributed_entry_points_reject_bad_input(bad):
         X = X.astype(np.float64) + 0.25
     else:
         X = X.astype(np.float64) + 200.0  # values above 255 would wrap in a uint8 cast
-    with pytest.raises(ValueError):
-        _fit_native(_never, None, X, y, SVMParams(), 1024, 1)
-    with pytest.raises(ValueError):
+    if bad in ("labels01", "shape"):
+        with pytest.raises(ValueError):
+            _fit_native(_never, None, X, y, SVMParams(), 1024, 1)
+    else:  # the decomposition entry points train non-pixel rows as FP64 rows -- never a uint8 cast
+        rows, u8 = _rows(X)
+        assert not u8 and rows.dtype == np.float64 and np.array_equal(rows, X)
+    with pytest.raises(ValueError):  # the pairwise solvers take pixel rows only
         DsmoGroup.fit(object.__new__(DsmoGroup), X, y)
 
 
