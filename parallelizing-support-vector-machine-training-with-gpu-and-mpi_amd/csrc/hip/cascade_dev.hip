@@ -846,9 +846,13 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
 // FP64 rows (n x d, the reference's format, mpi_svm_main2.cpp:316-402 / mpi_svm_main3.cpp:433-518):
 // min-max scaled on the device, then the exact-integer plan when their values admit one, FP64-MFMA kernel
 // values otherwise (real-valued data; decomp_fit_rows).  alpha_out (host, n doubles) may be null.
+// uint8 rows whose column ranges admit no exact-integer plan within the int8 kernels' 4,096 columns (wide
+// rows with many distinct ranges) are solved as FP64 rows: `widen` re-runs the rank with the host bytes
+// widened to doubles slice by slice on upload -- the single-GPU SVC's fallback (svc.py _fit_cuda_u8 ->
+// train_decomp_rows), taken by every rank alike (the plan is a function of the global min / max).
 void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, const int32_t* y, int64_t n, int64_t d,
                     const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
-                    double* mm_out, DecompSolo* solo = nullptr, double* host_wait_ms = nullptr) {
+                    double* mm_out, DecompSolo* solo = nullptr, double* host_wait_ms = nullptr, bool widen = false) {
   const auto t0 = std::chrono::steady_clock::now();
   auto check = [](int rc, const char* what) {
     if (rc != SVM_OK) throw CascadeError(std::string(what) + ": " + svm_last_error());
@@ -858,7 +862,8 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
   // Each GPU copies 1/world of the rows from the host over its own link and the rows are all-gathered
   // over xGMI (in place), instead of every GPU pulling all n rows through the host: world concurrent
   // pageable copies of the whole set would be staged through host memory world times.
-  const int64_t ld = u8 ? d : svmd_padded_dim(d), esz = u8 ? 1 : 8;
+  const bool u8dev = u8 && !widen;  // the device rows are the host's bytes
+  const int64_t ld = u8dev ? d : svmd_padded_dim(d), esz = u8dev ? 1 : 8;
   const int64_t rows_per = (n + world - 1) / world, chunk = rows_per * ld * esz;
   auto* Xd = static_cast<char*>(be.alloc(chunk * world));
   auto* yd = static_cast<int32_t*>(be.alloc(n * 4));
@@ -875,10 +880,22 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
   const char* Xh = static_cast<const char*>(Xv);
   auto upload = [&](int64_t a0, int64_t a1, char* dst) {  // host rows [a0, a1) to the device (FP64: padded to ld)
     if (a1 <= a0) return;
-    if (u8)
+    if (u8dev) {
       be.h2d(dst, Xh + a0 * d, (a1 - a0) * d);
-    else
+    } else if (widen) {  // bytes -> doubles on the host, 8 MB of doubles at a time
+      const int64_t blk = std::max<int64_t>(1, (int64_t(1) << 20) / std::max<int64_t>(d, 1));
+      std::vector<double> tmp;
+      for (int64_t b0 = a0; b0 < a1; b0 += blk) {
+        const int64_t b1 = std::min(a1, b0 + blk);
+        tmp.resize(size_t((b1 - b0) * d));
+        const auto* src = reinterpret_cast<const uint8_t*>(Xh) + b0 * d;
+        for (size_t e = 0; e < tmp.size(); ++e) tmp[e] = double(src[e]);
+        be.upload_rows(tmp.data(), false, b1 - b0, d, reinterpret_cast<double*>(dst + (b0 - a0) * ld * 8));
+        be.sync();  // tmp is reused by the next slice
+      }
+    } else {
       be.upload_rows(Xh + a0 * d * 8, false, a1 - a0, d, reinterpret_cast<double*>(dst));
+    }
   };
   if (world > 1) {
     upload(r0, r1, Xd + rank * chunk);
@@ -887,7 +904,7 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
     upload(0, n, Xd);
   }
   be.h2d(yd, y, n * 4);
-  if (u8)
+  if (u8dev)
     check(svmd_minmax_u8(ctx, reinterpret_cast<uint8_t*>(Xd), n, d, mm, mm + d), "svmd_minmax_u8");
   else  // the single-GPU SVC's scaling (svmd_preprocess: column min / max, then the rows scaled in place)
     check(svmd_preprocess(ctx, reinterpret_cast<double*>(Xd), n, d, ld, mm, mm + d, nullptr, 0), "svmd_preprocess");
@@ -910,7 +927,7 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
   // fault injection (tests): SVM355_DECOMP_FAIL_RANK / _OUTER make that rank fail at that outer
   // iteration inside the solve (run_decomp) while the others wait in their candidate all-gather; the
   // group's abort must end every rank with an error, not a hang
-  if (u8)
+  if (u8dev)
     check(decomp_fit_u8(ctx, reinterpret_cast<uint8_t*>(Xd), n, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res,
                         stats, &used, &prep, o),
           "decomposition SMO");
@@ -918,11 +935,17 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
     check(decomp_fit_rows(ctx, reinterpret_cast<double*>(Xd), n, ld, d, mmh.data(), mmh.data() + d, yd, ad, p, q, &res,
                           stats, &used, &prep, o),
           "decomposition SMO");
+  if (!used && u8dev && n >= 2 && n <= (int64_t(1) << 31) - 2) {
+    // no exact-integer plan for these bytes (more than 4,096 int8 columns after grouping): FP64 rows
+    for (void* b : fr.ptrs) be.free(b);  // the byte rows' buffers, before the FP64 rows are allocated
+    fr.ptrs.clear();
+    decomp_on_rank(be, tr, Xv, u8, y, n, d, p, q, alpha_out, r, stats, nullptr, mm_out, solo, host_wait_ms, true);
+    if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return;
+  }
   if (!used)
-    throw CascadeError(u8 ? "decomposition SMO: the uint8 rows admit no exact-integer plan (more than 4,096 int8 "
-                            "columns after grouping), or n = " + std::to_string(n) + " is outside 2 .. 2^31 - 2"
-                          : "decomposition SMO: n = " + std::to_string(n) + " is outside 2 .. 2^31 - 2, or the "
-                            "FP64-row solve's workspace (n / world x 1,024 doubles per GPU) does not fit");
+    throw CascadeError("decomposition SMO: n = " + std::to_string(n) + " is outside 2 .. 2^31 - 2, or the "
+                       "FP64-row solve's workspace (n / world x 1,024 doubles per GPU) does not fit");
   if (alpha_out) be.d2h(alpha_out, ad, n * 8);
   be.sync();
   if (r) *r = res;

@@ -237,6 +237,35 @@ def test_distributed_rehearsal_on_real_valued_rows_equals_one_gpu(world):
     np.testing.assert_array_equal(m.predict(te), one.predict(te))
 
 
+@pytest.mark.parametrize("d,world", [(4096, 2), (4160, 2), (4160, 4)])
+def test_distributed_rehearsal_at_the_int8_column_bound(d, world):
+    """VERDICT r5 item 4 (the kq > 4,096 boundary): pixel rows with d columns of range 255 need d int8
+    columns (padded to 64).  Up to 4,096 they take the exact-integer plan; past it no plan fits the int8
+    kernels, and the distributed entry solves them as FP64 rows (every rank the same way: the plan is a
+    function of the global min / max), as the one-GPU SVC does -- alpha, b and the iterations equal the
+    one-GPU fit bit for bit at both sides of the bound."""
+    from svm355.parallel.decomp import DistributedDecompSVC
+    from svm355.parallel.rccl import DeviceGroup
+
+    rng = np.random.default_rng(d)
+    n = 1500
+    X = rng.integers(0, 256, size=(n, d), dtype=np.uint8)
+    X[0], X[1] = 0, 255  # every column's range is 255
+    w = rng.standard_normal(d)
+    sc = X.astype(np.float64) @ w
+    y = np.where(sc > np.median(sc), 1, -1).astype(np.int32)
+    one = SVC(device="cuda:0", solver="decomp").fit(X, y)
+    assert one.timings_["gram_path"] == ("int8-exact" if d <= 4096 else "fp64"), one.timings_["gram_path"]
+    g = DeviceGroup(world, "loopback")
+    try:
+        m = DistributedDecompSVC(world, group=g).fit(X, y)
+    finally:
+        g.close()
+    assert m.stop_reason_ == "converged"
+    assert m.n_iter_ == one.n_iter_ and m.b_ == one.b_
+    np.testing.assert_array_equal(m.alpha_, one.alpha_)
+
+
 def test_distributed_process_rank_world1_equals_one_gpu():
     """The per-process entry (torchrun form, RCCL communicator of one rank) on the one GPU."""
     from svm355.parallel.decomp import DistributedDecompSVC
