@@ -3,7 +3,7 @@
 one GPU every rank has its own stream, so this splits a distributed run's device time per rank and per
 kernel (replicated kernels cost the same on every rank, divided ones ~1/P).  The ranks' streams are the
 P busiest; the per-kernel table shows each kernel's max over those streams (the critical path's share).
-Usage: rocpd_streams.py DB [--ranks P] [--top N] [--skip-first-fit]"""
+Usage: rocpd_streams.py DB [--ranks P] [--top N] [--exclude IDS]"""
 import argparse
 import collections
 import re
@@ -13,6 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("db")
 ap.add_argument("--ranks", type=int, default=0)
 ap.add_argument("--top", type=int, default=16)
+ap.add_argument("--exclude", default="", help="comma-separated stream ids to leave out (e.g. the one-GPU baseline fit's)")
 a = ap.parse_args()
 con = sqlite3.connect(a.db)
 cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
@@ -35,7 +36,8 @@ for n, s, e, st in rows:
     v[0] += 1
     v[1] += (e - s) / 1e6
 busy = {st: sum(v[1] for v in d.values()) for st, d in per.items()}
-streams = sorted(busy, key=lambda s: -busy[s])
+ex = {int(x) for x in a.exclude.split(",") if x}
+streams = sorted((s for s in busy if s not in ex), key=lambda s: -busy[s])
 if a.ranks:
     streams = streams[: a.ranks]
 print(f"{key}: " + "  ".join(f"{s}={busy[s]:.1f} ms" for s in streams))
