@@ -848,7 +848,7 @@ std::string group_exercise(Group& g, const std::string& script, double timeout_s
 // values otherwise (real-valued data; decomp_fit_rows).  alpha_out (host, n doubles) may be null.
 // uint8 rows whose column ranges admit no exact-integer plan within the int8 kernels' 4,096 columns (wide
 // rows with many distinct ranges) are solved as FP64 rows: `widen` re-runs the rank with the host bytes
-// widened to doubles slice by slice on upload -- the single-GPU SVC's fallback (svc.py _fit_cuda_u8 ->
+// widened to doubles on upload -- the single-GPU SVC's fallback (svc.py _fit_cuda_u8 ->
 // train_decomp_rows), taken by every rank alike (the plan is a function of the global min / max).
 void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, const int32_t* y, int64_t n, int64_t d,
                     const svm_params& p, int q, double* alpha_out, svm_result* r, int64_t* stats, double* ms_out,
@@ -882,17 +882,8 @@ void decomp_on_rank(HipBackend& be, Transport* tr, const void* Xv, bool u8, cons
     if (a1 <= a0) return;
     if (u8dev) {
       be.h2d(dst, Xh + a0 * d, (a1 - a0) * d);
-    } else if (widen) {  // bytes -> doubles on the host, 8 MB of doubles at a time
-      const int64_t blk = std::max<int64_t>(1, (int64_t(1) << 20) / std::max<int64_t>(d, 1));
-      std::vector<double> tmp;
-      for (int64_t b0 = a0; b0 < a1; b0 += blk) {
-        const int64_t b1 = std::min(a1, b0 + blk);
-        tmp.resize(size_t((b1 - b0) * d));
-        const auto* src = reinterpret_cast<const uint8_t*>(Xh) + b0 * d;
-        for (size_t e = 0; e < tmp.size(); ++e) tmp[e] = double(src[e]);
-        be.upload_rows(tmp.data(), false, b1 - b0, d, reinterpret_cast<double*>(dst + (b0 - a0) * ld * 8));
-        be.sync();  // tmp is reused by the next slice
-      }
+    } else if (widen) {  // the bytes widened to doubles on the device (svmd_upload_rows_u8)
+      be.upload_rows(Xh + a0 * d, true, a1 - a0, d, reinterpret_cast<double*>(dst));
     } else {
       be.upload_rows(Xh + a0 * d * 8, false, a1 - a0, d, reinterpret_cast<double*>(dst));
     }
