@@ -74,7 +74,7 @@ class SVMParams:
             k = int(s)
         except (TypeError, ValueError):
             return -2
-        return k if k > 0 and k == s else -2
+        return k if k >= 0 and k == s else -2  # 0: off, k > 0: a pass every k outer iterations
 
     def to_struct(self, verbose: int = 0):
         return params_struct(self.C, self.gamma, self.tau, self.eps, self.sv_tol, self.max_iter,
