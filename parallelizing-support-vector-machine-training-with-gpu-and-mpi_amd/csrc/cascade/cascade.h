@@ -379,7 +379,8 @@ inline int cascade_solver_for(int solver, int64_t k, int64_t warm_rows) {
 
 // cascade_state.bin layout (little-endian): char magic[8] = "SVM355C3"; int32 topology (0 star,
 // 1 tree); int32 reserved; int64 next_round; double b; int64 d; int64 k; uint64 fingerprint of the
-// training set (FNV-1a over n and the global column min / max); then k records of d + 3 doubles
+// training set (FNV-1a over n, the global column min / max and the ranks' hashes of their rows, labels
+// and global ids, when a checkpoint directory is set); then k records of d + 3 doubles
 // [scaled row (d) | y | alpha | global id] (backend independent).
 constexpr char kCheckpointMagic[9] = "SVM355C3";
 
