@@ -52,9 +52,10 @@ struct NewtonCfg {
   int32_t max_free = 640;  // |F| above this: no step (the factorisation costs |F|^3 / 6 FMAs)
 };
 
-// Off by default.  The device step (newton_wg) costs ~0.67 ms at |F| = 302 (probe; ~0.77 ms in situ) against
-// ~0.74 us per pair update it saves: on the 60k headline 16 steps take the pair updates from 9,760 to 4,532
-// and the fit from 21.4 to 29.9 ms (profiles/newton.md) -- it pays only below ~0.2 ms per step.
+// Off by default.  The device step (newton_wg) costs ~0.67 ms at |F| = 302 (probe; ~0.86 ms in situ), and
+// the inner-solve variant compiled with it (NWT) costs ~0.8 us more per pair update even when no step runs
+// (its SGPR spills), against ~1.6 us per pair update saved: on the 60k headline 16 steps take the pair
+// updates from 9,760 to 4,532 and the fit from 21.4 to 29.9 ms (profiles/newton.md).
 // SVM355_DECOMP_NEWTON=1 turns the step on; SVM355_DECOMP_NEWTON_{FRAC,EVERY,PER_SOLVE,REPEAT,MAX} tune
 // it (A/B runs; both sides read the same variables).
 inline NewtonCfg newton_cfg(const svm_params& p) {
