@@ -181,6 +181,7 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
   int64_t origin = 0, unshrinks = 0, passes = 0, min_active = nloc, n_active = nloc;
 
   int64_t outer = 0, inner_total = 0, changed_total = 0, last_inner_it = 0, newton_steps = 0;
+  int64_t chain_it = 0;  // inner-solve loop iterations (each one or more pair updates)
   int last_m = 0;
   NewtonCfg nwc = newton_cfg(p);
   nwc.on = nwc.on && inner_wss == 3;  // the device polishes in its default inner solve (second order + second pair)
@@ -465,6 +466,7 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
           ++it;
         }
       }
+      ++chain_it;
       since = moved_status ? 0 : since + 1;
     }
     // ---- moved columns (ascending position = ascending id), alpha written back
@@ -536,6 +538,7 @@ int decomp_solve(const double* K, int64_t ldk, const int32_t* y, int64_t n, doub
     stats[10] = min_active;
     stats[11] = 0;
     stats[12] = newton_steps;
+    stats[13] = chain_it;
   }
   if (res) {
     res->iterations = inner_total + 1;

@@ -102,7 +102,8 @@ def decomp_train_gram(K: np.ndarray, y: np.ndarray, params: SVMParams, alpha: Op
 
 def _decomp_stats(st) -> dict:
     return {"outer_iterations": int(st[0]), "inner_iterations": int(st[1]), "working_set": int(st[2]),
-            "solve_us": int(st[3]), "update_columns": int(st[4]), **N.shrink_stats(st)}
+            "solve_us": int(st[3]), "update_columns": int(st[4]), "chain_iterations": int(st[13]),
+            **N.shrink_stats(st)}
 
 
 def decomp_train_gram_dist(K: np.ndarray, y: np.ndarray, params: SVMParams, world: int = 1, comm=None,
